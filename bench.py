@@ -1,0 +1,202 @@
+#!/usr/bin/env python3
+"""Headline benchmark: ray-bounces/s on models/room.stl (BASELINE.json configs[1], "K2").
+
+One step = one pass of the hot path over one synthetic isotropic burst of 1M rays per GPU:
+  rt_trace   (trace_paths_kernel, kernel.py:38-98: ray generation, 3 bounces of closest hit vs
+              receiver + environment, reflect, full reference output contract: traced_paths,
+              received_paths, row_mask -- tracer.py:70-72)
+  rt_compact + rt_cir (tracer.py:87-117: received rows -> delay bins -> impulse response)
+  RCCL all-reduce of the impulse response (N > 1: the job's CIR is the sum over ray shards).
+Rays are sharded by global ray id (rank r traces ids [r*N, (r+1)*N)): per-GPU work is fixed as
+GPUs are added ("weak").  Inputs (mesh tables) are resident in HBM before the timed region.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL)
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "ray-bounces/sec on room.stl (1 GPU) + coverage cells/sec at 1/2/4/8 GPUs"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--rays", type=int, default=1_000_000, help="rays per GPU per step (K2: 1M)")
+    ap.add_argument("--bounces", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="rays per CPU-baseline chunk (~10 s total)")
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_k2.json"),
+                    help="per-launch HBM bytes measured by rocprofv3 PMC (profiles/)")
+    return ap.parse_args()
+
+
+def cpu_baseline(sample_rays, B, tx, rx, min_s=10.0, max_rays=400_000_000):
+    """The oracle (C restatement of kernel.py + tracer.py host tail) on the host cores."""
+    from oracle import oracle as orc
+    from rf_ray_tracing_warp_amd.mesh import load_stl, sphere
+
+    env = load_stl(os.path.join(REPO, "models", "room.stl"))
+    rxm = sphere(rx, 0.1, 1)
+    E, R = orc.Mesh(env.vertices, env.faces), orc.Mesh(rxm.vertices, rxm.faces)
+    threads = min(16, os.cpu_count() or 1)
+    orc.trace(E, R, tx, B, 0, 2000, nthreads=threads)  # warm
+    # bounded sample: consecutive chunks of the same burst (ray ids 0, 1, 2, ...) until ~min_s of CPU work
+    t0 = time.perf_counter()
+    done = 0
+    while True:
+        o = orc.trace(E, R, tx, B, done, sample_rays, want_traced=True, nthreads=threads)
+        paths = orc.clean_paths(o["received"], o["mask"])
+        orc.cir_from_paths(paths, 1, sample_rays, 2.998e8, 100e9, 100e-9)
+        done += sample_rays
+        dt = time.perf_counter() - t0
+        if dt >= min_s or done >= max_rays:
+            break
+    return {"value": done * B / dt, "unit": "ray-bounces/s", "cores": threads, "kind": "port",
+            "sample": f"{done} rays x {B} bounces (ray ids 0..{done - 1}, chunks of {sample_rays}) of the K2 "
+                      f"room.stl burst: trace + host CIR by oracle/rt_oracle.c (OpenMP, {threads} threads), "
+                      f"{dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = f"cuda:{local}"
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        dist.init_process_group("nccl", device_id=torch.device(dev))
+
+    from rf_ray_tracing_warp_amd import _lib
+    from rf_ray_tracing_warp_amd._lib import DeviceMesh, check, lib, ptr
+    from rf_ray_tracing_warp_amd.mesh import load_stl, sphere
+    from rf_ray_tracing_warp_amd.tracer import cir_flags
+
+    N, B = args.rays, args.bounces
+    P = B + 1
+    tx, rx, r_rx = (10.0, 0.0, 5.0), (-10.0, 0.0, 5.0), 0.1  # main.py:29-31 (room scene)
+    c, fs, win, tx_power = 2.998e8, 100e9, 100e-9, 1
+    n_bins = int(win * fs)
+    env_m = load_stl(os.path.join(REPO, "models", "room.stl"))
+    env = DeviceMesh(env_m.vertices, env_m.faces, local)
+    rxm = sphere(rx, r_rx, 1)
+    rxd = DeviceMesh(rxm.vertices, rxm.faces, local)
+    tx32 = np.asarray(tx, np.float32)
+
+    traced = torch.empty((N, P, 3), dtype=torch.float32, device=dev)
+    received = torch.empty((N, P, 3), dtype=torch.float32, device=dev)
+    mask = torch.empty(N, dtype=torch.int32, device=dev)
+    index = torch.empty(N, dtype=torch.int64, device=dev)
+    count = torch.empty(1, dtype=torch.int64, device=dev)
+    ws = torch.empty(int(lib().rt_compact_workspace_bytes(N)), dtype=torch.uint8, device=dev)
+    ir = torch.zeros(n_bins, dtype=torch.float64, device=dev)
+    amp0 = tx_power / (N * world)
+    ray_offset = rank * N
+    flags = cir_flags(c, fs)
+    L = lib()
+    stream = torch.cuda.current_stream()
+    sh = stream.cuda_stream
+    ev = []
+
+    def step(timed):
+        ir.zero_()
+        if timed:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+        check(L.rt_trace(env.handle, tx32.ctypes.data, rxd.handle, B, ray_offset, N, ptr(traced), ptr(received),
+                         ptr(mask), None, None, sh), "rt_trace")
+        if timed:
+            e1.record(stream)
+            ev.append((e0, e1))
+        check(L.rt_compact(ptr(mask), N, ptr(ws), ws.numel(), ptr(index), ptr(count), sh), "rt_compact")
+        check(L.rt_cir(ptr(received), ptr(index), ptr(count), N, B, amp0, c, fs, flags, n_bins, ptr(ir), None, None,
+                       sh), "rt_cir")
+        if world > 1:
+            dist.all_reduce(ir)
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+    received_rows = int(count.item())
+
+    if rank == 0:
+        bounces = world * N * B * args.steps
+        value = bounces / elapsed
+        bytes_per_launch = N * (24 * P + 4)  # traced + received rows + row_mask
+        achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+        traffic = None
+        try:
+            with open(args.traffic_json) as fh:
+                tj = json.load(fh)
+            if tj.get("rays") == N and tj.get("bounces") == B:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            pass
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "ray-bounces/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "models/room.stl (reference mesh) + synthetic isotropic burst (PCG ray ids, kernel.py:51-52)",
+            "config": {"workload": "K2: room.stl, 1 TX (10,0,5), RX (-10,0,5) r=0.1, 1M rays/GPU, 3 bounces, "
+                                   "traced+received+row_mask + CIR (10000 bins)",
+                       "rays_per_gpu": N, "bounces": B, "rays_total": N * world,
+                       "parallelism": f"ray-id shards x{world}, RCCL all-reduce of the CIR"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "k_trace_bf<3>", "kernel_ms": kern_ms,
+                         "algorithmic_bytes_per_launch": bytes_per_launch},
+            "received_rows_last_step": received_rows,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_sample, B, tx, rx)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,84 @@
+/*
+ * rfrt.h -- C ABI of librfrt.so, the MI355X-native replacement for the Warp hot path of
+ * rmenon1008/rf_ray_tracing_warp.  Plain pointers and sizes only; every device pointer is
+ * caller-owned (e.g. a PyTorch tensor's data_ptr()) and every launch is asynchronous on the
+ * caller's hipStream_t (pass NULL for the default stream).
+ *
+ * Error convention: functions return RT_OK (0) or a negative code; rt_last_error() gives the
+ * message of the last failure on the calling thread.  Nothing throws across the ABI.
+ * Threading: mesh create/destroy are not thread-safe for the same handle; launches are
+ * reentrant.  Reference paths below are relative to the reference repository root.
+ */
+#ifndef RFRT_H
+#define RFRT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RFRT_VERSION 1
+
+#define RT_OK 0
+#define RT_EINVAL (-1) /* bad argument: Warp raises a Python exception at launch (tracer.py:75) */
+#define RT_EHIP (-2)   /* HIP runtime error */
+
+/* rt_cir flags: NumPy 2 / NEP 50 promotes tracer.py:115 to float64 when light_speed_mps or
+ * sample_rate_hz is a NumPy float64 scalar instead of a Python float. */
+#define RT_CIR_C_F64 1
+#define RT_CIR_FS_F64 2
+
+typedef struct rt_mesh rt_mesh;
+
+const char* rt_last_error(void);
+int rt_version(void);
+
+/* Replaces wp.Mesh(points=wp.array(vertices, vec3), velocities=None, indices=wp.array(faces.flatten(),
+ * int32)) -- tracer.py:22-24 (environment) and tracer.py:28-30 (receiver sphere).
+ * vertices: host float32 (nv,3); faces: host int32 (nf,3).  Builds the device tables (and a BVH
+ * for large meshes) on `device`; the library owns the handle. */
+int rt_mesh_create(int device, const float* vertices, int64_t nv, const int32_t* faces, int64_t nf, rt_mesh** out);
+/* Replaces the wp.Mesh destructor (freed on Python GC in the reference). */
+int rt_mesh_destroy(rt_mesh* mesh);
+/* nf, bounds6 = (lo xyz, hi xyz), sphere4 = conservative bounding sphere (centre, radius). Any may be NULL. */
+int rt_mesh_info(const rt_mesh* mesh, int64_t* nf, float* bounds6, float* sphere4);
+
+/* Replaces wp.launch(kernel.trace_paths_kernel, dim=(n,1,1), inputs=[env.id, tx_pos, rx.id,
+ * max_bounces, traced_paths, received_paths, row_mask]) -- tracer.py:75-79, kernel.py:38-98.
+ * Traces global ray ids [ray_offset, ray_offset+n) (ray id = Warp tid; sharding keeps ids global).
+ * Device outputs, each optional (NULL), rows are ray - ray_offset:
+ *   traced   (n, B+1, 3) f32  kernel.py:55,88,95, NaN where the reference keeps its host NaN fill
+ *   received (n, B+1, 3) f32  kernel.py:89-90, longest prefix ending at the last RX hit, NaN after
+ *   row_mask (n) u32          kernel.py:91
+ *   hit_kind (n, B) i32       per bounce 0 miss / 1 env / 2 receiver   (diagnostic, not in reference)
+ *   hit_face (n, B) i32       per bounce face id of the chosen hit, -1 on miss (diagnostic)
+ * rx may be NULL (no receiver).  max_bounces > 8 requires `traced` (it holds the path). */
+int rt_trace(const rt_mesh* env, const float* tx_pos, const rt_mesh* rx, int max_bounces, int64_t ray_offset,
+             int64_t n, float* traced, float* received, uint32_t* row_mask, int32_t* hit_kind, int32_t* hit_face,
+             void* stream);
+
+/* Replaces tracer.py:87 (paths[row_mask != 0]): ids of the set rows in ray order, count on device.
+ * workspace: device scratch of rt_compact_workspace_bytes(n) bytes. */
+int64_t rt_compact_workspace_bytes(int64_t n);
+int rt_compact(const uint32_t* row_mask, int64_t n, void* workspace, int64_t workspace_bytes, int64_t* out_index,
+               int64_t* out_count, void* stream);
+
+/* Replaces tracer.py:90-117 (NaN strip, _bounce_amplitude product, float32 delay, IR accumulate).
+ * received: (n, B+1, 3) device rows; index/count: output of rt_compact; max_count: host upper bound
+ * of *count (grid size).  amp0 = tx_power / tx_num_rays (tracer.py:103).  impulse_response (n_bins) f64
+ * is accumulated into (+=); out_bin / out_amp (max_count) optional per-path diagnostics. */
+int rt_cir(const float* received, const int64_t* index, const int64_t* count, int64_t max_count, int max_bounces,
+           double amp0, double light_speed, double sample_rate, int flags, int64_t n_bins, double* impulse_response,
+           int32_t* out_bin, double* out_amp, void* stream);
+
+/* Self-test entry points used by the parity tests (not part of the reference surface). */
+int rt_selftest_math(const float* x, int64_t n, float* out, int op, void* stream);
+int rt_ray_dirs(int64_t ray_offset, int64_t n, float* out, void* stream);
+int rt_query(const rt_mesh* mesh, const float* origins, const float* dirs, int64_t n, float* t, int32_t* face,
+             void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RFRT_H */

@@ -43,6 +43,9 @@ def lib():
         L.orc_mesh_destroy.argtypes = [ctypes.c_void_p]
         L.orc_trace.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _f32p, ctypes.c_int, ctypes.c_int64,
                                 ctypes.c_int64, _f32p, _f32p, _u32p, _i32p, _i32p, ctypes.c_int]
+        L.orc_trace_ids.argtypes = [ctypes.c_void_p, ctypes.c_void_p, _f32p, ctypes.c_int, ctypes.c_int64,
+                                    ctypes.POINTER(ctypes.c_int64), ctypes.c_int64, _f32p, _f32p, _u32p, _i32p, _i32p,
+                                    ctypes.c_int]
         L.orc_ray_dirs.argtypes = [ctypes.c_int64, ctypes.c_int64, _f32p]
         L.orc_sincosf_bulk.argtypes = [_f32p, ctypes.c_int64, _f32p, _f32p]
         L.orc_acosf_bulk.argtypes = [_f32p, ctypes.c_int64, _f32p]
@@ -100,6 +103,26 @@ def trace(env: Mesh, rx: Mesh, tx, B, ray_offset, n, want_traced=True, nthreads=
     lib().orc_trace(env.h, rx.h, _p(tx, _f32p), B, ray_offset, n, _p(out["traced"], _f32p),
                     _p(out["received"], _f32p), _p(out["mask"], _u32p), _p(out["hit_kind"], _i32p),
                     _p(out["hit_face"], _i32p), int(nthreads))
+    return out
+
+
+def trace_ids(env: Mesh, rx: Mesh, tx, B, ids, want_traced=True, nthreads=None):
+    """trace() for an explicit list of ray ids (rows follow ``ids``)."""
+    ids = np.ascontiguousarray(ids, dtype=np.int64)
+    n, P = len(ids), B + 1
+    tx = np.ascontiguousarray(np.asarray(tx, dtype=np.float64).astype(np.float32))
+    out = {
+        "traced": np.empty((n, P, 3), np.float32) if want_traced else None,
+        "received": np.empty((n, P, 3), np.float32),
+        "mask": np.empty(n, np.uint32),
+        "hit_kind": np.empty((n, B), np.int32),
+        "hit_face": np.empty((n, B), np.int32),
+    }
+    if nthreads is None:
+        nthreads = min(16, os.cpu_count() or 1)
+    lib().orc_trace_ids(env.h, rx.h, _p(tx, _f32p), B, 0, ids.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), n,
+                        _p(out["traced"], _f32p), _p(out["received"], _f32p), _p(out["mask"], _u32p),
+                        _p(out["hit_kind"], _i32p), _p(out["hit_face"], _i32p), int(nthreads))
     return out
 
 

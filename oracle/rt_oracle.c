@@ -269,7 +269,8 @@ int orc_query(const orc_mesh* m, const float* o, const float* d, float max_t, fl
 }
 
 /*
- * trace_paths_kernel restatement (kernel.py:38-98), rays [ray_offset, ray_offset+n).
+ * trace_paths_kernel restatement (kernel.py:38-98), rays [ray_offset, ray_offset+n), or the
+ * explicit ray ids ids[0..n) when ids != NULL.
  * Outputs (row r = ray ray_offset+r), all optional (NULL):
  *   traced   (n, B+1, 3) f32  -- NaN where the reference leaves its host NaN fill
  *   received (n, B+1, 3) f32  -- longest prefix ending at the last RX hit, NaN after
@@ -277,9 +278,9 @@ int orc_query(const orc_mesh* m, const float* o, const float* d, float max_t, fl
  *   hit_kind (n, B) i32       -- per bounce: 0 miss, 1 env, 2 rx   (debug, not in reference)
  *   hit_face (n, B) i32       -- per bounce: face id of the chosen hit, -1 on miss
  */
-void orc_trace(const orc_mesh* env, const orc_mesh* rx, const float* tx, int B, int64_t ray_offset,
-               int64_t n, float* traced, float* received, uint32_t* mask, int32_t* hit_kind,
-               int32_t* hit_face, int nthreads)
+void orc_trace_ids(const orc_mesh* env, const orc_mesh* rx, const float* tx, int B, int64_t ray_offset,
+                   const int64_t* ids, int64_t n, float* traced, float* received, uint32_t* mask,
+                   int32_t* hit_kind, int32_t* hit_face, int nthreads)
 {
     const int P = B + 1;
     const float qnan = nanf("");
@@ -290,7 +291,7 @@ void orc_trace(const orc_mesh* env, const orc_mesh* rx, const float* tx, int B, 
         int last_rx = -1; /* index of last path point written by an RX hit */
         int written = 1;
         float dir[3], pos[3] = {tx[0], tx[1], tx[2]};
-        orc_ray_dir(ray_offset + r, dir);
+        orc_ray_dir(ids ? ids[r] : ray_offset + r, dir);
         memcpy(path[0], pos, 12);
         for (int b = 0; b < B; ++b) {
             float tr = 0, te = 0, nr[3], ne[3];
@@ -337,6 +338,13 @@ void orc_trace(const orc_mesh* env, const orc_mesh* rx, const float* tx, int B, 
         }
         if (mask) mask[r] = last_rx >= 0 ? 1u : 0u;
     }
+}
+
+void orc_trace(const orc_mesh* env, const orc_mesh* rx, const float* tx, int B, int64_t ray_offset,
+               int64_t n, float* traced, float* received, uint32_t* mask, int32_t* hit_kind,
+               int32_t* hit_face, int nthreads)
+{
+    orc_trace_ids(env, rx, tx, B, ray_offset, NULL, n, traced, received, mask, hit_kind, hit_face, nthreads);
 }
 
 /* bulk helpers for tests */

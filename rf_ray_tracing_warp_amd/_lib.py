@@ -1,0 +1,103 @@
+"""ctypes binding of librfrt.so (include/rfrt.h).
+
+There is no fallback: if the library is missing or fails to load, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "librfrt.so")
+
+RT_CIR_C_F64 = 1
+RT_CIR_FS_F64 = 2
+
+_vp = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_int = ctypes.c_int
+_lib = None
+
+
+class RfrtError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load librfrt.so once (raises RfrtError if it is not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RfrtError(f"{LIB_PATH} is not built: run `python -m rf_ray_tracing_warp_amd.build` "
+                        "(the HIP path has no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    L.rt_last_error.restype = ctypes.c_char_p
+    L.rt_version.restype = _int
+    L.rt_mesh_create.argtypes = [_int, _vp, _i64, _vp, _i64, ctypes.POINTER(_vp)]
+    L.rt_mesh_destroy.argtypes = [_vp]
+    L.rt_mesh_info.argtypes = [_vp, _vp, _vp, _vp]
+    L.rt_trace.argtypes = [_vp, _vp, _vp, _int, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp]
+    L.rt_compact_workspace_bytes.restype = _i64
+    L.rt_compact_workspace_bytes.argtypes = [_i64]
+    L.rt_compact.argtypes = [_vp, _i64, _vp, _i64, _vp, _vp, _vp]
+    L.rt_cir.argtypes = [_vp, _vp, _vp, _i64, _int, ctypes.c_double, ctypes.c_double, ctypes.c_double, _int, _i64,
+                         _vp, _vp, _vp, _vp]
+    L.rt_selftest_math.argtypes = [_vp, _i64, _vp, _int, _vp]
+    L.rt_ray_dirs.argtypes = [_i64, _i64, _vp, _vp]
+    L.rt_query.argtypes = [_vp, _vp, _vp, _i64, _vp, _vp, _vp]
+    for name in ("rt_mesh_create", "rt_mesh_destroy", "rt_mesh_info", "rt_trace", "rt_compact", "rt_cir",
+                 "rt_selftest_math", "rt_ray_dirs", "rt_query"):
+        getattr(L, name).restype = _int
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = lib().rt_last_error().decode(errors="replace")
+        raise RfrtError(f"{what or 'librfrt'} failed ({rc}): {msg}")
+
+
+def ptr(t) -> int | None:
+    """data_ptr() of a torch tensor (None -> NULL)."""
+    return None if t is None else t.data_ptr()
+
+
+def stream_handle(device) -> int:
+    import torch
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+class DeviceMesh:
+    """A triangle mesh resident on one GPU (the wp.Mesh of tracer.py:24,30)."""
+
+    def __init__(self, vertices, faces, device: int = 0):
+        v = np.ascontiguousarray(np.asarray(vertices, dtype=np.float64).astype(np.float32)).reshape(-1, 3)
+        f = np.ascontiguousarray(np.asarray(faces).astype(np.int32)).reshape(-1, 3)
+        self.device = int(device)
+        self.num_faces = len(f)
+        self._h = _vp()
+        check(lib().rt_mesh_create(self.device, v.ctypes.data, len(v), f.ctypes.data, len(f), ctypes.byref(self._h)),
+              "rt_mesh_create")
+
+    @property
+    def handle(self):
+        return self._h
+
+    def info(self):
+        nf = ctypes.c_int64()
+        b = np.zeros(6, np.float32)
+        s = np.zeros(4, np.float32)
+        check(lib().rt_mesh_info(self._h, ctypes.byref(nf), b.ctypes.data, s.ctypes.data), "rt_mesh_info")
+        return int(nf.value), b, s
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value and _lib is not None:
+            _lib.rt_mesh_destroy(self._h)
+            self._h = _vp()
+
+    def __del__(self):
+        self.close()

@@ -1,0 +1,210 @@
+// cir.hip -- the host tail of Tracer.compute_cir (tracer.py:84-117) on the device.
+//
+//   rt_compact : row_mask -> ray ids of received rows in ray-id order (tracer.py:87)
+//                3 kernels: per-tile counts, one-block exclusive scan, ordered scatter.
+//   rt_cir     : per received row, the NaN strip (tracer.py:90-97), Fresnel product over the
+//                interior vertices (tracer.py:106-111, _bounce_amplitude :34-61), float32 path
+//                length and delay bin (tracer.py:112-115, NumPy 2 / NEP 50 semantics), then
+//                impulse_response[bin] += amplitude (tracer.py:116-117).
+//
+// Exactness: the bin is computed with the reference's exact float32 operation sequence
+// (np.dot on float32 = f32-rounded products summed in double, rounded once; norm = sqrtf of
+// it), so bins match bit for bit.  The amplitude uses double acos/sin/asin/cos where the
+// reference uses NumPy's float32 arccos and Python's math: agreement ~1e-7 relative.
+// Accumulation uses a double atomic add (order differs from the host loop at ~1e-16).
+#include <math.h>
+
+#include "../../include/rfrt.h"
+#include "rt_internal.h"
+
+namespace {
+
+constexpr int TILE = 2048;  // flags per compaction tile (256 threads x 8)
+
+__global__ __launch_bounds__(256) void k_count(const uint32_t* mask, int64_t n, int64_t* tile_count) {
+  __shared__ int wsum[4];
+  const int64_t base = (int64_t)blockIdx.x * TILE;
+  int c = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int64_t i = base + k * 256 + threadIdx.x;
+    c += (i < n && mask[i] != 0u) ? 1 : 0;
+  }
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) tile_count[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+
+__global__ __launch_bounds__(1024) void k_scan(int64_t* tile_count, int64_t ntiles, int64_t* total) {
+  // single block exclusive scan, in place, chunks of 1024
+  __shared__ int64_t buf[1024];
+  __shared__ int64_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int64_t base = 0; base < ntiles; base += 1024) {
+    const int64_t i = base + threadIdx.x;
+    const int64_t v = i < ntiles ? tile_count[i] : 0;
+    buf[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+      const int64_t add = threadIdx.x >= (unsigned)o ? buf[threadIdx.x - o] : 0;
+      __syncthreads();
+      buf[threadIdx.x] += add;
+      __syncthreads();
+    }
+    if (i < ntiles) tile_count[i] = carry + buf[threadIdx.x] - v;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry += buf[1023];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *total = carry;
+}
+
+__global__ __launch_bounds__(256) void k_scatter(const uint32_t* mask, int64_t n, const int64_t* tile_off,
+                                                 int64_t* out_index) {
+  __shared__ int wbase[4];
+  const int64_t base = (int64_t)blockIdx.x * TILE;
+  int64_t run = tile_off[blockIdx.x];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int k = 0; k < 8; ++k) {
+    const int64_t i = base + k * 256 + threadIdx.x;
+    const bool f = i < n && mask[i] != 0u;
+    const unsigned long long bal = __ballot(f);
+    const int wc = __popcll(bal);
+    if (lane == 0) wbase[w] = wc;
+    __syncthreads();
+    int before = 0;
+    for (int j = 0; j < w; ++j) before += wbase[j];
+    const int total = wbase[0] + wbase[1] + wbase[2] + wbase[3];
+    const int rank = __popcll(bal & ((1ull << lane) - 1ull));
+    if (f) out_index[run + before + rank] = i;
+    run += total;
+    __syncthreads();
+  }
+}
+
+// np.dot(float32[3], float32[3]): f32 products, summed in double left to right, rounded once
+__device__ __forceinline__ float npdot(const float* a, const float* b) {
+  const float p0 = a[0] * b[0], p1 = a[1] * b[1], p2 = a[2] * b[2];
+  return (float)(((double)p0 + (double)p1) + (double)p2);
+}
+__device__ __forceinline__ float npnorm(const float* a) { return sqrtf(npdot(a, a)); }
+
+// Tracer._bounce_amplitude (tracer.py:34-61) for a float32 angle
+__device__ __forceinline__ double bounce_amplitude(float angle) {
+  if (isnan(angle)) return 0.0;
+  const float theta32 = 1.57079637050628662109375f - angle / 2.0f;  // f32(pi/2) - angle/2 in f32
+  const double theta = (double)theta32;
+  const double theta_i = asin(sin(theta) / 5.0);
+  const double num = cos(theta_i) - 5.0 * cos(theta);
+  const double den = cos(theta_i) + 5.0 * cos(theta);
+  const double q = num / den;
+  double amp = -(q * q);
+  if (amp < -1.0) amp = -1.0;
+  if (isnan(amp)) return 0.0;
+  return -amp;
+}
+
+__device__ void cir_one(const float* received, const int64_t* index, int64_t k, int P, double amp0, float c32,
+                        float fs32, double c64, double fs64, int flags, int64_t n_bins, double* ir, int32_t* out_bin,
+                        double* out_amp);
+
+__global__ __launch_bounds__(256) void k_cir(const float* received, const int64_t* index, const int64_t* count,
+                                             int P, double amp0, float c32, float fs32, double c64, double fs64,
+                                             int flags, int64_t n_bins, double* ir, int32_t* out_bin,
+                                             double* out_amp) {
+  const int64_t cnt = *count;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < cnt; k += (int64_t)gridDim.x * blockDim.x)
+    cir_one(received, index, k, P, amp0, c32, fs32, c64, fs64, flags, n_bins, ir, out_bin, out_amp);
+}
+
+__device__ void cir_one(const float* received, const int64_t* index, int64_t k, int P, double amp0, float c32,
+                        float fs32, double c64, double fs64, int flags, int64_t n_bins, double* ir, int32_t* out_bin,
+                        double* out_amp) {
+  const float* row = received + index[k] * (int64_t)(P * 3);
+  // tracer.py:90-97: cut at the first point with a NaN component
+  int L = 0;
+  while (L < P && !(isnan(row[3 * L]) || isnan(row[3 * L + 1]) || isnan(row[3 * L + 2]))) ++L;
+  double amp = amp0;
+  float dist = 0.0f;
+  for (int j = 0; j + 2 < L; ++j) {
+    const float* p1 = row + 3 * j;
+    const float* p2 = p1 + 3;
+    const float* p3 = p2 + 3;
+    const float s1[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+    const float s2[3] = {p3[0] - p2[0], p3[1] - p2[1], p3[2] - p2[2]};
+    const float l1 = npnorm(s1);
+    const float cosv = npdot(s1, s2) / (l1 * npnorm(s2));
+    const float angle = (float)acos((double)cosv);
+    amp *= bounce_amplitude(angle);
+    dist += l1;
+  }
+  if (L >= 2) {
+    const float* a = row + 3 * (L - 2);
+    const float d[3] = {a[0] - a[3], a[1] - a[4], a[2] - a[5]};
+    dist += npnorm(d);
+  }
+  // delay_samples = int((distance / light_speed_mps) * sample_rate_hz)   (tracer.py:115)
+  double dl;
+  if (flags & RT_CIR_C_F64) {
+    const double q = (double)dist / c64;
+    dl = q * fs64;
+  } else {
+    const float q = dist / c32;
+    dl = (flags & RT_CIR_FS_F64) ? (double)q * fs64 : (double)(q * fs32);
+  }
+  const int64_t bin = (int64_t)dl;  // int() truncates toward zero
+  if (out_bin) out_bin[k] = (int32_t)(bin < 2147483647 ? bin : 2147483647);
+  if (out_amp) out_amp[k] = amp;
+  if (ir && bin < n_bins) atomicAdd(ir + bin, amp);
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t rt_compact_workspace_bytes(int64_t n) { return (int64_t)(((n + TILE - 1) / TILE) + 1) * 8; }
+
+int rt_compact(const uint32_t* row_mask, int64_t n, void* workspace, int64_t workspace_bytes, int64_t* out_index,
+               int64_t* out_count, void* stream) {
+  if (n < 0 || !out_count || (n > 0 && (!row_mask || !out_index || !workspace))) {
+    rt::set_error("rt_compact: invalid arguments");
+    return RT_EINVAL;
+  }
+  const int64_t ntiles = (n + TILE - 1) / TILE;
+  if (workspace_bytes < rt_compact_workspace_bytes(n)) {
+    rt::set_error("rt_compact: workspace too small");
+    return RT_EINVAL;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  if (n == 0) {
+    RT_HIP(hipMemsetAsync(out_count, 0, 8, s));
+    return RT_OK;
+  }
+  int64_t* tiles = (int64_t*)workspace;
+  hipLaunchKernelGGL(k_count, dim3((unsigned)ntiles), dim3(256), 0, s, row_mask, n, tiles);
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, tiles, ntiles, out_count);
+  hipLaunchKernelGGL(k_scatter, dim3((unsigned)ntiles), dim3(256), 0, s, row_mask, n, tiles, out_index);
+  RT_HIP(hipGetLastError());
+  return RT_OK;
+}
+
+int rt_cir(const float* received, const int64_t* index, const int64_t* count, int64_t max_count, int max_bounces,
+           double amp0, double light_speed, double sample_rate, int flags, int64_t n_bins, double* impulse_response,
+           int32_t* out_bin, double* out_amp, void* stream) {
+  if (!received || !index || !count || max_count < 0 || max_bounces < 1 || n_bins < 0) {
+    rt::set_error("rt_cir: invalid arguments");
+    return RT_EINVAL;
+  }
+  if (max_count == 0) return RT_OK;
+  const int64_t want = (max_count + 255) / 256;
+  const unsigned grid = (unsigned)(want < 1024 ? want : 1024);
+  hipLaunchKernelGGL(k_cir, dim3(grid), dim3(256), 0, (hipStream_t)stream, received, index, count, max_bounces + 1,
+                     amp0, (float)light_speed, (float)sample_rate, light_speed, sample_rate, flags, n_bins,
+                     impulse_response, out_bin, out_amp);
+  RT_HIP(hipGetLastError());
+  return RT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,43 @@
+// rt_internal.h -- host-side structures shared by the librfrt translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+// Device-resident triangle mesh (the object wp.Mesh is in the reference, tracer.py:24,30).
+//
+// HBM layout (all float4, 16-byte aligned):
+//   perm  [nf][6][3]  corners of face f permuted for shear case kz*2+swap, packed
+//                     (p0 p1 p2 q0)(q1 q2 r0 r1)(r2 0 0 0) with 0/1/2 = [kx]/[ky]/[kz]
+//                     -- 288 B per face, read as 2x ds_read_b128 + ds_read_b32
+//   nrm   [nf]        unit geometric normal normalize(cross(q-p, r-p)), w = 0
+//   bvh nodes (optional, large meshes): see bvh.h
+struct rt_mesh {
+  int device = 0;
+  int64_t nf = 0;
+  float4* perm = nullptr;
+  float4* nrm = nullptr;
+  // bounding sphere (centre, conservative radius) and box, computed on the host in double
+  float center[3] = {0, 0, 0};
+  float radius = 0.0f;
+  float lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
+  // BVH (built when nf > RT_BRUTE_MAX_FACES)
+  float4* nodes = nullptr;  // [nnodes][4]: child0 box lo/hi, child1 box lo/hi packed, see bvh.h
+  int32_t* leaf_faces = nullptr;
+  int64_t nnodes = 0;
+};
+
+namespace rt {
+void set_error(const std::string& msg);
+int hip_fail(hipError_t e, const char* what);
+}  // namespace rt
+
+#define RT_HIP(call)                                                   \
+  do {                                                                 \
+    hipError_t _e = (call);                                            \
+    if (_e != hipSuccess) return rt::hip_fail(_e, #call);              \
+  } while (0)
+
+// faces at or below this count are traced by the brute-force LDS kernel (whole mesh in LDS)
+#define RT_BRUTE_MAX_FACES 192

@@ -1,0 +1,285 @@
+// trace.hip -- trace_paths_kernel (kernel.py:38-98) as CDNA4 HIP.
+//
+// One lane = one ray (global ray id = ray_offset + row).  The whole bounce loop runs in
+// registers: position, direction and the P = B+1 path points never leave VGPRs until the
+// final row stores.  The environment mesh is staged once per workgroup into LDS as the
+// host-built permuted-corner table (288 B/face), so every lane reads its shear case with a
+// conflict-free ds_read_b128 (6 cases = 6 distinct 16-B slots per face).  The receiver mesh
+// (80 faces for the reference's icosphere) stays in HBM/L2: a conservative bounding-sphere
+// test keeps nearly every wave from touching it.
+//
+// Semantics kept from the reference: no early exit (Q1: a miss repeats
+// forever, so it is skipped, which changes nothing), an RX hit does not stop the ray (Q2),
+// no t_min (Q3), no renormalisation after reflect (Q4), traced_paths is scratch (Q6).
+#include <math.h>
+
+#include "rt_device.h"
+#include "rt_internal.h"
+
+namespace {
+
+struct TraceArgs {
+  const float4* env_perm;
+  const float4* env_nrm;
+  int env_nf;
+  const float4* rx_perm;
+  int rx_nf;
+  float rx_c[3];
+  float rx_r2;  // conservative squared radius of the receiver's bounding sphere
+  float tx[3];
+  int64_t ray_offset;
+  int64_t n;
+  float* traced;    // (n, P, 3) or null
+  float* received;  // (n, P, 3) or null
+  uint32_t* mask;   // (n) or null
+  int32_t* hit_kind;  // (n, B) or null
+  int32_t* hit_face;  // (n, B) or null
+};
+
+// Closest hit over a brute-force face list whose permuted table lives at `tab`
+// (LDS for the environment, global for the receiver).
+template <typename Ptr>
+__device__ __forceinline__ rt::Hit query_faces(Ptr tab, int nf, const rt::Shear& s) {
+  rt::Hit h;
+  rt::hit_init(h);
+  const int off = s.kcase * 3;
+  for (int f = 0; f < nf; ++f) {
+    const float4 q0 = tab[f * 18 + off + 0];
+    const float4 q1 = tab[f * 18 + off + 1];
+    const float c2 = tab[f * 18 + off + 2].x;
+    float T, det;
+    if (rt::tri_test(s, q0, q1, c2, T, det)) rt::hit_consider(h, T, det, f);
+  }
+  return h;
+}
+
+// Can a receiver hit possibly be nearer than t_limit?  Conservative: the receiver's faces all
+// lie inside the ball (centre c, squared radius r2 padded on the host).
+__device__ __forceinline__ bool rx_maybe(const TraceArgs& a, float3 o, float3 d, float t_limit) {
+  const float ox = o.x - a.rx_c[0], oy = o.y - a.rx_c[1], oz = o.z - a.rx_c[2];
+  const float cc = ox * ox + oy * oy + oz * oz - a.rx_r2;
+  if (cc <= 0.0f) return true;  // origin inside the ball
+  const float b = ox * d.x + oy * d.y + oz * d.z;
+  if (b >= 0.0f) return false;  // ball behind the origin
+  const float dd = d.x * d.x + d.y * d.y + d.z * d.z;
+  const float disc = b * b - dd * cc;
+  if (disc < 0.0f) return false;
+  const float t_enter = (-b - sqrtf(disc)) / dd;
+  return t_enter <= t_limit * 1.0001f + 1e-4f;
+}
+
+__device__ __forceinline__ void store_row(float* dst, const float (*pts)[3], int P) {
+  // rows are 12*P bytes; use 16-byte stores whenever the row start allows it
+  for (int i = 0; i < P; ++i) {
+    dst[3 * i + 0] = pts[i][0];
+    dst[3 * i + 1] = pts[i][1];
+    dst[3 * i + 2] = pts[i][2];
+  }
+}
+
+template <int B>
+__global__ __launch_bounds__(256) void k_trace_bf(TraceArgs a) {
+  constexpr int P = B + 1;
+  extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
+  // stage the environment table (coalesced float4 copy)
+  const int nvec = a.env_nf * 18;
+  for (int i = threadIdx.x; i < nvec; i += blockDim.x) lds_tab[i] = a.env_perm[i];
+  __syncthreads();
+
+  const float qnan = __builtin_nanf("");
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; row < a.n; row += stride) {
+    const int64_t gid = a.ray_offset + row;
+    float3 dir = rt::ray_dir(gid);
+    float3 pos = make_float3(a.tx[0], a.tx[1], a.tx[2]);
+    float path[P][3];
+#pragma unroll
+    for (int i = 0; i < P; ++i) path[i][0] = path[i][1] = path[i][2] = qnan;
+    path[0][0] = pos.x;
+    path[0][1] = pos.y;
+    path[0][2] = pos.z;
+    int last_rx = -1;
+    bool alive = true;
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      int kind = 0, face = -1;
+      if (alive) {
+        const rt::Shear s = rt::make_shear(pos, dir);
+        const rt::Hit he = query_faces(lds_tab, a.env_nf, s);
+        const bool env_hit = he.face >= 0;
+        rt::Hit hr;
+        rt::hit_init(hr);
+        if (a.rx_nf > 0 && rx_maybe(a, pos, dir, env_hit ? he.t : RT_MAX_T))
+          hr = query_faces(a.rx_perm, a.rx_nf, s);
+        const bool rx_hit = hr.face >= 0;
+        if (rx_hit && (!env_hit || he.t > hr.t)) {  // kernel.py:85
+          pos.x = fmaf(dir.x, hr.t, pos.x);
+          pos.y = fmaf(dir.y, hr.t, pos.y);
+          pos.z = fmaf(dir.z, hr.t, pos.z);
+          path[b + 1][0] = pos.x;
+          path[b + 1][1] = pos.y;
+          path[b + 1][2] = pos.z;
+          last_rx = b + 1;
+          kind = 2;
+          face = hr.face;
+        } else if (env_hit) {  // kernel.py:93-96
+          pos.x = fmaf(dir.x, he.t, pos.x);
+          pos.y = fmaf(dir.y, he.t, pos.y);
+          pos.z = fmaf(dir.z, he.t, pos.z);
+          path[b + 1][0] = pos.x;
+          path[b + 1][1] = pos.y;
+          path[b + 1][2] = pos.z;
+          const float4 n4 = a.env_nrm[he.face];
+          const float3 n = make_float3(n4.x, n4.y, n4.z);
+          const float sc = 2.0f * rt::dot3(dir, n);
+          dir.x = fmaf(-sc, n.x, dir.x);
+          dir.y = fmaf(-sc, n.y, dir.y);
+          dir.z = fmaf(-sc, n.z, dir.z);
+          kind = 1;
+          face = he.face;
+        } else {
+          alive = false;  // kernel.py:97-98: every later iteration repeats this miss
+        }
+      }
+      if (a.hit_kind) a.hit_kind[row * B + b] = kind;
+      if (a.hit_face) a.hit_face[row * B + b] = face;
+    }
+    if (a.traced) store_row(a.traced + row * (P * 3), path, P);
+    if (a.received) {
+      float rec[P][3];
+#pragma unroll
+      for (int i = 0; i < P; ++i) {
+        const bool keep = i <= last_rx;
+        rec[i][0] = keep ? path[i][0] : qnan;
+        rec[i][1] = keep ? path[i][1] : qnan;
+        rec[i][2] = keep ? path[i][2] : qnan;
+      }
+      store_row(a.received + row * (P * 3), rec, P);
+    }
+    if (a.mask) a.mask[row] = last_rx >= 0 ? 1u : 0u;
+  }
+}
+
+// Generic fallback for B beyond the register-resident instantiations: the path lives in
+// the output rows themselves (same semantics, slower).
+__global__ __launch_bounds__(256) void k_trace_bf_generic(TraceArgs a, int B) {
+  extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
+  const int nvec = a.env_nf * 18;
+  for (int i = threadIdx.x; i < nvec; i += blockDim.x) lds_tab[i] = a.env_perm[i];
+  __syncthreads();
+  const int P = B + 1;
+  const float qnan = __builtin_nanf("");
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; row < a.n; row += stride) {
+    const int64_t gid = a.ray_offset + row;
+    float3 dir = rt::ray_dir(gid);
+    float3 pos = make_float3(a.tx[0], a.tx[1], a.tx[2]);
+    float* tr = a.traced ? a.traced + row * (int64_t)(P * 3) : nullptr;
+    float* rc = a.received ? a.received + row * (int64_t)(P * 3) : nullptr;
+    for (int i = 0; i < 3 * P; ++i) {
+      if (tr) tr[i] = qnan;
+      if (rc) rc[i] = qnan;
+    }
+    if (tr) { tr[0] = pos.x; tr[1] = pos.y; tr[2] = pos.z; }
+    int last_rx = -1;
+    bool alive = true;
+    for (int b = 0; b < B; ++b) {
+      int kind = 0, face = -1;
+      if (alive) {
+        const rt::Shear s = rt::make_shear(pos, dir);
+        const rt::Hit he = query_faces(lds_tab, a.env_nf, s);
+        const bool env_hit = he.face >= 0;
+        rt::Hit hr;
+        rt::hit_init(hr);
+        if (a.rx_nf > 0 && rx_maybe(a, pos, dir, env_hit ? he.t : RT_MAX_T))
+          hr = query_faces(a.rx_perm, a.rx_nf, s);
+        const bool rx_hit = hr.face >= 0;
+        if (rx_hit && (!env_hit || he.t > hr.t)) {
+          pos.x = fmaf(dir.x, hr.t, pos.x);
+          pos.y = fmaf(dir.y, hr.t, pos.y);
+          pos.z = fmaf(dir.z, hr.t, pos.z);
+          if (tr) { tr[3 * (b + 1)] = pos.x; tr[3 * (b + 1) + 1] = pos.y; tr[3 * (b + 1) + 2] = pos.z; }
+          last_rx = b + 1;
+          kind = 2;
+          face = hr.face;
+        } else if (env_hit) {
+          pos.x = fmaf(dir.x, he.t, pos.x);
+          pos.y = fmaf(dir.y, he.t, pos.y);
+          pos.z = fmaf(dir.z, he.t, pos.z);
+          if (tr) { tr[3 * (b + 1)] = pos.x; tr[3 * (b + 1) + 1] = pos.y; tr[3 * (b + 1) + 2] = pos.z; }
+          const float4 n4 = a.env_nrm[he.face];
+          const float3 n = make_float3(n4.x, n4.y, n4.z);
+          const float sc = 2.0f * rt::dot3(dir, n);
+          dir.x = fmaf(-sc, n.x, dir.x);
+          dir.y = fmaf(-sc, n.y, dir.y);
+          dir.z = fmaf(-sc, n.z, dir.z);
+          kind = 1;
+          face = he.face;
+        } else {
+          alive = false;
+        }
+        if (kind == 2 && rc) {  // kernel.py:89-90: copy the traced prefix
+          if (tr) {
+            for (int i = 0; i < 3 * (b + 2); ++i) rc[i] = tr[i];
+          }
+        }
+      }
+      if (a.hit_kind) a.hit_kind[row * B + b] = kind;
+      if (a.hit_face) a.hit_face[row * B + b] = face;
+    }
+    if (a.mask) a.mask[row] = last_rx >= 0 ? 1u : 0u;
+  }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ launch (C++ side of rt_trace)
+namespace rt {
+
+int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B, int64_t ray_offset, int64_t n,
+                 float* traced, float* received, uint32_t* mask, int32_t* hit_kind, int32_t* hit_face,
+                 hipStream_t stream) {
+  if (n == 0) return 0;
+  TraceArgs a;
+  a.env_perm = env->perm;
+  a.env_nrm = env->nrm;
+  a.env_nf = (int)env->nf;
+  a.rx_perm = rx ? rx->perm : nullptr;
+  a.rx_nf = rx ? (int)rx->nf : 0;
+  for (int k = 0; k < 3; ++k) {
+    a.rx_c[k] = rx ? rx->center[k] : 0.0f;
+    a.tx[k] = tx[k];
+  }
+  a.rx_r2 = rx ? rx->radius * rx->radius : 0.0f;
+  a.ray_offset = ray_offset;
+  a.n = n;
+  a.traced = traced;
+  a.received = received;
+  a.mask = mask;
+  a.hit_kind = hit_kind;
+  a.hit_face = hit_face;
+  const size_t lds = (size_t)env->nf * 18 * sizeof(float4);
+  int dev_cu = 256;
+  const int64_t want = (n + 255) / 256;
+  const int64_t cap = (int64_t)dev_cu * 16;
+  const int grid = (int)(want < cap ? want : cap);
+  const dim3 blk(256);
+  // a generic (non-generic-Warp) B>8 falls back to the row-resident kernel
+  if (traced == nullptr && B > 8) {
+    set_error("rt_trace: max_bounces > 8 requires the traced buffer (scratch rows)");
+    return -1;
+  }
+  switch (B) {
+#define RT_CASE(BB) \
+  case BB: hipLaunchKernelGGL(k_trace_bf<BB>, dim3(grid), blk, lds, stream, a); break;
+    RT_CASE(1) RT_CASE(2) RT_CASE(3) RT_CASE(4) RT_CASE(5) RT_CASE(6) RT_CASE(7) RT_CASE(8)
+#undef RT_CASE
+    default:
+      hipLaunchKernelGGL(k_trace_bf_generic, dim3(grid), blk, lds, stream, a, B);
+      break;
+  }
+  RT_HIP(hipGetLastError());
+  return 0;
+}
+
+}  // namespace rt

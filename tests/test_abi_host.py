@@ -1,0 +1,75 @@
+"""CPU-only checks of the boundary and host logic (no compute calls: there is no GPU here)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from rf_ray_tracing_warp_amd import _lib
+from rf_ray_tracing_warp_amd.mesh import load_stl, sphere
+from rf_ray_tracing_warp_amd.tracer import cir_flags
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    src = open(os.path.join(REPO, "include", "rfrt.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(rt_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.lib()
+    names = _declared()
+    assert len(names) >= 10
+    for n in names:
+        assert hasattr(L, n), n
+    assert L.rt_version() == 1
+
+
+def test_error_channel_without_gpu_work():
+    L = _lib.lib()
+    # invalid arguments are rejected before any device call
+    rc = L.rt_trace(None, None, None, 3, 0, 10, None, None, None, None, None, None)
+    assert rc == -1
+    assert b"invalid" in L.rt_last_error()
+    with pytest.raises(_lib.RfrtError):
+        _lib.check(rc, "rt_trace")
+    assert L.rt_compact_workspace_bytes(1_000_000) >= 8 * (1_000_000 // 2048)
+
+
+def test_stl_loader_room():
+    m = load_stl(os.path.join(REPO, "models", "room.stl"))
+    assert m.faces.shape == (44, 3) and m.vertices.shape == (24, 3)
+    e = load_stl(os.path.join(REPO, "models", "almost_empty.stl"))
+    assert e.faces.shape == (12, 3) and e.vertices.shape == (8, 3)
+    np.testing.assert_allclose(e.bounds, [[-0.05] * 3, [0.05] * 3], atol=1e-7)
+
+
+def test_stl_ascii_roundtrip(tmp_path):
+    m = load_stl(os.path.join(REPO, "models", "room.stl"))
+    lines = ["solid t"]
+    for f in m.faces:
+        lines += ["facet normal 0 0 0", "outer loop"]
+        lines += ["vertex %r %r %r" % tuple(float(x) for x in m.vertices[i].astype(np.float32)) for i in f]
+        lines += ["endloop", "endfacet"]
+    lines.append("endsolid t")
+    p = tmp_path / "a.stl"
+    p.write_text("\n".join(lines))
+    a = load_stl(str(p))
+    np.testing.assert_array_equal(a.triangles.astype(np.float32), m.triangles.astype(np.float32))
+
+
+def test_rx_icosphere_shape():
+    s = sphere((-10, 0, 5), 0.1, 1)  # tracer.py:27
+    assert s.vertices.shape == (42, 3) and s.faces.shape == (80, 3)
+    r = np.linalg.norm(s.vertices - [-10, 0, 5], axis=1)
+    np.testing.assert_allclose(r, 0.1, rtol=1e-12)
+
+
+def test_nep50_cir_flags():
+    assert cir_flags(2.998e8, 100e9) == 0
+    assert cir_flags(np.float64(2.998e8), 100e9) == _lib.RT_CIR_C_F64
+    assert cir_flags(2.998e8, np.float64(100e9)) == _lib.RT_CIR_FS_F64
+    assert cir_flags(np.float32(2.998e8), 100e9) == 0

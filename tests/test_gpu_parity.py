@@ -1,0 +1,255 @@
+"""HIP path vs the CPU oracle, through the C ABI (needs an MI355X).
+
+Bar: bit-exact for everything the kernel computes (directions, hit t, hit face ids, bounce
+kinds, every path point, row_mask); impulse response within 1e-5 relative (north_star) with
+bins identical.  Full-size configs are checked per ray on a spread subsample (any ray id can be
+re-traced by the oracle alone) plus every received ray.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from oracle import oracle as orc  # noqa: E402
+from rf_ray_tracing_warp_amd import _lib  # noqa: E402
+from rf_ray_tracing_warp_amd._lib import DeviceMesh, check, lib, ptr  # noqa: E402
+from rf_ray_tracing_warp_amd.mesh import load_stl, sphere  # noqa: E402
+from rf_ray_tracing_warp_amd.tracer import Tracer  # noqa: E402
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+DEV = "cuda:0"
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu(require_gpu):
+    lib()
+
+
+@pytest.fixture(scope="module")
+def room():
+    return load_stl(os.path.join(REPO, "models", "room.stl"))
+
+
+@pytest.fixture(scope="module")
+def empty():
+    return load_stl(os.path.join(REPO, "models", "almost_empty.stl"))
+
+
+def _bits(a):
+    return np.ascontiguousarray(a).view(np.uint32)
+
+
+@pytest.mark.parametrize("op,gen", [
+    (0, lambda r: np.abs(r.standard_normal(1 << 20)).astype(np.float32) * np.float32(1e3)),
+    (1, lambda r: (r.standard_normal(1 << 20) * 10).astype(np.float32)),
+    (2, lambda r: r.uniform(0, 2 * np.pi, 1 << 20).astype(np.float32)),
+    (3, lambda r: r.uniform(0, 2 * np.pi, 1 << 20).astype(np.float32)),
+    (4, lambda r: r.uniform(-1, 1, 1 << 20).astype(np.float32)),
+])
+def test_math_bitexact(op, gen):
+    x = gen(np.random.default_rng(op))
+    if op == 4:
+        x[:5] = [-1.0, 1.0, 0.5, -0.5, 0.0]
+    xt = torch.from_numpy(x).to(DEV)
+    out = torch.empty_like(xt)
+    check(lib().rt_selftest_math(ptr(xt), x.size, ptr(out), op, _stream()))
+    got = out.cpu().numpy()
+    if op == 0:
+        ref = np.sqrt(x)
+    elif op == 1:
+        ref = (np.float32(1.0) / x).astype(np.float32)
+    elif op in (2, 3):
+        s, c = orc.sincosf(x)
+        ref = s if op == 2 else c
+    else:
+        ref = orc.acosf(x)
+    np.testing.assert_array_equal(_bits(got), _bits(ref))
+
+
+@pytest.mark.parametrize("offset,n", [(0, 1 << 20), (79_000_000, 1 << 18), ((1 << 31) - 100, 100)])
+def test_ray_dirs_bitexact(offset, n):
+    out = torch.empty((n, 3), dtype=torch.float32, device=DEV)
+    check(lib().rt_ray_dirs(offset, n, ptr(out), _stream()))
+    np.testing.assert_array_equal(_bits(out.cpu().numpy()), _bits(orc.ray_dirs(offset, n)))
+
+
+def _random_rays(rng, n, lo, hi):
+    o = rng.uniform(lo, hi, (n, 3)).astype(np.float32)
+    d = rng.standard_normal((n, 3))
+    d /= np.linalg.norm(d, axis=1)[:, None]
+    return o, d.astype(np.float32)
+
+
+@pytest.mark.parametrize("which", ["room", "rx1", "rx3"])
+def test_query_bitexact(which, room):
+    rng = np.random.default_rng(7)
+    if which == "room":
+        v, f = room.vertices, room.faces
+        o, d = _random_rays(rng, 200_000, -16, 16)
+    else:
+        m = sphere((-10.0, 0.0, 5.0), 0.1, 1 if which == "rx1" else 3)
+        v, f = m.vertices, m.faces
+        o, d = _random_rays(rng, 200_000, -0.2, 0.2)
+        o += np.array([-10.0, 0.0, 5.0], np.float32)  # origins around the sphere (inside and out)
+    dm = DeviceMesh(v, f)
+    ot, dt = torch.from_numpy(o).to(DEV), torch.from_numpy(d).to(DEV)
+    t = torch.empty(len(o), dtype=torch.float32, device=DEV)
+    face = torch.empty(len(o), dtype=torch.int32, device=DEV)
+    check(lib().rt_query(dm.handle, ptr(ot), ptr(dt), len(o), ptr(t), ptr(face), _stream()))
+    rt, rf, _ = orc.Mesh(v, f).query(o, d)
+    np.testing.assert_array_equal(face.cpu().numpy(), rf)
+    np.testing.assert_array_equal(_bits(t.cpu().numpy()), _bits(rt))
+    assert (rf >= 0).mean() > 0.05
+
+
+def _gpu_trace(env, rxm, tx, B, off, n, want_traced=True):
+    e = DeviceMesh(env.vertices, env.faces)
+    r = DeviceMesh(rxm.vertices, rxm.faces) if rxm is not None else None
+    P = B + 1
+    out = {
+        "traced": torch.empty((n, P, 3), dtype=torch.float32, device=DEV) if want_traced else None,
+        "received": torch.empty((n, P, 3), dtype=torch.float32, device=DEV),
+        "mask": torch.empty(n, dtype=torch.int32, device=DEV),
+        "hit_kind": torch.empty((n, B), dtype=torch.int32, device=DEV),
+        "hit_face": torch.empty((n, B), dtype=torch.int32, device=DEV),
+    }
+    tx32 = np.asarray(tx, np.float32)
+    check(lib().rt_trace(e.handle, tx32.ctypes.data, r.handle if r else None, B, off, n, ptr(out["traced"]),
+                         ptr(out["received"]), ptr(out["mask"]), ptr(out["hit_kind"]), ptr(out["hit_face"]),
+                         _stream()))
+    torch.cuda.synchronize()
+    return {k: (v.cpu().numpy() if v is not None else None) for k, v in out.items()}
+
+
+def _assert_trace_equal(g, o, rows=None):
+    for k in ("traced", "received"):
+        if g[k] is None or o[k] is None:
+            continue
+        a = g[k] if rows is None else g[k][rows]
+        np.testing.assert_array_equal(_bits(a), _bits(o[k]), err_msg=k)
+    for k in ("hit_kind", "hit_face"):
+        a = g[k] if rows is None else g[k][rows]
+        np.testing.assert_array_equal(a, o[k], err_msg=k)
+    a = g["mask"] if rows is None else g["mask"][rows]
+    np.testing.assert_array_equal(a.astype(np.uint32), o["mask"])
+
+
+@pytest.mark.parametrize("cfg", [
+    # K1: almost_empty, tx (1,0,1), rx (41,0,1), 10k rays, 1 bounce (main.py:25-27)
+    ("almost_empty", (1, 0, 1), (41, 0, 1), 1, 0, 10_000),
+    ("room", (10, 0, 5), (-10, 0, 5), 3, 0, 60_000),
+    ("room", (10, 0, 5), (5, 3, 4), 3, 1_000_000, 60_000),
+    ("room", (10, 0, 5), (-10, 8, 5), 5, 3, 40_000),
+    ("room", (0, 5, 7), (10, 0.5, 5), 8, 17, 20_000),
+    ("room", (10, 0, 5), (9.95, 0.02, 5.01), 4, 0, 20_000),  # tx inside the receiver ball
+])
+def test_trace_bitexact_small(cfg, room, empty):
+    name, tx, rx, B, off, n = cfg
+    env = room if name == "room" else empty
+    rxm = sphere(rx, 0.1, 1)
+    g = _gpu_trace(env, rxm, tx, B, off, n)
+    o = orc.trace(orc.Mesh(env.vertices, env.faces), orc.Mesh(rxm.vertices, rxm.faces), tx, B, off, n)
+    _assert_trace_equal(g, o)
+
+
+def test_trace_generic_b12(room):
+    rxm = sphere((5, 3, 4), 0.1, 1)
+    g = _gpu_trace(room, rxm, (10, 0, 5), 12, 5, 8_000)
+    o = orc.trace(orc.Mesh(room.vertices, room.faces), orc.Mesh(rxm.vertices, rxm.faces), (10, 0, 5), 12, 5, 8_000)
+    _assert_trace_equal(g, o)
+
+
+def test_trace_k2_full_size(room):
+    """K2: room.stl, 1M rays, 3 bounces -- every received row + a 1/50 subsample, bit-exact."""
+    n, B, tx, rx = 1_000_000, 3, (10, 0, 5), (-10, 8, 5)
+    rxm = sphere(rx, 0.1, 1)
+    g = _gpu_trace(room, rxm, tx, B, 0, n)
+    E, R = orc.Mesh(room.vertices, room.faces), orc.Mesh(rxm.vertices, rxm.faces)
+    rows = np.union1d(np.arange(0, n, 50), np.nonzero(g["mask"])[0])
+    o = orc.trace_ids(E, R, tx, B, rows)
+    _assert_trace_equal(g, o, rows)
+    # invariants over all rows: received is a prefix of traced; mask <-> any RX hit
+    tr, rc, hk = g["traced"], g["received"], g["hit_kind"]
+    has_rx = (hk == 2).any(axis=1)
+    np.testing.assert_array_equal(g["mask"].astype(bool), has_rx)
+    fin = ~np.isnan(rc[..., 0])
+    np.testing.assert_array_equal(rc[fin], tr[fin])
+
+
+def test_artifact_scene_html_gpu(empty):
+    """The reference artifact's 119 received rays (tests/golden/scene_html.npz) on the GPU."""
+    g = np.load(os.path.join(HERE, "golden", "scene_html.npz"))
+    rxm = sphere(g["rx"], 0.1, 3)
+    ids = np.sort(g["cone_ids"])
+    ids = ids[ids <= g["ray_ids"].max()]
+    got = []
+    for i in ids:
+        r = _gpu_trace(empty, rxm, g["tx"], 3, int(i), 1, want_traced=False)
+        if r["mask"][0]:
+            got.append(int(i))
+            k = int(np.nonzero(g["ray_ids"] == i)[0][0])
+            assert np.abs(r["received"][0][1] - g["paths"][k][1]).max() < 4e-6
+    assert sorted(got) == sorted(g["ray_ids"].tolist())
+
+
+# ---------------------------------------------------------------------------- CIR
+def _device_cir(received, mask, B, c, fs, win, txp, N):
+    rec = torch.from_numpy(np.ascontiguousarray(received)).to(DEV)
+    m = torch.from_numpy(mask.astype(np.int32)).to(DEV)
+    n = len(received)
+    ws = torch.empty(int(lib().rt_compact_workspace_bytes(n)), dtype=torch.uint8, device=DEV)
+    idx = torch.empty(max(n, 1), dtype=torch.int64, device=DEV)
+    cnt = torch.empty(1, dtype=torch.int64, device=DEV)
+    check(lib().rt_compact(ptr(m), n, ptr(ws), ws.numel(), ptr(idx), ptr(cnt), _stream()))
+    nb = int(win * fs)
+    ir = torch.zeros(nb, dtype=torch.float64, device=DEV)
+    bins = torch.full((max(n, 1),), -1, dtype=torch.int32, device=DEV)
+    amps = torch.zeros(max(n, 1), dtype=torch.float64, device=DEV)
+    check(lib().rt_cir(ptr(rec), ptr(idx), ptr(cnt), n, B, txp / N, c, fs, 0, nb, ptr(ir), ptr(bins), ptr(amps),
+                       _stream()))
+    k = int(cnt.item())
+    return ir.cpu().numpy(), idx[:k].cpu().numpy(), bins[:k].cpu().numpy(), amps[:k].cpu().numpy()
+
+
+@pytest.mark.parametrize("case", ["edge", "room0", "room1", "room2"])
+def test_cir_matches_reference_golden(case):
+    h = np.load(os.path.join(HERE, "golden", "host_cir.npz"))
+    rec, mask = h[f"{case}_received"], h[f"{case}_mask"]
+    c, fs, win, txp = h[f"{case}_params"]
+    ir, idx, bins, amps = _device_cir(rec, mask, rec.shape[1] - 1, float(c), float(fs), float(win), float(txp),
+                                      len(rec))
+    np.testing.assert_array_equal(idx, np.nonzero(mask)[0])
+    ref = h[f"{case}_ir"]
+    np.testing.assert_array_equal(np.nonzero(ir)[0], np.nonzero(ref)[0])
+    np.testing.assert_allclose(ir, ref, rtol=1e-5, atol=0)
+    paths = orc.clean_paths(rec, mask)
+    for p, b, a in zip(paths, bins, amps):
+        rb, ra = orc.path_bin_amp(p, float(txp), len(rec), float(c), float(fs))
+        assert b == rb
+        assert abs(a - ra) <= 1e-5 * abs(ra)
+
+
+def test_compute_cir_end_to_end(room):
+    """Tracer.compute_cir == oracle trace + reference host CIR (K2-shaped, 200k rays)."""
+    N, B, tx, rx = 200_000, 3, (10, 0, 5), (5, 3, 4)
+    t = Tracer(room, 2.998e8, 100e9, 100e-9, B, N)
+    paths, ir = t.compute_cir(np.array(tx), 1, np.array(rx), 0.1)
+    rxm = sphere(rx, 0.1, 1)
+    o = orc.trace(orc.Mesh(room.vertices, room.faces), orc.Mesh(rxm.vertices, rxm.faces), tx, B, 0, N,
+                  want_traced=False)
+    ref_paths = orc.clean_paths(o["received"], o["mask"])
+    assert len(paths) == len(ref_paths) > 0
+    for a, b in zip(paths, ref_paths):
+        np.testing.assert_array_equal(a, b)
+    ref_ir = orc.cir_from_paths(ref_paths, 1, N, 2.998e8, 100e9, 100e-9)
+    np.testing.assert_array_equal(np.nonzero(ir)[0], np.nonzero(ref_ir)[0])
+    np.testing.assert_allclose(ir, ref_ir, rtol=1e-5, atol=0)
