@@ -2,7 +2,8 @@
 
 ``python -m rf_ray_tracing_warp_amd.build`` (or ``__graft_entry__.build()``).  Objects are rebuilt
 only when their source or a header is newer.  -ffp-contract=off is part of the arithmetic
-contract (only explicit fmaf() fuse; see rt_device.h).
+contract (only explicit fmaf() fuse; see rt_device.h).  -fno-slp-vectorize: SLP packing into
+v_pk_*_f32 buys no f32 throughput on gfx950 and costs register-shuffle moves in the triangle loop.
 """
 from __future__ import annotations
 
@@ -21,7 +22,7 @@ LIB = os.path.join(PKG, "librfrt.so")
 ARCH = os.environ.get("RFRT_ARCH", "gfx950")
 
 CFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-contract=off",
-          "-fno-fast-math", "-Wall", "-Wno-unused-function", f"-I{os.path.join(REPO, 'include')}"]
+          "-fno-fast-math", "-fno-slp-vectorize", "-Wall", "-Wno-unused-function", f"-I{os.path.join(REPO, 'include')}"]
 
 
 def hipcc() -> str:

@@ -128,7 +128,8 @@ __device__ __forceinline__ bool tri_test(const Shear& s, float4 q0, float4 q1, f
   float U = fmaf(Cx, By, -(Cy * Bx));
   float V = fmaf(Ax, Cy, -(Ay * Cx));
   float W = fmaf(Bx, Ay, -(By * Ax));
-  if (U == 0.0f || V == 0.0f || W == 0.0f) {  // edge/vertex case: recompute in double
+  // any of U,V,W == 0 (min3 of magnitudes: one v_min3 + one compare; U,V,W are never NaN here)
+  if (fminf(fminf(fabsf(U), fabsf(V)), fabsf(W)) == 0.0f) {  // edge/vertex case: recompute in double
     U = (float)((double)Cx * (double)By - (double)Cy * (double)Bx);
     V = (float)((double)Ax * (double)Cy - (double)Ay * (double)Cx);
     W = (float)((double)Bx * (double)Ay - (double)By * (double)Ax);
@@ -152,13 +153,21 @@ __device__ __forceinline__ void hit_init(Hit& h) {
   h.t = RT_MAX_T;
   h.face = -1;
 }
-__device__ __forceinline__ void hit_consider(Hit& h, float T, float det, int face) {
+// Exact update: t = T*(1/det) with the correctly rounded reciprocal, as Warp computes it.
+__device__ __forceinline__ void hit_update_exact(Hit& h, float T, float det, int face) {
   const float t = T * (1.0f / det);
   const bool better = (t < h.t) | ((t == h.t) & (face < h.face));
   if (better & (t >= 0.0f) & (t < RT_MAX_T)) {
     h.t = t;
     h.face = face;
   }
+}
+// Screened update: v_rcp_f32 (1 ulp) gives a = T*rcp(det) within 2^-21 of the exact t, so a
+// candidate with a > h.t*(1+2^-16) cannot win and skips the ~12-instruction IEEE division.
+// The decision (and so every output bit) is identical to hit_update_exact.
+__device__ __forceinline__ void hit_consider(Hit& h, float T, float det, int face) {
+  const float a = fabsf(T) * __builtin_amdgcn_rcpf(fabsf(det));
+  if (!(a > h.t * 1.0000153f)) hit_update_exact(h, T, det, face);
 }
 
 }  // namespace rt
