@@ -72,6 +72,38 @@ int rt_cir(const float* received, const int64_t* index, const int64_t* count, in
            double amp0, double light_speed, double sample_rate, int flags, int64_t n_bins, double* impulse_response,
            int32_t* out_bin, double* out_amp, void* stream);
 
+/* ---------------------------------------------------------------- coverage (coverage.py:38-57)
+ * Receiver cells on a lattice: cell (i,j,k), index (k*ny + j)*nx + i, centre
+ * (x0 + i*dx, y0 + j*dy, z0 + k*dz) computed in double.  Each cell is the reference's
+ * Tracer.compute_cir(tx_pos, tx_power, centre, rx_radius) followed by the signal power of
+ * coverage.py:45-52; rt_coverage computes all cells exactly by shared trajectories. */
+typedef struct {
+  double x0, y0, z0, dx, dy, dz;
+  int64_t nx, ny, nz;
+} rt_grid;
+
+typedef struct rt_coverage rt_coverage;
+
+/* Plan a coverage run: env mesh, bounces (1..15), rays per cell (global ids ray_offset + [0,n)),
+ * receiver radius; cells with index % shard_count == shard_index are computed (multi-GPU). */
+int rt_coverage_create(int device, const rt_mesh* env, int max_bounces, int64_t n_rays, int64_t ray_offset,
+                       const rt_grid* grid, double rx_radius, int shard_index, int shard_count, rt_coverage** out);
+int rt_coverage_destroy(rt_coverage* cov);
+/* Run for one transmitter.  power (n_cells f64, device): mean square of the nonzero samples of
+ * np.convolve(ir, sin(2*pi*2.4e9*t), 'same') (coverage.py:45-52), NaN for a cell that receives
+ * nothing, 0 for cells of other shards (sum-reduce the map across ranks).  alpha = phase step per
+ * sample = (2*pi*2.4e9) * sample_window_s / (n_bins - 1).  stats[0] = candidate (cell, ray, bounce)
+ * triples.  Synchronises the stream once (candidate count). */
+int rt_coverage_run(rt_coverage* cov, const float* tx_pos, double tx_power, double light_speed, double sample_rate,
+                    int flags, int64_t n_bins, double alpha, double* power, int64_t* stats, void* stream);
+/* Sparse per-cell impulse responses of the last run: keys (cell << 32 | bin) ascending, amplitudes. */
+int rt_coverage_received(rt_coverage* cov, uint64_t* keys_out, double* amps_out, int64_t max_out, int64_t* n_out,
+                         void* stream);
+/* Signal power (same definition) of `rows` dense impulse responses (rows, n_bins) f64 on the device.
+ * scratch: rows * n_bins * 16 bytes of device memory. */
+int rt_power_dense(const double* impulse_responses, int64_t rows, int64_t n_bins, double alpha, void* scratch,
+                   int64_t scratch_bytes, double* power, void* stream);
+
 /* Self-test entry points used by the parity tests (not part of the reference surface). */
 int rt_selftest_math(const float* x, int64_t n, float* out, int op, void* stream);
 int rt_ray_dirs(int64_t ray_offset, int64_t n, float* out, void* stream);

@@ -182,8 +182,15 @@ def clean_paths(received, mask):
     return cleaned
 
 
-def cir_from_paths(cleaned_paths, tx_power, tx_num_rays, light_speed_mps, sample_rate_hz, sample_window_s):
-    """tracer.py:101-117."""
+def _arccos_cr(x):
+    """float32 arccos rounded once from double: the device's choice (NumPy's SIMD float32 arccos is
+    a few ulp off; used only to separate that rounding from other differences in the tests)."""
+    return np.float32(math.acos(float(x))) if abs(float(x)) <= 1.0 else np.float32("nan")
+
+
+def cir_from_paths(cleaned_paths, tx_power, tx_num_rays, light_speed_mps, sample_rate_hz, sample_window_s,
+                   arccos=np.arccos):
+    """tracer.py:101-117 (``arccos`` replaceable only for the conditioning checks of the tests)."""
     with np.errstate(all="ignore"):
         impulse_response = np.zeros(int(sample_window_s * sample_rate_hz))
         for path in cleaned_paths:
@@ -193,7 +200,7 @@ def cir_from_paths(cleaned_paths, tx_power, tx_num_rays, light_speed_mps, sample
                 seg1 = p2 - p1
                 seg2 = p3 - p2
                 seg1_len = np.linalg.norm(seg1)
-                angle_between = np.arccos(np.dot(seg1, seg2) / (seg1_len * np.linalg.norm(seg2)))
+                angle_between = arccos(np.dot(seg1, seg2) / (seg1_len * np.linalg.norm(seg2)))
                 amplitude *= bounce_amplitude(angle_between)
                 distance += seg1_len
             distance += np.linalg.norm(path[-2] - path[-1])
@@ -234,3 +241,27 @@ def to_dbm(power):
     """main.py:12-13."""
     with np.errstate(all="ignore"):
         return 10 * np.log10(power / 1e-3)
+
+
+def coverage_loop(env: Mesh, tx, centers, B, n_rays, c=2.998e8, fs=100e9, win=100e-9, tx_power=1, rx_radius=0.1,
+                  nthreads=None, with_cr=False):
+    """coverage.py:38-57 literally: for every receiver centre a full trace (kernel.py) with that
+    cell's icosphere (tracer.py:27), the host CIR (tracer.py:84-117) and the signal power
+    (coverage.py:45-52).  Returns (power per cell, list of impulse responses)."""
+    import sys as _sys
+    _sys.path.insert(0, os.path.dirname(_HERE))
+    from rf_ray_tracing_warp_amd.mesh import sphere
+
+    powers, irs, powers_cr = [], [], []
+    for cen in np.asarray(centers, dtype=np.float64).reshape(-1, 3):
+        rxm = sphere(cen, rx_radius, 1)
+        o = trace(env, Mesh(rxm.vertices, rxm.faces), tx, B, 0, n_rays, want_traced=False, nthreads=nthreads)
+        paths = clean_paths(o["received"], o["mask"])
+        ir = cir_from_paths(paths, tx_power, n_rays, c, fs, win)
+        irs.append(ir)
+        powers.append(signal_power(ir, win))
+        if with_cr:
+            powers_cr.append(signal_power(cir_from_paths(paths, tx_power, n_rays, c, fs, win, arccos=_arccos_cr), win))
+    if with_cr:
+        return np.array(powers), irs, np.array(powers_cr)
+    return np.array(powers), irs

@@ -45,11 +45,19 @@ def lib():
     L.rt_compact.argtypes = [_vp, _i64, _vp, _i64, _vp, _vp, _vp]
     L.rt_cir.argtypes = [_vp, _vp, _vp, _i64, _int, ctypes.c_double, ctypes.c_double, ctypes.c_double, _int, _i64,
                          _vp, _vp, _vp, _vp]
+    L.rt_coverage_create.argtypes = [_int, _vp, _int, _i64, _i64, _vp, ctypes.c_double, _int, _int,
+                                     ctypes.POINTER(_vp)]
+    L.rt_coverage_destroy.argtypes = [_vp]
+    L.rt_coverage_run.argtypes = [_vp, _vp, ctypes.c_double, ctypes.c_double, ctypes.c_double, _int, _i64,
+                                  ctypes.c_double, _vp, _vp, _vp]
+    L.rt_coverage_received.argtypes = [_vp, _vp, _vp, _i64, ctypes.POINTER(_i64), _vp]
+    L.rt_power_dense.argtypes = [_vp, _i64, _i64, ctypes.c_double, _vp, _i64, _vp, _vp]
     L.rt_selftest_math.argtypes = [_vp, _i64, _vp, _int, _vp]
     L.rt_ray_dirs.argtypes = [_i64, _i64, _vp, _vp]
     L.rt_query.argtypes = [_vp, _vp, _vp, _i64, _vp, _vp, _vp]
     for name in ("rt_mesh_create", "rt_mesh_destroy", "rt_mesh_info", "rt_trace", "rt_compact", "rt_cir",
-                 "rt_selftest_math", "rt_ray_dirs", "rt_query"):
+                 "rt_coverage_create", "rt_coverage_destroy", "rt_coverage_run", "rt_coverage_received",
+                 "rt_power_dense", "rt_selftest_math", "rt_ray_dirs", "rt_query"):
         getattr(L, name).restype = _int
     _lib = L
     return L

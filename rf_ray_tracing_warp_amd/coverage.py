@@ -1,0 +1,198 @@
+"""Coverage map: the reference's coverage.py on the device.
+
+coverage.py:38-57 loops over receiver positions, runs ``Tracer.compute_cir`` for each and turns the
+impulse response into a received signal power (coverage.py:45-52), then dBm.  ``Coverage`` computes
+the same per-cell power for a whole lattice of receivers in one shot (csrc/coverage.hip, exact
+shared-trajectory algorithm).  Cells can be sharded across ranks (one process per GPU); the power
+map is then sum-reduced over the process group (RCCL over xGMI with the "nccl" backend).
+
+    grid = CoverageGrid.from_ranges(range(-15, 16, 2), range(-15, 16, 2), range(0, 16, 2))  # coverage.py:38-40
+    cov = Coverage(mesh, 2.998e8, 100e9, 100e-9, max_bounces=2, tx_num_rays=1_000_000, grid=grid)
+    power = cov.run(tx_pos=(10, 0, 5), tx_power=1)        # (nz, ny, nx) float64 watts, NaN = no path
+    dbm = to_dbm(power)
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from ._lib import DeviceMesh, check, lib, ptr
+from .power import CARRIER_HZ, to_dbm
+from .tracer import cir_flags
+
+__all__ = ["CoverageGrid", "Coverage", "coverage_points", "phase_step"]
+
+
+class _Grid(ctypes.Structure):
+    _fields_ = [("x0", ctypes.c_double), ("y0", ctypes.c_double), ("z0", ctypes.c_double),
+                ("dx", ctypes.c_double), ("dy", ctypes.c_double), ("dz", ctypes.c_double),
+                ("nx", ctypes.c_int64), ("ny", ctypes.c_int64), ("nz", ctypes.c_int64)]
+
+
+@dataclass(frozen=True)
+class CoverageGrid:
+    """Receiver lattice: cell (i,j,k) centre = (x0 + i*dx, y0 + j*dy, z0 + k*dz) in float64."""
+
+    x0: float
+    y0: float
+    z0: float
+    dx: float
+    dy: float
+    dz: float
+    nx: int
+    ny: int
+    nz: int
+
+    @classmethod
+    def from_ranges(cls, xs, ys, zs):
+        """From three arithmetic progressions (e.g. the range() loops of coverage.py:38-40)."""
+        def ap(v):
+            v = list(v)
+            step = float(v[1] - v[0]) if len(v) > 1 else 1.0
+            if any(abs((v[i] - v[0]) - i * step) > 1e-12 * max(1.0, abs(step) * len(v)) for i in range(len(v))):
+                raise ValueError("coverage grid axes must be arithmetic progressions")
+            return float(v[0]), step, len(v)
+        (x0, dx, nx), (y0, dy, ny), (z0, dz, nz) = ap(xs), ap(ys), ap(zs)
+        return cls(x0, y0, z0, dx, dy, dz, nx, ny, nz)
+
+    @classmethod
+    def square(cls, n, half_extent, z):
+        """n x n cells covering [-h, h]^2 at height z, centres -h + (i + 1/2) * 2h/n."""
+        d = 2.0 * half_extent / n
+        return cls(-half_extent + 0.5 * d, -half_extent + 0.5 * d, float(z), d, d, 1.0, n, n, 1)
+
+    @property
+    def num_cells(self) -> int:
+        return self.nx * self.ny * self.nz
+
+    def centers(self) -> np.ndarray:
+        """(nz, ny, nx, 3) float64 centres, the exact doubles the device uses."""
+        i = np.arange(self.nx, dtype=np.float64)
+        j = np.arange(self.ny, dtype=np.float64)
+        k = np.arange(self.nz, dtype=np.float64)
+        X = self.x0 + i * self.dx
+        Y = self.y0 + j * self.dy
+        Z = self.z0 + k * self.dz
+        out = np.empty((self.nz, self.ny, self.nx, 3))
+        out[..., 0] = X[None, None, :]
+        out[..., 1] = Y[None, :, None]
+        out[..., 2] = Z[:, None, None]
+        return out
+
+    def _c(self):
+        return _Grid(self.x0, self.y0, self.z0, self.dx, self.dy, self.dz, self.nx, self.ny, self.nz)
+
+
+def phase_step(sample_window_s, n_bins) -> float:
+    """Phase of np.sin(2*np.pi*2.4e9*np.linspace(0, window, n)) per sample (coverage.py:45-46)."""
+    return (2 * np.pi * CARRIER_HZ) * (sample_window_s / (n_bins - 1))
+
+
+class Coverage:
+    """All receiver cells of ``grid`` for one transmitter: coverage.py:38-57 in one device pass."""
+
+    def __init__(self, environment_trimesh, light_speed_mps, sample_rate_hz, sample_window_s, max_bounces,
+                 tx_num_rays, grid: CoverageGrid, rx_radius=0.1, device: int | None = None, shard_index: int = 0,
+                 shard_count: int = 1, env_mesh: DeviceMesh | None = None):
+        import torch
+
+        if not torch.cuda.is_available():
+            raise _lib.RfrtError("Coverage needs a ROCm GPU (librfrt has no CPU path)")
+        self.device = torch.cuda.current_device() if device is None else int(device)
+        self.light_speed_mps = light_speed_mps
+        self.sample_rate_hz = sample_rate_hz
+        self.sample_window_s = sample_window_s
+        self.max_bounces = int(max_bounces)
+        self.tx_num_rays = int(tx_num_rays)
+        self.grid = grid
+        self.rx_radius = float(rx_radius)
+        self.n_bins = int(sample_window_s * sample_rate_hz)
+        self.shard_index, self.shard_count = int(shard_index), int(shard_count)
+        self.env = env_mesh or DeviceMesh(environment_trimesh.vertices, environment_trimesh.faces, self.device)
+        self._h = _lib._vp()
+        g = grid._c()
+        check(lib().rt_coverage_create(self.device, self.env.handle, self.max_bounces, self.tx_num_rays, 0,
+                                       ctypes.byref(g), self.rx_radius, self.shard_index, self.shard_count,
+                                       ctypes.byref(self._h)), "rt_coverage_create")
+        self.power = torch.empty(grid.num_cells, dtype=torch.float64, device=f"cuda:{self.device}")
+        self.last_candidates = 0
+
+    def run_device(self, tx_pos, tx_power=1):
+        """Launch; returns the (num_cells,) float64 device tensor (0 for cells of other shards)."""
+        tx = np.ascontiguousarray(np.asarray(tx_pos, dtype=np.float64).astype(np.float32))
+        stats = np.zeros(2, np.int64)
+        check(lib().rt_coverage_run(self._h, tx.ctypes.data, float(tx_power), float(self.light_speed_mps),
+                                    float(self.sample_rate_hz), cir_flags(self.light_speed_mps, self.sample_rate_hz),
+                                    self.n_bins, phase_step(self.sample_window_s, self.n_bins), ptr(self.power),
+                                    stats.ctypes.data, _lib.stream_handle(self.device)), "rt_coverage_run")
+        self.last_candidates = int(stats[0])
+        return self.power
+
+    def run(self, tx_pos, tx_power=1, process_group=None):
+        """Power map (nz, ny, nx) float64 on the host; with a process group, sum-reduced over ranks."""
+        p = self.run_device(tx_pos, tx_power)
+        if process_group is not None or self.shard_count > 1:
+            import torch.distributed as dist
+            dist.all_reduce(p, group=process_group)
+        g = self.grid
+        return p.cpu().numpy().reshape(g.nz, g.ny, g.nx)
+
+    def impulse_responses(self):
+        """Sparse per-cell impulse responses of the last run: (cell, bin, amplitude) arrays."""
+        import torch
+
+        n = ctypes.c_int64()
+        check(lib().rt_coverage_received(self._h, None, None, 0, ctypes.byref(n), _lib.stream_handle(self.device)),
+              "rt_coverage_received")
+        m = n.value
+        dev = f"cuda:{self.device}"
+        keys = torch.empty(max(m, 1), dtype=torch.int64, device=dev)
+        amps = torch.empty(max(m, 1), dtype=torch.float64, device=dev)
+        check(lib().rt_coverage_received(self._h, ptr(keys), ptr(amps), m, ctypes.byref(n),
+                                         _lib.stream_handle(self.device)), "rt_coverage_received")
+        k = keys[:m].cpu().numpy().view(np.uint64)
+        return (k >> np.uint64(32)).astype(np.int64), (k & np.uint64(0xFFFFFFFF)).astype(np.int64), \
+            amps[:m].cpu().numpy()
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value and _lib._lib is not None:
+            _lib._lib.rt_coverage_destroy(self._h)
+            self._h = _lib._vp()
+
+    def __del__(self):
+        self.close()
+
+
+def coverage_points(power_map, grid: CoverageGrid):
+    """(rx_pos, dBm) pairs in coverage.py's loop order (x outer, then y, then z; coverage.py:38-57)."""
+    c = grid.centers()
+    out = []
+    for i in range(grid.nx):
+        for j in range(grid.ny):
+            for k in range(grid.nz):
+                out.append((c[k, j, i], float(to_dbm(power_map[k, j, i]))))
+    return out
+
+
+def _dist_shard():
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+def coverage_map(environment_trimesh, tx_pos, grid: CoverageGrid, light_speed_mps=2.998e8, sample_rate_hz=100e9,
+                 sample_window_s=100e-9, max_bounces=2, tx_num_rays=1_000_000, tx_power=1, rx_radius=0.1,
+                 device=None):
+    """coverage.py as a function.  Under torch.distributed, cells are sharded over the ranks and the
+    power map is all-reduced; every rank returns the full map."""
+    rank, world = _dist_shard()
+    cov = Coverage(environment_trimesh, light_speed_mps, sample_rate_hz, sample_window_s, max_bounces, tx_num_rays,
+                   grid, rx_radius, device=device, shard_index=rank, shard_count=world)
+    try:
+        return cov.run(tx_pos, tx_power)
+    finally:
+        cov.close()

@@ -1,0 +1,820 @@
+// coverage.hip -- coverage.py (coverage.py:38-57) on the device, exact, by shared trajectories.
+//
+// The reference runs a full Tracer.compute_cir per receiver cell (cells x N x B queries) and then
+// main.py/coverage.py's signal power (np.convolve with a sampled 2.4 GHz sine).  Every cell sees
+// the same rays (rand_init(tid) depends on tid only, kernel.py:51) and a receiver miss never moves
+// the ray (kernel.py:85-98), so for every cell a ray follows its environment-only trajectory
+// bit for bit until the first bounce k where that cell's receiver wins (hit, and nearer than the
+// environment or the environment missed).  This file:
+//
+//   k_traj    trace every ray once against the environment only: p_k, d_k, t_env_k (SoA in HBM)
+//   k_cand    for every segment (p_k, d_k, [0, min(t_env_k, max_t)]) enumerate the lattice cells
+//             whose (padded) receiver ball it touches -> keys (cell, ray, k)         [capsule raster]
+//   sort      radix sort of the keys: candidates grouped by (cell, ray), k ascending
+//   k_win     exact receiver test of each candidate (the cell's icosphere, 80 faces, unrolled)
+//   k_replay  first winning k of each (cell, ray): replay from (p_k, d_k) with the full per-cell
+//             semantics of kernel.py:57-98, then the CIR body of tracer.py:101-117 -> (cell, bin, amp)
+//   sort + reduce-by-key: per-cell sparse impulse response, bins ascending
+//   k_power   closed-form mean square of the nonzero samples of ir (*) sin(2 pi 2.4e9 t)
+//             ('same' mode, np.nonzero) over the piecewise-constant active-bin intervals
+//
+// Cost: N*B environment queries + (#candidates) receiver tests + (#received) replays, instead of
+// cells*N*B*(env + receiver) queries.  Results equal the per-cell reference loop (tests compare
+// against the oracle's per-cell trace + NumPy power); cells are sharded cyclically over ranks.
+#include <hipcub/hipcub.hpp>
+#include <math.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "../../include/rfrt.h"
+#include "rt_device.h"
+#include "rt_icosphere1.h"
+#include "rt_internal.h"
+
+namespace {
+
+
+struct CovParams {
+  const float4* env_perm;
+  const float4* env_nrm;
+  int env_nf;
+  float tx[3];
+  int B;
+  int64_t n;           // rays
+  int64_t ray_offset;  // global id of ray 0
+  rt_grid g;
+  double r_rx;       // receiver radius (tracer.py:26 rx_radius)
+  double r_pad;      // conservative ball radius for candidate search
+  int shard, nshard;  // cell % nshard == shard are ours
+  // trajectory SoA [k][n]
+  float *px, *py, *pz, *dx, *dy, *dz, *te;
+  uint8_t* nseg;
+  // candidates
+  uint64_t* keys;
+  int64_t cap;
+  unsigned long long* count;
+  // CIR
+  double amp0;
+  float c32, fs32;
+  double c64, fs64;
+  int flags;
+  int64_t n_bins;
+};
+
+__device__ __forceinline__ int64_t ncells(const rt_grid& g) { return g.nx * g.ny * g.nz; }
+
+__device__ __forceinline__ void cell_center(const rt_grid& g, int64_t cell, double c[3]) {
+  const int64_t i = cell % g.nx, j = (cell / g.nx) % g.ny, k = cell / (g.nx * g.ny);
+  c[0] = g.x0 + (double)i * g.dx;
+  c[1] = g.y0 + (double)j * g.dy;
+  c[2] = g.z0 + (double)k * g.dz;
+}
+
+// environment closest hit from the LDS table (same code path as the trace kernel)
+__device__ __forceinline__ rt::Hit env_query(const float4* tab, int nf, const rt::Shear& s) {
+  rt::Hit h;
+  rt::hit_init(h);
+  const int off = s.kcase * 3;
+  for (int f = 0; f < nf; ++f) {
+    const float4 q0 = tab[f * 18 + off + 0];
+    const float4 q1 = tab[f * 18 + off + 1];
+    const float c2 = tab[f * 18 + off + 2].x;
+    float T, det;
+    if (rt::tri_test(s, q0, q1, c2, T, det)) rt::hit_consider(h, T, det, f);
+  }
+  return h;
+}
+
+// The cell's receiver: vertex i = (float)(unit_i * r + centre) in double, exactly mesh.sphere() +
+// astype(float32) (tracer.py:27-28), generated directly in the ray's permuted axis order
+// (x=[kx], y=[ky], z=[kz]) so the 80 unrolled faces index registers with compile-time indices.
+struct RxPerm {
+  float v[RT_ICO1_NV][3];
+};
+__device__ __forceinline__ void make_rx_perm(const rt_grid& g, int64_t cell, double r, int kx, int ky, int kz,
+                                             RxPerm& rx) {
+  double c[3];
+  cell_center(g, cell, c);
+#pragma unroll
+  for (int i = 0; i < RT_ICO1_NV; ++i) {
+    float w[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const double m = rt_ico1_v[i][k] * r;
+      w[k] = (float)(m + c[k]);
+    }
+    rx.v[i][0] = kx == 0 ? w[0] : (kx == 1 ? w[1] : w[2]);
+    rx.v[i][1] = ky == 0 ? w[0] : (ky == 1 ? w[1] : w[2]);
+    rx.v[i][2] = kz == 0 ? w[0] : (kz == 1 ? w[1] : w[2]);
+  }
+}
+
+// receiver closest hit for ray (o, d) against cell's icosphere (80 faces, unrolled)
+__device__ __forceinline__ rt::Hit rx_query(const rt_grid& g, int64_t cell, double r, float3 o, float3 d) {
+  const rt::Shear s = rt::make_shear(o, d);
+  const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+  const int kz = (ax > ay && ax > az) ? 0 : ((ay > az) ? 1 : 2);
+  int kx = kz + 1;
+  if (kx == 3) kx = 0;
+  int ky = kx + 1;
+  if (ky == 3) ky = 0;
+  if (rt::comp(d, kz) < 0.0f) {
+    const int t = kx;
+    kx = ky;
+    ky = t;
+  }
+  RxPerm rx;
+  make_rx_perm(g, cell, r, kx, ky, kz, rx);
+  rt::Hit h;
+  rt::hit_init(h);
+#pragma unroll
+  for (int f = 0; f < RT_ICO1_NF; ++f) {
+    const float* a = rx.v[rt_ico1_f[f][0]];
+    const float* b = rx.v[rt_ico1_f[f][1]];
+    const float* c = rx.v[rt_ico1_f[f][2]];
+    float T, det;
+    if (rt::tri_test(s, make_float4(a[0], a[1], a[2], b[0]), make_float4(b[1], b[2], c[0], c[1]), c[2], T, det))
+      rt::hit_consider(h, T, det, f);
+  }
+  return h;
+}
+
+// ------------------------------------------------------------------ 1. environment trajectories
+__global__ __launch_bounds__(256) void k_traj(CovParams p) {
+  extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
+  for (int i = threadIdx.x; i < p.env_nf * 18; i += blockDim.x) lds_tab[i] = p.env_perm[i];
+  __syncthreads();
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < p.n; r += stride) {
+    float3 dir = rt::ray_dir(p.ray_offset + r);
+    float3 pos = make_float3(p.tx[0], p.tx[1], p.tx[2]);
+    int nseg = 0;
+    for (int k = 0; k < p.B; ++k) {
+      const rt::Shear s = rt::make_shear(pos, dir);
+      const rt::Hit he = env_query(lds_tab, p.env_nf, s);
+      const int64_t o = (int64_t)k * p.n + r;
+      p.px[o] = pos.x;
+      p.py[o] = pos.y;
+      p.pz[o] = pos.z;
+      p.dx[o] = dir.x;
+      p.dy[o] = dir.y;
+      p.dz[o] = dir.z;
+      nseg = k + 1;
+      if (he.face < 0) {  // escapes: this segment is infinite, later iterations repeat the miss
+        p.te[o] = INFINITY;
+        break;
+      }
+      p.te[o] = he.t;
+      pos.x = fmaf(dir.x, he.t, pos.x);
+      pos.y = fmaf(dir.y, he.t, pos.y);
+      pos.z = fmaf(dir.z, he.t, pos.z);
+      const float4 n4 = p.env_nrm[he.face];
+      const float3 n = make_float3(n4.x, n4.y, n4.z);
+      const float sc = 2.0f * rt::dot3(dir, n);
+      dir.x = fmaf(-sc, n.x, dir.x);
+      dir.y = fmaf(-sc, n.y, dir.y);
+      dir.z = fmaf(-sc, n.z, dir.z);
+    }
+    p.nseg[r] = (uint8_t)nseg;
+  }
+}
+
+// ------------------------------------------------------------------ 2. candidate cells per segment
+// Two passes over the same enumeration: COUNT writes the per-ray candidate count, WRITE stores the
+// keys at the exclusive-scan offset of the ray (no atomics, deterministic order).
+struct Emit {
+  bool write;
+  int64_t n;       // candidates emitted so far for this ray
+  uint64_t* dst;   // keys + offset[r] (WRITE)
+  __device__ __forceinline__ void operator()(const CovParams& p, int64_t cell, int64_t r, int k) {
+    if (cell % p.nshard != p.shard) return;
+    if (write) dst[n] = ((uint64_t)cell << 28) | ((uint64_t)r << 4) | (uint64_t)k;
+    ++n;
+  }
+};
+
+// does the segment x(t) = o + t d, t in [0, tmax] pass within rp of centre c?  (double, conservative)
+__device__ __forceinline__ bool seg_ball(const double o[3], const double d[3], double tmax, const double c[3],
+                                         double rp2) {
+  const double w0 = c[0] - o[0], w1 = c[1] - o[1], w2 = c[2] - o[2];
+  const double dd = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
+  double t = (w0 * d[0] + w1 * d[1] + w2 * d[2]) / dd;
+  t = t < 0.0 ? 0.0 : (t > tmax ? tmax : t);
+  const double e0 = o[0] + t * d[0] - c[0], e1 = o[1] + t * d[1] - c[1], e2 = o[2] + t * d[2] - c[2];
+  return e0 * e0 + e1 * e1 + e2 * e2 <= rp2;
+}
+
+__device__ __forceinline__ int64_t clampi(int64_t v, int64_t lo, int64_t hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// t-interval of the segment inside |x_axis(t) - c| <= rp  intersected with [t0, t1]
+__device__ __forceinline__ bool slab(double o, double d, double c, double rp, double& t0, double& t1) {
+  if (fabs(d) < 1e-300) return fabs(o - c) <= rp;
+  double a = (c - rp - o) / d, b = (c + rp - o) / d;
+  if (a > b) {
+    const double t = a;
+    a = b;
+    b = t;
+  }
+  t0 = fmax(t0, a);
+  t1 = fmin(t1, b);
+  return t0 <= t1;
+}
+
+__global__ __launch_bounds__(256) void k_cand(CovParams p, int64_t* ray_count, const int64_t* ray_offset) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const rt_grid& g = p.g;
+  const double rp = p.r_pad, rp2 = rp * rp;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < p.n; r += stride) {
+    Emit emit;
+    emit.write = ray_offset != nullptr;
+    emit.n = 0;
+    emit.dst = emit.write ? p.keys + ray_offset[r] : nullptr;
+    const int ns = p.nseg[r];
+    for (int k = 0; k < ns; ++k) {
+      const int64_t o_ = (int64_t)k * p.n + r;
+      const double o[3] = {p.px[o_], p.py[o_], p.pz[o_]};
+      const double d[3] = {p.dx[o_], p.dy[o_], p.dz[o_]};
+      const double te = p.te[o_];
+      const double tmax = te < (double)RT_MAX_T ? te : (double)RT_MAX_T;
+      // dominant lattice walk axis among x/y (z layers are few)
+      for (int64_t kz = 0; kz < g.nz; ++kz) {
+        const double zc = g.z0 + (double)kz * g.dz;
+        double ta = 0.0, tb = tmax;
+        if (!slab(o[2], d[2], zc, rp, ta, tb)) continue;
+        const bool xmajor = fabs(d[0]) >= fabs(d[1]);
+        const int A = xmajor ? 0 : 1, Bx = xmajor ? 1 : 0;
+        const double a0 = A == 0 ? g.x0 : g.y0, da = A == 0 ? g.dx : g.dy;
+        const int64_t na = A == 0 ? g.nx : g.ny;
+        const double b0 = Bx == 0 ? g.x0 : g.y0, db = Bx == 0 ? g.dx : g.dy;
+        const int64_t nb = Bx == 0 ? g.nx : g.ny;
+        const double qa0 = o[A] + ta * d[A], qa1 = o[A] + tb * d[A];
+        const double amin = fmin(qa0, qa1) - rp, amax = fmax(qa0, qa1) + rp;
+        int64_t ia0 = (int64_t)floor((amin - a0) / da), ia1 = (int64_t)ceil((amax - a0) / da);
+        ia0 = clampi(ia0, 0, na - 1);
+        ia1 = clampi(ia1, 0, na - 1);
+        if ((amax - a0) / da < -1.0 || (amin - a0) / da > (double)na) continue;
+        for (int64_t ia = ia0; ia <= ia1; ++ia) {
+          const double ac = a0 + (double)ia * da;
+          double t0 = ta, t1 = tb;
+          if (!slab(o[A], d[A], ac, rp, t0, t1)) continue;
+          const double qb0 = o[Bx] + t0 * d[Bx], qb1 = o[Bx] + t1 * d[Bx];
+          const double bmin = fmin(qb0, qb1) - rp, bmax = fmax(qb0, qb1) + rp;
+          if ((bmax - b0) / db < -1.0 || (bmin - b0) / db > (double)nb) continue;
+          const int64_t ib0 = clampi((int64_t)floor((bmin - b0) / db), 0, nb - 1);
+          const int64_t ib1 = clampi((int64_t)ceil((bmax - b0) / db), 0, nb - 1);
+          for (int64_t ib = ib0; ib <= ib1; ++ib) {
+            const int64_t ix = A == 0 ? ia : ib, iy = A == 0 ? ib : ia;
+            const int64_t cell = (kz * g.ny + iy) * g.nx + ix;
+            double c[3];
+            cell_center(g, cell, c);
+            if (seg_ball(o, d, tmax, c, rp2)) emit(p, cell, r, k);
+          }
+        }
+      }
+    }
+    if (!emit.write) ray_count[r] = emit.n;
+  }
+}
+
+// ------------------------------------------------------------------ 3. exact receiver test per candidate
+__global__ __launch_bounds__(256) void k_win(CovParams p, const uint64_t* keys, int64_t nkeys, uint8_t* win) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nkeys; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t key = keys[i];
+    const int64_t cell = (int64_t)(key >> 28), r = (int64_t)((key >> 4) & 0xFFFFFF);
+    const int k = (int)(key & 15);
+    const int64_t o_ = (int64_t)k * p.n + r;
+    const float3 o = make_float3(p.px[o_], p.py[o_], p.pz[o_]);
+    const float3 d = make_float3(p.dx[o_], p.dy[o_], p.dz[o_]);
+    const float te = p.te[o_];
+    const rt::Hit hr = rx_query(p.g, cell, p.r_rx, o, d);
+    // kernel.py:85 -- receiver wins if hit and (env missed or env strictly farther)
+    win[i] = (hr.face >= 0 && (isinf(te) || te > hr.t)) ? 1 : 0;
+  }
+}
+
+// np.dot / norm on float32 3-vectors and _bounce_amplitude (tracer.py:106-113), as cir.hip
+__device__ __forceinline__ float npdot(const float* a, const float* b) {
+  const float p0 = a[0] * b[0], p1 = a[1] * b[1], p2 = a[2] * b[2];
+  return (float)(((double)p0 + (double)p1) + (double)p2);
+}
+__device__ __forceinline__ double bounce_amp(float angle) {
+  if (isnan(angle)) return 0.0;
+  const double theta = (double)(1.57079637050628662109375f - angle / 2.0f);
+  const double ti = asin(sin(theta) / 5.0);
+  const double q = (cos(ti) - 5.0 * cos(theta)) / (cos(ti) + 5.0 * cos(theta));
+  double amp = -(q * q);
+  if (amp < -1.0) amp = -1.0;
+  if (isnan(amp)) return 0.0;
+  return -amp;
+}
+
+// Incremental form of tracer.py:104-113 for a path that grows one point at a time: distance is
+// the ordered float32 sum of segment norms, amplitude the ordered product of _bounce_amplitude over
+// interior vertices -- identical operations to the loop over (p1, p2, p3) triples.
+struct PathAcc {
+  float prev[3], seg[3];
+  int npts;
+  float dist;
+  double amp;
+  __device__ __forceinline__ void start(float x, float y, float z, double amp0) {
+    prev[0] = x;
+    prev[1] = y;
+    prev[2] = z;
+    npts = 1;
+    dist = 0.0f;
+    amp = amp0;
+  }
+  __device__ __forceinline__ void add(float x, float y, float z) {
+    const float s2[3] = {x - prev[0], y - prev[1], z - prev[2]};
+    if (npts >= 2) {  // vertex prev is interior: angle between seg (p1->p2) and s2 (p2->p3)
+      const float l1 = sqrtf(npdot(seg, seg));
+      const float cosv = npdot(seg, s2) / (l1 * sqrtf(npdot(s2, s2)));
+      amp *= bounce_amp((float)acos((double)cosv));
+    }
+    dist += sqrtf(npdot(s2, s2));
+    seg[0] = s2[0];
+    seg[1] = s2[1];
+    seg[2] = s2[2];
+    prev[0] = x;
+    prev[1] = y;
+    prev[2] = z;
+    ++npts;
+  }
+};
+
+// ------------------------------------------------------------------ 4. replay + CIR body
+__global__ __launch_bounds__(256) void k_replay(CovParams p, const uint64_t* keys, int64_t nkeys, const uint8_t* win,
+                                                uint64_t* out_key, double* out_amp) {
+  extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
+  for (int i = threadIdx.x; i < p.env_nf * 18; i += blockDim.x) lds_tab[i] = p.env_perm[i];
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nkeys; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t key = keys[i];
+    bool first = win[i] != 0;
+    for (int64_t j = i - 1; first && j >= 0 && (keys[j] >> 4) == (key >> 4); --j)
+      if (win[j]) first = false;
+    if (!first) {
+      out_key[i] = ~0ull;
+      out_amp[i] = 0.0;
+      continue;
+    }
+    const int64_t cell = (int64_t)(key >> 28), r = (int64_t)((key >> 4) & 0xFFFFFF);
+    const int k0 = (int)(key & 15);
+    PathAcc acc;
+    acc.start(p.px[r], p.py[r], p.pz[r], p.amp0);  // p_0 = tx
+    for (int q = 1; q <= k0; ++q) {                 // environment prefix p_1 .. p_k0
+      const int64_t o_ = (int64_t)q * p.n + r;
+      acc.add(p.px[o_], p.py[o_], p.pz[o_]);
+    }
+    const int64_t o0 = (int64_t)k0 * p.n + r;
+    float3 pos = make_float3(p.px[o0], p.py[o0], p.pz[o0]);
+    float3 dir = make_float3(p.dx[o0], p.dy[o0], p.dz[o0]);
+    float rec_dist = 0.0f;
+    double rec_amp = 0.0;
+    for (int b = k0; b < p.B; ++b) {  // kernel.py:57-98 with this cell's receiver
+      const rt::Shear s = rt::make_shear(pos, dir);
+      const rt::Hit he = env_query(lds_tab, p.env_nf, s);
+      const rt::Hit hr = rx_query(p.g, cell, p.r_rx, pos, dir);
+      const bool env_hit = he.face >= 0, rx_hit = hr.face >= 0;
+      if (rx_hit && (!env_hit || he.t > hr.t)) {
+        pos.x = fmaf(dir.x, hr.t, pos.x);
+        pos.y = fmaf(dir.y, hr.t, pos.y);
+        pos.z = fmaf(dir.z, hr.t, pos.z);
+        acc.add(pos.x, pos.y, pos.z);
+        rec_dist = acc.dist;  // received_paths = traced prefix through this point (kernel.py:89-90)
+        rec_amp = acc.amp;
+      } else if (env_hit) {
+        pos.x = fmaf(dir.x, he.t, pos.x);
+        pos.y = fmaf(dir.y, he.t, pos.y);
+        pos.z = fmaf(dir.z, he.t, pos.z);
+        acc.add(pos.x, pos.y, pos.z);
+        const float4 n4 = p.env_nrm[he.face];
+        const float3 n = make_float3(n4.x, n4.y, n4.z);
+        const float sc = 2.0f * rt::dot3(dir, n);
+        dir.x = fmaf(-sc, n.x, dir.x);
+        dir.y = fmaf(-sc, n.y, dir.y);
+        dir.z = fmaf(-sc, n.z, dir.z);
+      } else {
+        break;
+      }
+    }
+    double dl;
+    if (p.flags & RT_CIR_C_F64) {
+      dl = ((double)rec_dist / p.c64) * p.fs64;
+    } else {
+      const float q = rec_dist / p.c32;
+      dl = (p.flags & RT_CIR_FS_F64) ? (double)q * p.fs64 : (double)(q * p.fs32);
+    }
+    const int64_t bin = (int64_t)dl;
+    // amplitudes are >= 0; a zero one (NaN angle -> _bounce_amplitude 0, tracer.py:35-37) leaves
+    // impulse_response[bin] untouched, so it must not become an active bin of the power sweep
+    if (bin < p.n_bins && rec_amp != 0.0) {
+      out_key[i] = ((uint64_t)cell << 32) | (uint64_t)bin;
+      out_amp[i] = rec_amp;
+    } else {
+      out_key[i] = ~0ull;
+      out_amp[i] = 0.0;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ 5. closed-form signal power
+struct PowerParams {
+  int64_t n_bins;
+  int64_t half;   // (n-1)//2 : np.convolve 'same' offset
+  double alpha;   // phase per sample: (2*pi*2.4e9) * (window/(n-1))
+};
+
+__device__ __forceinline__ void two_sum(double& s, double& c, double x) {  // Neumaier running sum
+  const double t = s + x;
+  c += fabs(s) >= fabs(x) ? (s - t) + x : (x - t) + s;
+  s = t;
+}
+
+// mean square of the nonzero samples of y = ir (*) sin, for a sparse ir with ascending bins m[k]
+__device__ double power_sparse(const uint64_t* keys, const double* amps, int64_t lo, int64_t hi, const PowerParams& P) {
+  if (hi <= lo) return __builtin_nan("");
+  const int64_t n = P.n_bins, half = P.half;
+  const double al = P.alpha, sa = sin(al);
+  double Ps = 0, Pc = 0, Qs = 0, Qc = 0;  // running sums of a_k cos(alpha c_k), a_k sin(alpha c_k)
+  double total = 0.0, tc = 0.0;
+  int64_t count = 0;
+  int64_t is = lo, ie = lo;  // active terms = [ie, is)
+  int64_t x = 0;
+  auto sk = [&](int64_t k) { const int64_t m = (int64_t)(keys[k] & 0xFFFFFFFFull); return m - half > 0 ? m - half : 0; };
+  auto ek = [&](int64_t k) { const int64_t m = (int64_t)(keys[k] & 0xFFFFFFFFull); const int64_t e = m + (n - 1 - half); return e < n - 1 ? e : n - 1; };
+  auto term = [&](int64_t k, double sgn) {
+    const int64_t m = (int64_t)(keys[k] & 0xFFFFFFFFull);
+    const double ph = al * (double)(half - m);
+    two_sum(Ps, Pc, sgn * amps[k] * cos(ph));
+    two_sum(Qs, Qc, sgn * amps[k] * sin(ph));
+  };
+  while (true) {
+    bool started_alone = false;
+    int64_t nstart = 0;
+    while (is < hi && sk(is) <= x) {
+      term(is, 1.0);
+      ++is;
+      ++nstart;
+    }
+    while (ie < is && ek(ie) < x) {
+      term(ie, -1.0);
+      ++ie;
+    }
+    if (is - ie == 1 && nstart == 1) {
+      const int64_t m = (int64_t)(keys[is - 1] & 0xFFFFFFFFull);
+      started_alone = (m - half == x);  // its sample index i + c_k = 0 -> sin(0) = 0 exactly
+    }
+    int64_t nx = n;
+    if (is < hi && sk(is) < nx) nx = sk(is);
+    if (ie < is && ek(ie) + 1 < nx) nx = ek(ie) + 1;
+    if (ie < is) {
+      const double Pv = Ps + Pc, Qv = Qs + Qc;
+      const int64_t u = x, v = nx - 1, L = v - u + 1;
+      const double sl = sin((double)L * al), su = (double)(u + v) * al;
+      const double D = sl * cos(su) / sa, E = sl * sin(su) / sa;
+      const double sss = 0.5 * ((double)L - D), scc = 0.5 * ((double)L + D), ssc = 0.5 * E;
+      two_sum(total, tc, Pv * Pv * sss + Qv * Qv * scc + 2.0 * Pv * Qv * ssc);
+      count += L - (started_alone ? 1 : 0);
+    }
+    if (nx >= n) break;
+    x = nx;
+  }
+  return count > 0 ? (total + tc) / (double)count : __builtin_nan("");
+}
+
+__global__ __launch_bounds__(256) void k_power(const uint64_t* ukeys, const double* uamps, const int64_t* nuniq,
+                                               rt_grid g, int shard, int nshard, PowerParams P, double* power) {
+  const int64_t nc = g.nx * g.ny * g.nz;
+  const int64_t nu = *nuniq;
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nc; c += (int64_t)gridDim.x * blockDim.x) {
+    if (c % nshard != shard) {
+      power[c] = 0.0;  // other ranks own it; the power map is sum-reduced across ranks
+      continue;
+    }
+    // [lo, hi) = unique (cell, bin) keys of this cell
+    const uint64_t k0 = (uint64_t)c << 32, k1 = (uint64_t)(c + 1) << 32;
+    int64_t a = 0, b = nu;
+    while (a < b) {
+      const int64_t m = (a + b) >> 1;
+      if (ukeys[m] < k0) a = m + 1; else b = m;
+    }
+    int64_t lo = a;
+    b = nu;
+    while (a < b) {
+      const int64_t m = (a + b) >> 1;
+      if (ukeys[m] < k1) a = m + 1; else b = m;
+    }
+    power[c] = power_sparse(ukeys, uamps, lo, a, P);
+  }
+}
+
+// power of dense impulse responses (one per row), e.g. from the per-cell reference loop
+__global__ __launch_bounds__(64) void k_power_dense(const double* ir, int64_t rows, PowerParams P, uint64_t* scratch_keys,
+                                                    double* scratch_amps, double* power) {
+  const int64_t row = blockIdx.x;
+  if (row >= rows || threadIdx.x != 0) return;
+  const double* x = ir + row * P.n_bins;
+  uint64_t* kk = scratch_keys + row * P.n_bins;
+  double* aa = scratch_amps + row * P.n_bins;
+  int64_t K = 0;
+  for (int64_t m = 0; m < P.n_bins; ++m)
+    if (x[m] != 0.0) {
+      kk[K] = (uint64_t)m;
+      aa[K] = x[m];
+      ++K;
+    }
+  power[row] = power_sparse(kk, aa, 0, K, P);
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ host side
+struct rt_coverage {
+  int device = 0;
+  const rt_mesh* env = nullptr;
+  int B = 0;
+  int64_t n = 0, ray_offset = 0;
+  rt_grid grid{};
+  double r_rx = 0.1;
+  int shard = 0, nshard = 1;
+  // buffers
+  float* traj = nullptr;  // 7 * B * n floats
+  uint8_t* nseg = nullptr;
+  uint64_t *keys = nullptr, *keys_sorted = nullptr, *okeys = nullptr, *okeys_sorted = nullptr, *ukeys = nullptr;
+  double *oamps = nullptr, *oamps_sorted = nullptr, *uamps = nullptr;
+  uint8_t* win = nullptr;
+  unsigned long long* count = nullptr;
+  int64_t* nuniq = nullptr;
+  int64_t *ray_count = nullptr, *ray_off = nullptr;
+  void* scan_tmp = nullptr;
+  size_t scan_bytes = 0;
+  void* tmp = nullptr;
+  size_t tmp_bytes = 0;
+  int64_t cap = 0;
+  int64_t last_candidates = 0;
+};
+
+namespace {
+
+void free_cands(rt_coverage* c) {
+  for (void* q : {(void*)c->keys, (void*)c->keys_sorted, (void*)c->okeys, (void*)c->okeys_sorted, (void*)c->ukeys,
+                  (void*)c->oamps, (void*)c->oamps_sorted, (void*)c->uamps, (void*)c->win, c->tmp})
+    if (q) (void)hipFree(q);
+  c->keys = c->keys_sorted = c->okeys = c->okeys_sorted = c->ukeys = nullptr;
+  c->oamps = c->oamps_sorted = c->uamps = nullptr;
+  c->win = nullptr;
+  c->tmp = nullptr;
+  c->tmp_bytes = 0;
+  c->cap = 0;
+}
+
+int alloc_cands(rt_coverage* c, int64_t cap) {
+  free_cands(c);
+  RT_HIP(hipMalloc(&c->keys, cap * 8));
+  RT_HIP(hipMalloc(&c->keys_sorted, cap * 8));
+  RT_HIP(hipMalloc(&c->okeys, cap * 8));
+  RT_HIP(hipMalloc(&c->okeys_sorted, cap * 8));
+  RT_HIP(hipMalloc(&c->ukeys, cap * 8));
+  RT_HIP(hipMalloc(&c->oamps, cap * 8));
+  RT_HIP(hipMalloc(&c->oamps_sorted, cap * 8));
+  RT_HIP(hipMalloc(&c->uamps, cap * 8));
+  RT_HIP(hipMalloc(&c->win, cap));
+  size_t b1 = 0, b2 = 0, b3 = 0;
+  RT_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, b1, c->keys, c->keys_sorted, (int)cap, 0, 64));
+  RT_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, b2, c->okeys, c->okeys_sorted, c->oamps, c->oamps_sorted,
+                                            (int)cap, 0, 64));
+  RT_HIP(hipcub::DeviceReduce::ReduceByKey(nullptr, b3, c->okeys_sorted, c->ukeys, c->oamps_sorted, c->uamps,
+                                           c->nuniq, hipcub::Sum(), (int)cap));
+  c->tmp_bytes = std::max(b1, std::max(b2, b3));
+  RT_HIP(hipMalloc(&c->tmp, c->tmp_bytes));
+  c->cap = cap;
+  return RT_OK;
+}
+
+int bits_for(uint64_t v) {
+  int b = 0;
+  while (b < 64 && (v >> b) != 0) ++b;
+  return b;
+}
+}  // namespace
+
+extern "C" {
+
+int rt_coverage_create(int device, const rt_mesh* env, int max_bounces, int64_t n_rays, int64_t ray_offset,
+                       const rt_grid* grid, double rx_radius, int shard_index, int shard_count, rt_coverage** out) {
+  if (!out || !env || !grid || max_bounces < 1 || max_bounces > 15 || n_rays <= 0 || n_rays > (1 << 24) ||
+      shard_count < 1 || shard_index < 0 || shard_index >= shard_count || grid->nx < 1 || grid->ny < 1 || grid->nz < 1 ||
+      rx_radius <= 0) {
+    rt::set_error("rt_coverage_create: invalid arguments (max_bounces 1..15, n_rays 1..2^24 per call)");
+    return RT_EINVAL;
+  }
+  if (env->nf > RT_BRUTE_MAX_FACES) {
+    rt::set_error("rt_coverage_create: environment above RT_BRUTE_MAX_FACES faces needs the BVH path");
+    return RT_EINVAL;
+  }
+  const int64_t nc = grid->nx * grid->ny * grid->nz;
+  if (bits_for((uint64_t)nc) > 32) {
+    rt::set_error("rt_coverage_create: too many cells");
+    return RT_EINVAL;
+  }
+  RT_HIP(hipSetDevice(device));
+  int rc = RT_OK;
+  rt_coverage* c = new rt_coverage();
+  c->device = device;
+  c->env = env;
+  c->B = max_bounces;
+  c->n = n_rays;
+  c->ray_offset = ray_offset;
+  c->grid = *grid;
+  c->r_rx = rx_radius;
+  c->shard = shard_index;
+  c->nshard = shard_count;
+  hipError_t e = hipMalloc(&c->traj, sizeof(float) * 7 * max_bounces * n_rays);
+  if (e == hipSuccess) e = hipMalloc(&c->nseg, n_rays);
+  if (e == hipSuccess) e = hipMalloc(&c->count, 8);
+  if (e == hipSuccess) e = hipMalloc(&c->nuniq, 8);
+  if (e == hipSuccess) e = hipMalloc(&c->ray_count, 8 * n_rays);
+  if (e == hipSuccess) e = hipMalloc(&c->ray_off, 8 * (n_rays + 1));
+  if (e == hipSuccess)
+    e = hipcub::DeviceScan::ExclusiveSum(nullptr, c->scan_bytes, c->ray_count, c->ray_off, (int)n_rays);
+  if (e == hipSuccess) e = hipMalloc(&c->scan_tmp, std::max<size_t>(c->scan_bytes, 16));
+  if (e != hipSuccess) {
+    rt_coverage_destroy(c);
+    return rt::hip_fail(e, "rt_coverage_create");
+  }
+  rc = alloc_cands(c, std::max<int64_t>(1 << 20, 8 * n_rays));
+  if (rc) {
+    rt_coverage_destroy(c);
+    return rc;
+  }
+  *out = c;
+  return RT_OK;
+}
+
+int rt_coverage_destroy(rt_coverage* c) {
+  if (!c) return RT_OK;
+  (void)hipSetDevice(c->device);
+  free_cands(c);
+  if (c->traj) (void)hipFree(c->traj);
+  if (c->nseg) (void)hipFree(c->nseg);
+  if (c->count) (void)hipFree(c->count);
+  if (c->nuniq) (void)hipFree(c->nuniq);
+  if (c->ray_count) (void)hipFree(c->ray_count);
+  if (c->ray_off) (void)hipFree(c->ray_off);
+  if (c->scan_tmp) (void)hipFree(c->scan_tmp);
+  delete c;
+  return RT_OK;
+}
+
+int rt_coverage_run(rt_coverage* c, const float* tx_pos, double tx_power, double light_speed, double sample_rate,
+                    int flags, int64_t n_bins, double alpha, double* power, int64_t* stats, void* stream) {
+  if (!c || !tx_pos || !power || n_bins < 1 || n_bins >= ((int64_t)1 << 32)) {
+    rt::set_error("rt_coverage_run: invalid arguments");
+    return RT_EINVAL;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  RT_HIP(hipSetDevice(c->device));
+  CovParams p{};
+  p.env_perm = c->env->perm;
+  p.env_nrm = c->env->nrm;
+  p.env_nf = (int)c->env->nf;
+  for (int k = 0; k < 3; ++k) p.tx[k] = tx_pos[k];
+  p.B = c->B;
+  p.n = c->n;
+  p.ray_offset = c->ray_offset;
+  p.g = c->grid;
+  p.r_rx = c->r_rx;
+  {
+    // every receiver vertex lies within r of the centre (|unit| = 1 up to rounding); pad for f32/f64 rounding
+    const double amax = fmax(fabs(c->grid.x0) + fabs(c->grid.dx) * (double)c->grid.nx,
+                             fmax(fabs(c->grid.y0) + fabs(c->grid.dy) * (double)c->grid.ny,
+                                  fabs(c->grid.z0) + fabs(c->grid.dz) * (double)c->grid.nz));
+    p.r_pad = c->r_rx * (1.0 + 1e-3) + 1e-5 * (1.0 + amax);
+  }
+  p.shard = c->shard;
+  p.nshard = c->nshard;
+  const int64_t BN = (int64_t)c->B * c->n;
+  p.px = c->traj;
+  p.py = p.px + BN;
+  p.pz = p.py + BN;
+  p.dx = p.pz + BN;
+  p.dy = p.dx + BN;
+  p.dz = p.dy + BN;
+  p.te = p.dz + BN;
+  p.nseg = c->nseg;
+  p.count = c->count;
+  p.amp0 = tx_power / (double)c->n;
+  p.c32 = (float)light_speed;
+  p.fs32 = (float)sample_rate;
+  p.c64 = light_speed;
+  p.fs64 = sample_rate;
+  p.flags = flags;
+  p.n_bins = n_bins;
+  const size_t lds = (size_t)p.env_nf * 18 * sizeof(float4);
+  const unsigned grid_rays = (unsigned)std::min<int64_t>((c->n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_traj, dim3(grid_rays), dim3(256), lds, s, p);
+  RT_HIP(hipGetLastError());
+  // candidates: count per ray, exclusive scan, write
+  hipLaunchKernelGGL(k_cand, dim3(grid_rays), dim3(256), 0, s, p, c->ray_count, (const int64_t*)nullptr);
+  RT_HIP(hipGetLastError());
+  size_t sb = c->scan_bytes;
+  RT_HIP(hipcub::DeviceScan::ExclusiveSum(c->scan_tmp, sb, c->ray_count, c->ray_off, (int)c->n, s));
+  int64_t last[2] = {0, 0};
+  RT_HIP(hipMemcpyAsync(&last[0], c->ray_off + (c->n - 1), 8, hipMemcpyDeviceToHost, s));
+  RT_HIP(hipMemcpyAsync(&last[1], c->ray_count + (c->n - 1), 8, hipMemcpyDeviceToHost, s));
+  RT_HIP(hipStreamSynchronize(s));
+  const int64_t ncand = last[0] + last[1];
+  if (ncand > c->cap) {
+    int rc = alloc_cands(c, ncand + ncand / 4 + 1024);
+    if (rc) return rc;
+  }
+  if (ncand > ((int64_t)1 << 31) - 1) {
+    rt::set_error("rt_coverage_run: more than 2^31 candidates; shard the rays");
+    return RT_EINVAL;
+  }
+  p.keys = c->keys;
+  p.cap = c->cap;
+  if (ncand > 0) {
+    hipLaunchKernelGGL(k_cand, dim3(grid_rays), dim3(256), 0, s, p, (int64_t*)nullptr, (const int64_t*)c->ray_off);
+    RT_HIP(hipGetLastError());
+  }
+  c->last_candidates = ncand;
+  const int64_t ncell = c->grid.nx * c->grid.ny * c->grid.nz;
+  PowerParams P;
+  P.n_bins = n_bins;
+  P.half = (n_bins - 1) / 2;
+  P.alpha = alpha;
+  const unsigned grid_cells = (unsigned)std::min<int64_t>((ncell + 255) / 256, 8192);
+  if (ncand == 0) {
+    RT_HIP(hipMemsetAsync(c->nuniq, 0, 8, s));
+    hipLaunchKernelGGL(k_power, dim3(grid_cells), dim3(256), 0, s, c->ukeys, c->uamps, c->nuniq, c->grid, c->shard,
+                       c->nshard, P, power);
+    RT_HIP(hipGetLastError());
+    if (stats) stats[0] = stats[1] = 0;
+    return RT_OK;
+  }
+  const int endbit = 28 + bits_for((uint64_t)ncell);
+  size_t tb = c->tmp_bytes;
+  RT_HIP(hipcub::DeviceRadixSort::SortKeys(c->tmp, tb, c->keys, c->keys_sorted, (int)ncand, 0, endbit, s));
+  const unsigned grid_c = (unsigned)std::min<int64_t>((ncand + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_win, dim3(grid_c), dim3(256), 0, s, p, c->keys_sorted, ncand, c->win);
+  RT_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_replay, dim3(grid_c), dim3(256), lds, s, p, c->keys_sorted, ncand, c->win, c->okeys, c->oamps);
+  RT_HIP(hipGetLastError());
+  tb = c->tmp_bytes;
+  RT_HIP(hipcub::DeviceRadixSort::SortPairs(c->tmp, tb, c->okeys, c->okeys_sorted, c->oamps, c->oamps_sorted,
+                                            (int)ncand, 0, 64, s));
+  tb = c->tmp_bytes;
+  RT_HIP(hipcub::DeviceReduce::ReduceByKey(c->tmp, tb, c->okeys_sorted, c->ukeys, c->oamps_sorted, c->uamps, c->nuniq,
+                                           hipcub::Sum(), (int)ncand, s));
+  hipLaunchKernelGGL(k_power, dim3(grid_cells), dim3(256), 0, s, c->ukeys, c->uamps, c->nuniq, c->grid, c->shard,
+                     c->nshard, P, power);
+  RT_HIP(hipGetLastError());
+  if (stats) {
+    stats[0] = ncand;
+    stats[1] = c->cap;
+  }
+  return RT_OK;
+}
+
+int rt_coverage_received(rt_coverage* c, uint64_t* keys_out, double* amps_out, int64_t max_out, int64_t* n_out,
+                         void* stream) {
+  // the per-cell sparse impulse responses of the last run: (cell << 32 | bin, amplitude), ascending
+  if (!c || !n_out) {
+    rt::set_error("rt_coverage_received: invalid arguments");
+    return RT_EINVAL;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  int64_t nu = 0;
+  RT_HIP(hipMemcpyAsync(&nu, c->nuniq, 8, hipMemcpyDeviceToHost, s));
+  RT_HIP(hipStreamSynchronize(s));
+  if (c->last_candidates == 0) nu = 0;
+  *n_out = nu;
+  const int64_t m = std::min(nu, max_out);
+  if (m > 0 && keys_out) RT_HIP(hipMemcpyAsync(keys_out, c->ukeys, m * 8, hipMemcpyDeviceToDevice, s));
+  if (m > 0 && amps_out) RT_HIP(hipMemcpyAsync(amps_out, c->uamps, m * 8, hipMemcpyDeviceToDevice, s));
+  return RT_OK;
+}
+
+int rt_power_dense(const double* impulse_responses, int64_t rows, int64_t n_bins, double alpha, void* scratch,
+                   int64_t scratch_bytes, double* power, void* stream) {
+  if (!impulse_responses || rows < 0 || n_bins < 1 || !power || scratch_bytes < rows * n_bins * 16) {
+    rt::set_error("rt_power_dense: invalid arguments (scratch >= rows*n_bins*16 bytes)");
+    return RT_EINVAL;
+  }
+  if (rows == 0) return RT_OK;
+  PowerParams P;
+  P.n_bins = n_bins;
+  P.half = (n_bins - 1) / 2;
+  P.alpha = alpha;
+  uint64_t* kk = (uint64_t*)scratch;
+  double* aa = (double*)(kk + rows * n_bins);
+  hipLaunchKernelGGL(k_power_dense, dim3((unsigned)rows), dim3(64), 0, (hipStream_t)stream, impulse_responses, rows, P,
+                     kk, aa, power);
+  RT_HIP(hipGetLastError());
+  return RT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,102 @@
+"""Coverage map on the GPU (shared-trajectory algorithm) vs the oracle's literal per-cell loop
+(coverage.py:38-57: per cell a full trace + host CIR + np.convolve power).  Needs an MI355X.
+
+Bar: the per-cell sparse impulse responses have identical bins; each cell's impulse response agrees
+within 1e-5 relative norm-wise (max |diff| <= 1e-5 * max |ir|) and its power within 1e-5 relative
+(north_star); cells that receive nothing are NaN in both.  Single entries are compared norm-wise
+because the reference's float32 np.arccos (NumPy SIMD, a few ulp) moves an amplitude whose Fresnel
+factor sits near its zero by more than 1e-5 of itself ("Tolerances")."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+from oracle import oracle as orc  # noqa: E402
+from rf_ray_tracing_warp_amd._lib import check, lib, ptr  # noqa: E402
+from rf_ray_tracing_warp_amd.coverage import Coverage, CoverageGrid, phase_step  # noqa: E402
+from rf_ray_tracing_warp_amd.mesh import load_stl  # noqa: E402
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu(require_gpu):
+    lib()
+
+
+@pytest.fixture(scope="module")
+def room():
+    return load_stl(os.path.join(REPO, "models", "room.stl"))
+
+
+def _compare(cov, grid, env_np, tx, B, N, win=100e-9):
+    power = cov.run(tx, 1).reshape(-1)
+    cells, bins, amps = cov.impulse_responses()
+    E = orc.Mesh(env_np.vertices, env_np.faces)
+    ref_p, ref_irs, ref_cr = orc.coverage_loop(E, tx, grid.centers().reshape(-1, 3), B, N, win=win, with_cr=True)
+    for c in range(grid.num_cells):
+        sel = cells == c
+        rb = np.nonzero(ref_irs[c])[0]
+        np.testing.assert_array_equal(bins[sel], rb, err_msg=f"cell {c}")
+        if len(rb):
+            scale = np.abs(ref_irs[c]).max()
+            assert np.abs(amps[sel] - ref_irs[c][rb]).max() <= 1e-5 * scale, f"cell {c}"
+    np.testing.assert_array_equal(np.isnan(power), np.isnan(ref_p))
+    ok = ~np.isnan(ref_p)
+    # (1) same computation as the reference with the arccos rounded once: agreement to 1e-9
+    np.testing.assert_allclose(power[ok], ref_cr[ok], rtol=1e-9)
+    # (2) vs the reference itself: 1e-5, plus exactly the spread its own float32 arccos rounding causes
+    allowed = 1e-5 * np.abs(ref_p[ok]) + 1.01 * np.abs(ref_cr[ok] - ref_p[ok])
+    assert np.all(np.abs(power[ok] - ref_p[ok]) <= allowed)
+    assert np.mean(np.abs(power[ok] - ref_p[ok]) <= 1e-5 * np.abs(ref_p[ok])) >= 0.9
+    return power, ref_p
+
+
+@pytest.mark.parametrize("grid,tx,B,N", [
+    (CoverageGrid.square(12, 15, 5), (10, 0, 5), 3, 30_000),                  # K3 shape, coarse
+    (CoverageGrid(8.0, -0.5, 4.6, 0.13, 0.11, 0.2, 10, 10, 5), (10, 0, 5), 3, 20_000),  # around/at the TX
+    (CoverageGrid.from_ranges(range(-15, 16, 6), range(-15, 16, 6), range(0, 16, 5)), (10, 0, 5), 2, 20_000),
+])
+def test_coverage_matches_per_cell_loop(room, grid, tx, B, N):
+    cov = Coverage(room, 2.998e8, 100e9, 100e-9, B, N, grid)
+    power, ref = _compare(cov, grid, room, tx, B, N)
+    assert np.isfinite(ref).sum() >= 3  # the test exercises cells that receive paths
+    cov.close()
+
+
+def test_coverage_sharded_sum_equals_whole(room):
+    grid, tx, B, N = CoverageGrid.square(16, 15, 5), (10, 0, 5), 3, 20_000
+    whole = Coverage(room, 2.998e8, 100e9, 100e-9, B, N, grid).run(tx)
+    parts = [Coverage(room, 2.998e8, 100e9, 100e-9, B, N, grid, shard_index=s, shard_count=3).run_device(tx).clone()
+             for s in range(3)]
+    total = (parts[0] + parts[1] + parts[2]).cpu().numpy().reshape(whole.shape)
+    np.testing.assert_array_equal(np.isnan(total), np.isnan(whole))
+    ok = ~np.isnan(whole)
+    np.testing.assert_array_equal(total[ok], whole[ok])
+
+
+def test_power_dense_matches_numpy():
+    rng = np.random.default_rng(3)
+    n, win, rows = 10000, 100e-9, 24
+    irs = np.zeros((rows, n))
+    for r in range(rows):
+        K = int(rng.integers(0, 30))
+        irs[r, rng.choice(n, K, replace=False)] = rng.uniform(1e-8, 1e-5, K)
+    irs[1, :] = 0
+    irs[1, 4999] = 1e-6  # isolated sin(0) sample
+    irs[2, :] = 0
+    irs[2, [0, 9999]] = [2e-6, 3e-6]
+    t = torch.from_numpy(irs).cuda()
+    out = torch.empty(rows, dtype=torch.float64, device="cuda")
+    scratch = torch.empty(rows * n * 16, dtype=torch.uint8, device="cuda")
+    check(lib().rt_power_dense(ptr(t), rows, n, phase_step(win, n), ptr(scratch), scratch.numel(), ptr(out),
+                               torch.cuda.current_stream().cuda_stream))
+    got = out.cpu().numpy()
+    ref = np.array([orc.signal_power(irs[r], win) for r in range(rows)])
+    np.testing.assert_array_equal(np.isnan(got), np.isnan(ref))
+    ok = ~np.isnan(ref)
+    np.testing.assert_allclose(got[ok], ref[ok], rtol=1e-9)
