@@ -41,6 +41,10 @@ def parse():
     ap.add_argument("--bounces", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="rays per CPU-baseline chunk (~10 s total)")
+    ap.add_argument("--no-coverage", action="store_true")
+    ap.add_argument("--coverage-grid", type=int, default=256, help="K3: n x n receiver cells at z=5 on room.stl")
+    ap.add_argument("--coverage-rays", type=int, default=1_000_000)
+    ap.add_argument("--coverage-runs", type=int, default=3)
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_k2.json"),
                     help="per-launch HBM bytes measured by rocprofv3 PMC (profiles/)")
     return ap.parse_args()
@@ -71,6 +75,51 @@ def cpu_baseline(sample_rays, B, tx, rx, min_s=10.0, max_rays=400_000_000):
             "sample": f"{done} rays x {B} bounces (ray ids 0..{done - 1}, chunks of {sample_rays}) of the K2 "
                       f"room.stl burst: trace + host CIR by oracle/rt_oracle.c (OpenMP, {threads} threads), "
                       f"{dt:.1f} s"}
+
+
+def coverage_leg(args, env_m, env, local, rank, world, dist):
+    """K3: coverage.py on room.stl, n x n cells at z = 5, tx (10,0,5), 1M rays per cell, 3 bounces.
+    Cells are sharded cyclically over the ranks; the power map is sum-reduced (RCCL)."""
+    import torch
+    from rf_ray_tracing_warp_amd.coverage import Coverage, CoverageGrid
+
+    grid = CoverageGrid.square(args.coverage_grid, 15.0, 5.0)
+    cov = Coverage(env_m, 2.998e8, 100e9, 100e-9, args.bounces, args.coverage_rays, grid, 0.1, device=local,
+                   shard_index=rank, shard_count=world, env_mesh=env)
+    tx = (10.0, 0.0, 5.0)
+
+    def one():
+        p = cov.run_device(tx, 1)
+        if world > 1:
+            dist.all_reduce(p)
+        return p
+
+    one()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.coverage_runs):
+        p = one()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = (time.perf_counter() - t0) / args.coverage_runs
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t[0])
+    pm = p.cpu().numpy()
+    cand = torch.tensor([float(cov.last_candidates)], dtype=torch.float64, device=f"cuda:{local}")
+    if world > 1:
+        dist.all_reduce(cand)
+    cov.close()
+    return {"metric": "coverage cells/sec", "value": grid.num_cells / dt, "unit": "cells/s", "ms_per_map": dt * 1e3,
+            "workload": f"K3: room.stl, {grid.nx}x{grid.ny} receivers at z=5 (centres -15+(i+1/2)*30/{grid.nx}), "
+                        f"tx (10,0,5), {args.coverage_rays} rays per cell, {args.bounces} bounces, 10000 bins, "
+                        f"signal power per cell; cells sharded cyclically x{world} + RCCL sum of the power map",
+            "scaling": "strong", "cells_receiving": int(np.isfinite(pm).sum()),
+            "candidates": int(cand.item()), "algorithm": "exact shared-trajectory (csrc/coverage.hip)"}
 
 
 def main():
@@ -155,6 +204,10 @@ def main():
         elapsed, kern_ms = float(t[0]), float(t[1])
     received_rows = int(count.item())
 
+    cov_out = None
+    if not args.no_coverage:
+        cov_out = coverage_leg(args, env_m, env, local, rank, world, dist)
+
     if rank == 0:
         bounces = world * N * B * args.steps
         value = bounces / elapsed
@@ -191,6 +244,8 @@ def main():
                          "algorithmic_bytes_per_launch": bytes_per_launch},
             "received_rows_last_step": received_rows,
         }
+        if cov_out is not None:
+            out["coverage"] = cov_out
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_sample, B, tx, rx)
         print(json.dumps(out), flush=True)

@@ -8,12 +8,16 @@
 // environment or the environment missed).  This file:
 //
 //   k_traj    trace every ray once against the environment only: p_k, d_k, t_env_k (SoA in HBM)
-//   k_cand    for every segment (p_k, d_k, [0, min(t_env_k, max_t)]) enumerate the lattice cells
-//             whose (padded) receiver ball it touches -> keys (cell, ray, k)         [capsule raster]
+//   k_cols    for every segment (p_k, d_k, [0, min(t_env_k, max_t)]) and z layer: the lattice
+//             columns its padded capsule crosses -> column items                      [capsule raster]
+//   k_cells   one column item per lane (balanced: a grazing ray's hundreds of cells spread over
+//             many lanes): ball test of the few cells of the column -> keys (cell, ray, k)
 //   sort      radix sort of the keys: candidates grouped by (cell, ray), k ascending
 //   k_win     exact receiver test of each candidate (the cell's icosphere, 80 faces, unrolled)
-//   k_replay  first winning k of each (cell, ray): replay from (p_k, d_k) with the full per-cell
-//             semantics of kernel.py:57-98, then the CIR body of tracer.py:101-117 -> (cell, bin, amp)
+//   k_first   the first winning k of each (cell, ray) -> compact replay list
+//   k_replay  replay from (p_k, d_k) with the full per-cell semantics of kernel.py:57-98, then the
+//             CIR body of tracer.py:101-117 -> (cell, bin, amp)
+// Appends use one atomic per wave (prefix sum of the lanes' counts).
 //   sort + reduce-by-key: per-cell sparse impulse response, bins ascending
 //   k_power   closed-form mean square of the nonzero samples of ir (*) sin(2 pi 2.4e9 t)
 //             ('same' mode, np.nonzero) over the piecewise-constant active-bin intervals
@@ -50,7 +54,10 @@ struct CovParams {
   // trajectory SoA [k][n]
   float *px, *py, *pz, *dx, *dy, *dz, *te;
   uint8_t* nseg;
-  // candidates
+  // column items and candidates (wave-aggregated appends; counts on the device)
+  uint64_t* items;
+  int64_t item_cap;
+  unsigned long long* item_count;
   uint64_t* keys;
   int64_t cap;
   unsigned long long* count;
@@ -181,18 +188,33 @@ __global__ __launch_bounds__(256) void k_traj(CovParams p) {
 }
 
 // ------------------------------------------------------------------ 2. candidate cells per segment
-// Two passes over the same enumeration: COUNT writes the per-ray candidate count, WRITE stores the
-// keys at the exclusive-scan offset of the ray (no atomics, deterministic order).
-struct Emit {
-  bool write;
-  int64_t n;       // candidates emitted so far for this ray
-  uint64_t* dst;   // keys + offset[r] (WRITE)
-  __device__ __forceinline__ void operator()(const CovParams& p, int64_t cell, int64_t r, int k) {
-    if (cell % p.nshard != p.shard) return;
-    if (write) dst[n] = ((uint64_t)cell << 28) | ((uint64_t)r << 4) | (uint64_t)k;
-    ++n;
+// One atomic per 256-thread block: exclusive prefix of the threads' counts (wave scan + LDS),
+// thread 0 reserves the block's total.  Every thread of the block must call it (inactive: c = 0);
+// one same-address atomic per wave measured 1.6 ms for 8.5M keys, per block it is 4x fewer.
+__device__ __forceinline__ unsigned long long block_append(unsigned long long* ctr, unsigned c, unsigned& prefix) {
+  __shared__ unsigned wsum[4];
+  __shared__ unsigned long long bbase;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  unsigned x = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
   }
-};
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  unsigned before = 0;
+  for (int j = 0; j < w; ++j) before += wsum[j];
+  if (threadIdx.x == 0) {
+    const unsigned total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    bbase = total ? atomicAdd(ctr, (unsigned long long)total) : 0ull;
+  }
+  __syncthreads();
+  prefix = before + x - c;
+  const unsigned long long b = bbase;
+  __syncthreads();  // wsum / bbase are reused by the next call
+  return b;
+}
 
 // does the segment x(t) = o + t d, t in [0, tmax] pass within rp of centre c?  (double, conservative)
 __device__ __forceinline__ bool seg_ball(const double o[3], const double d[3], double tmax, const double c[3],
@@ -221,64 +243,132 @@ __device__ __forceinline__ bool slab(double o, double d, double c, double rp, do
   return t0 <= t1;
 }
 
-__global__ __launch_bounds__(256) void k_cand(CovParams p, int64_t* ray_count, const int64_t* ray_offset) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+// geometry of one segment (shared by k_cols and k_cells so both see identical doubles)
+struct Seg {
+  double o[3], d[3], tmax;
+  int A, Bx;  // walk axis (major of |d.x|, |d.y|) and cross axis
+};
+__device__ __forceinline__ Seg load_seg(const CovParams& p, int64_t r, int k) {
+  Seg s;
+  const int64_t o_ = (int64_t)k * p.n + r;
+  s.o[0] = p.px[o_];
+  s.o[1] = p.py[o_];
+  s.o[2] = p.pz[o_];
+  s.d[0] = p.dx[o_];
+  s.d[1] = p.dy[o_];
+  s.d[2] = p.dz[o_];
+  const double te = p.te[o_];
+  s.tmax = te < (double)RT_MAX_T ? te : (double)RT_MAX_T;
+  s.A = fabs(s.d[0]) >= fabs(s.d[1]) ? 0 : 1;
+  s.Bx = 1 - s.A;
+  return s;
+}
+// column range of layer kz: [ia0, ia1] (empty if ia0 > ia1), t-range of the layer slab in ta, tb
+__device__ __forceinline__ void seg_columns(const CovParams& p, const Seg& s, int64_t kz, double& ta, double& tb,
+                                            int64_t& ia0, int64_t& ia1) {
   const rt_grid& g = p.g;
-  const double rp = p.r_pad, rp2 = rp * rp;
-  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < p.n; r += stride) {
-    Emit emit;
-    emit.write = ray_offset != nullptr;
-    emit.n = 0;
-    emit.dst = emit.write ? p.keys + ray_offset[r] : nullptr;
-    const int ns = p.nseg[r];
+  const double rp = p.r_pad;
+  ia0 = 1;
+  ia1 = 0;
+  ta = 0.0;
+  tb = s.tmax;
+  if (!slab(s.o[2], s.d[2], g.z0 + (double)kz * g.dz, rp, ta, tb)) return;
+  const double a0 = s.A == 0 ? g.x0 : g.y0, da = s.A == 0 ? g.dx : g.dy;
+  const int64_t na = s.A == 0 ? g.nx : g.ny;
+  const double qa0 = s.o[s.A] + ta * s.d[s.A], qa1 = s.o[s.A] + tb * s.d[s.A];
+  const double amin = fmin(qa0, qa1) - rp, amax = fmax(qa0, qa1) + rp;
+  if ((amax - a0) / da < -1.0 || (amin - a0) / da > (double)na) return;
+  ia0 = clampi((int64_t)floor((amin - a0) / da), 0, na - 1);
+  ia1 = clampi((int64_t)ceil((amax - a0) / da), 0, na - 1);
+}
+
+// pass A: per ray, the (segment, layer, column) items.  item = r<<40 | k<<36 | kz<<24 | ia
+__global__ __launch_bounds__(256) void k_cols(CovParams p) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < p.n; base += stride) {
+    const int64_t r = base + threadIdx.x;
+    const bool active = r < p.n;
+    unsigned c = 0;
+    const int ns = active ? p.nseg[r] : 0;
     for (int k = 0; k < ns; ++k) {
-      const int64_t o_ = (int64_t)k * p.n + r;
-      const double o[3] = {p.px[o_], p.py[o_], p.pz[o_]};
-      const double d[3] = {p.dx[o_], p.dy[o_], p.dz[o_]};
-      const double te = p.te[o_];
-      const double tmax = te < (double)RT_MAX_T ? te : (double)RT_MAX_T;
-      // dominant lattice walk axis among x/y (z layers are few)
-      for (int64_t kz = 0; kz < g.nz; ++kz) {
-        const double zc = g.z0 + (double)kz * g.dz;
-        double ta = 0.0, tb = tmax;
-        if (!slab(o[2], d[2], zc, rp, ta, tb)) continue;
-        const bool xmajor = fabs(d[0]) >= fabs(d[1]);
-        const int A = xmajor ? 0 : 1, Bx = xmajor ? 1 : 0;
-        const double a0 = A == 0 ? g.x0 : g.y0, da = A == 0 ? g.dx : g.dy;
-        const int64_t na = A == 0 ? g.nx : g.ny;
-        const double b0 = Bx == 0 ? g.x0 : g.y0, db = Bx == 0 ? g.dx : g.dy;
-        const int64_t nb = Bx == 0 ? g.nx : g.ny;
-        const double qa0 = o[A] + ta * d[A], qa1 = o[A] + tb * d[A];
-        const double amin = fmin(qa0, qa1) - rp, amax = fmax(qa0, qa1) + rp;
-        int64_t ia0 = (int64_t)floor((amin - a0) / da), ia1 = (int64_t)ceil((amax - a0) / da);
-        ia0 = clampi(ia0, 0, na - 1);
-        ia1 = clampi(ia1, 0, na - 1);
-        if ((amax - a0) / da < -1.0 || (amin - a0) / da > (double)na) continue;
-        for (int64_t ia = ia0; ia <= ia1; ++ia) {
-          const double ac = a0 + (double)ia * da;
-          double t0 = ta, t1 = tb;
-          if (!slab(o[A], d[A], ac, rp, t0, t1)) continue;
-          const double qb0 = o[Bx] + t0 * d[Bx], qb1 = o[Bx] + t1 * d[Bx];
-          const double bmin = fmin(qb0, qb1) - rp, bmax = fmax(qb0, qb1) + rp;
-          if ((bmax - b0) / db < -1.0 || (bmin - b0) / db > (double)nb) continue;
-          const int64_t ib0 = clampi((int64_t)floor((bmin - b0) / db), 0, nb - 1);
-          const int64_t ib1 = clampi((int64_t)ceil((bmax - b0) / db), 0, nb - 1);
-          for (int64_t ib = ib0; ib <= ib1; ++ib) {
-            const int64_t ix = A == 0 ? ia : ib, iy = A == 0 ? ib : ia;
-            const int64_t cell = (kz * g.ny + iy) * g.nx + ix;
-            double c[3];
-            cell_center(g, cell, c);
-            if (seg_ball(o, d, tmax, c, rp2)) emit(p, cell, r, k);
-          }
-        }
+      const Seg s = load_seg(p, r, k);
+      for (int64_t kz = 0; kz < p.g.nz; ++kz) {
+        double ta, tb;
+        int64_t ia0, ia1;
+        seg_columns(p, s, kz, ta, tb, ia0, ia1);
+        if (ia1 >= ia0) c += (unsigned)(ia1 - ia0 + 1);
       }
     }
-    if (!emit.write) ray_count[r] = emit.n;
+    unsigned pre;
+    const unsigned long long at = block_append(p.item_count, c, pre);
+    int64_t w = (int64_t)(at + pre);
+    for (int k = 0; k < ns; ++k) {
+      const Seg s = load_seg(p, r, k);
+      for (int64_t kz = 0; kz < p.g.nz; ++kz) {
+        double ta, tb;
+        int64_t ia0, ia1;
+        seg_columns(p, s, kz, ta, tb, ia0, ia1);
+        for (int64_t ia = ia0; ia <= ia1; ++ia, ++w)
+          if (w < p.item_cap)
+            p.items[w] = ((uint64_t)r << 40) | ((uint64_t)k << 36) | ((uint64_t)kz << 24) | (uint64_t)ia;
+      }
+    }
+  }
+}
+
+// pass B: one column item per lane -> candidate keys (cell, ray, k) for the cells of our shard
+template <bool WRITE>
+__device__ __forceinline__ unsigned column_cells(const CovParams& p, uint64_t item, uint64_t* dst) {
+  const rt_grid& g = p.g;
+  const double rp = p.r_pad, rp2 = rp * rp;
+  const int64_t r = (int64_t)(item >> 40), ia = (int64_t)(item & 0xFFFFFF), kz = (int64_t)((item >> 24) & 0xFFF);
+  const int k = (int)((item >> 36) & 15);
+  const Seg s = load_seg(p, r, k);
+  double ta, tb;
+  int64_t ia0, ia1;
+  seg_columns(p, s, kz, ta, tb, ia0, ia1);
+  const double a0 = s.A == 0 ? g.x0 : g.y0, da = s.A == 0 ? g.dx : g.dy;
+  const double b0 = s.Bx == 0 ? g.x0 : g.y0, db = s.Bx == 0 ? g.dx : g.dy;
+  const int64_t nb = s.Bx == 0 ? g.nx : g.ny;
+  double t0 = ta, t1 = tb;
+  unsigned c = 0;
+  if (!slab(s.o[s.A], s.d[s.A], a0 + (double)ia * da, rp, t0, t1)) return 0;
+  const double qb0 = s.o[s.Bx] + t0 * s.d[s.Bx], qb1 = s.o[s.Bx] + t1 * s.d[s.Bx];
+  const double bmin = fmin(qb0, qb1) - rp, bmax = fmax(qb0, qb1) + rp;
+  if ((bmax - b0) / db < -1.0 || (bmin - b0) / db > (double)nb) return 0;
+  const int64_t ib0 = clampi((int64_t)floor((bmin - b0) / db), 0, nb - 1);
+  const int64_t ib1 = clampi((int64_t)ceil((bmax - b0) / db), 0, nb - 1);
+  for (int64_t ib = ib0; ib <= ib1; ++ib) {
+    const int64_t ix = s.A == 0 ? ia : ib, iy = s.A == 0 ? ib : ia;
+    const int64_t cell = (kz * g.ny + iy) * g.nx + ix;
+    if (cell % p.nshard != p.shard) continue;
+    double cc[3];
+    cell_center(g, cell, cc);
+    if (seg_ball(s.o, s.d, s.tmax, cc, rp2)) {
+      if (WRITE) dst[c] = ((uint64_t)cell << 28) | ((uint64_t)r << 4) | (uint64_t)k;
+      ++c;
+    }
+  }
+  return c;
+}
+
+__global__ __launch_bounds__(256) void k_cells(CovParams p) {
+  const int64_t nitems = (int64_t)min(*p.item_count, (unsigned long long)p.item_cap);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < nitems; base += stride) {
+    const int64_t i = base + threadIdx.x;
+    const bool active = i < nitems;
+    const uint64_t item = active ? p.items[i] : 0;
+    const unsigned c = active ? column_cells<false>(p, item, nullptr) : 0;
+    unsigned pre;
+    const unsigned long long at = block_append(p.count, c, pre);
+    if (c && (int64_t)(at + pre + c) <= p.cap) column_cells<true>(p, item, p.keys + at + pre);
   }
 }
 
 // ------------------------------------------------------------------ 3. exact receiver test per candidate
-__global__ __launch_bounds__(256) void k_win(CovParams p, const uint64_t* keys, int64_t nkeys, uint8_t* win) {
+__global__ __launch_bounds__(256) void k_win(CovParams p, const uint64_t* keys, int64_t nkeys, uint8_t* win,
+                                             float* trx) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nkeys; i += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t key = keys[i];
     const int64_t cell = (int64_t)(key >> 28), r = (int64_t)((key >> 4) & 0xFFFFFF);
@@ -290,6 +380,7 @@ __global__ __launch_bounds__(256) void k_win(CovParams p, const uint64_t* keys, 
     const rt::Hit hr = rx_query(p.g, cell, p.r_rx, o, d);
     // kernel.py:85 -- receiver wins if hit and (env missed or env strictly farther)
     win[i] = (hr.face >= 0 && (isinf(te) || te > hr.t)) ? 1 : 0;
+    trx[i] = hr.t;
   }
 }
 
@@ -344,21 +435,37 @@ struct PathAcc {
 };
 
 // ------------------------------------------------------------------ 4. replay + CIR body
-__global__ __launch_bounds__(256) void k_replay(CovParams p, const uint64_t* keys, int64_t nkeys, const uint8_t* win,
+// first winning bounce of each (cell, ray) group -> replay list (key indices)
+__global__ __launch_bounds__(256) void k_first(const uint64_t* keys, int64_t nkeys, const uint8_t* win, int64_t* list,
+                                               unsigned long long* list_count) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < nkeys; base += stride) {
+    const int64_t i = base + threadIdx.x;
+    bool first = i < nkeys && win[i] != 0;
+    if (first) {
+      const uint64_t g = keys[i] >> 4;
+      for (int64_t j = i - 1; j >= 0 && (keys[j] >> 4) == g; --j)
+        if (win[j]) {
+          first = false;
+          break;
+        }
+    }
+    unsigned pre;
+    const unsigned long long at = block_append(list_count, first ? 1u : 0u, pre);
+    if (first) list[at + pre] = i;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_replay(CovParams p, const uint64_t* keys, const float* trx,
+                                                const int64_t* list, const unsigned long long* list_count,
                                                 uint64_t* out_key, double* out_amp) {
   extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
   for (int i = threadIdx.x; i < p.env_nf * 18; i += blockDim.x) lds_tab[i] = p.env_perm[i];
   __syncthreads();
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nkeys; i += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t nl = (int64_t)*list_count;
+  for (int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; li < nl; li += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = list[li];
     const uint64_t key = keys[i];
-    bool first = win[i] != 0;
-    for (int64_t j = i - 1; first && j >= 0 && (keys[j] >> 4) == (key >> 4); --j)
-      if (win[j]) first = false;
-    if (!first) {
-      out_key[i] = ~0ull;
-      out_amp[i] = 0.0;
-      continue;
-    }
     const int64_t cell = (int64_t)(key >> 28), r = (int64_t)((key >> 4) & 0xFFFFFF);
     const int k0 = (int)(key & 15);
     PathAcc acc;
@@ -369,32 +476,38 @@ __global__ __launch_bounds__(256) void k_replay(CovParams p, const uint64_t* key
     }
     const int64_t o0 = (int64_t)k0 * p.n + r;
     float3 pos = make_float3(p.px[o0], p.py[o0], p.pz[o0]);
-    float3 dir = make_float3(p.dx[o0], p.dy[o0], p.dz[o0]);
-    float rec_dist = 0.0f;
-    double rec_amp = 0.0;
-    for (int b = k0; b < p.B; ++b) {  // kernel.py:57-98 with this cell's receiver
-      const rt::Shear s = rt::make_shear(pos, dir);
+    const float3 dir = make_float3(p.dx[o0], p.dy[o0], p.dz[o0]);
+    // bounce k0: the receiver wins (k_win) at t = trx[i]
+    pos.x = fmaf(dir.x, trx[i], pos.x);
+    pos.y = fmaf(dir.y, trx[i], pos.y);
+    pos.z = fmaf(dir.z, trx[i], pos.z);
+    acc.add(pos.x, pos.y, pos.z);
+    float rec_dist = acc.dist;
+    double rec_amp = acc.amp;
+    float3 d = dir;
+    for (int b = k0 + 1; b < p.B; ++b) {  // kernel.py:57-98 with this cell's receiver
+      const rt::Shear s = rt::make_shear(pos, d);
       const rt::Hit he = env_query(lds_tab, p.env_nf, s);
-      const rt::Hit hr = rx_query(p.g, cell, p.r_rx, pos, dir);
+      const rt::Hit hr = rx_query(p.g, cell, p.r_rx, pos, d);
       const bool env_hit = he.face >= 0, rx_hit = hr.face >= 0;
       if (rx_hit && (!env_hit || he.t > hr.t)) {
-        pos.x = fmaf(dir.x, hr.t, pos.x);
-        pos.y = fmaf(dir.y, hr.t, pos.y);
-        pos.z = fmaf(dir.z, hr.t, pos.z);
+        pos.x = fmaf(d.x, hr.t, pos.x);
+        pos.y = fmaf(d.y, hr.t, pos.y);
+        pos.z = fmaf(d.z, hr.t, pos.z);
         acc.add(pos.x, pos.y, pos.z);
         rec_dist = acc.dist;  // received_paths = traced prefix through this point (kernel.py:89-90)
         rec_amp = acc.amp;
       } else if (env_hit) {
-        pos.x = fmaf(dir.x, he.t, pos.x);
-        pos.y = fmaf(dir.y, he.t, pos.y);
-        pos.z = fmaf(dir.z, he.t, pos.z);
+        pos.x = fmaf(d.x, he.t, pos.x);
+        pos.y = fmaf(d.y, he.t, pos.y);
+        pos.z = fmaf(d.z, he.t, pos.z);
         acc.add(pos.x, pos.y, pos.z);
         const float4 n4 = p.env_nrm[he.face];
         const float3 n = make_float3(n4.x, n4.y, n4.z);
-        const float sc = 2.0f * rt::dot3(dir, n);
-        dir.x = fmaf(-sc, n.x, dir.x);
-        dir.y = fmaf(-sc, n.y, dir.y);
-        dir.z = fmaf(-sc, n.z, dir.z);
+        const float sc = 2.0f * rt::dot3(d, n);
+        d.x = fmaf(-sc, n.x, d.x);
+        d.y = fmaf(-sc, n.y, d.y);
+        d.z = fmaf(-sc, n.z, d.z);
       } else {
         break;
       }
@@ -412,9 +525,6 @@ __global__ __launch_bounds__(256) void k_replay(CovParams p, const uint64_t* key
     if (bin < p.n_bins && rec_amp != 0.0) {
       out_key[i] = ((uint64_t)cell << 32) | (uint64_t)bin;
       out_amp[i] = rec_amp;
-    } else {
-      out_key[i] = ~0ull;
-      out_amp[i] = 0.0;
     }
   }
 }
@@ -545,11 +655,12 @@ struct rt_coverage {
   uint64_t *keys = nullptr, *keys_sorted = nullptr, *okeys = nullptr, *okeys_sorted = nullptr, *ukeys = nullptr;
   double *oamps = nullptr, *oamps_sorted = nullptr, *uamps = nullptr;
   uint8_t* win = nullptr;
-  unsigned long long* count = nullptr;
+  float* trx = nullptr;
+  int64_t* list = nullptr;
+  uint64_t* items = nullptr;
+  int64_t item_cap = 0;
+  unsigned long long* counters = nullptr;  // [0] candidates, [1] column items, [2] replay list
   int64_t* nuniq = nullptr;
-  int64_t *ray_count = nullptr, *ray_off = nullptr;
-  void* scan_tmp = nullptr;
-  size_t scan_bytes = 0;
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
   int64_t cap = 0;
@@ -560,11 +671,14 @@ namespace {
 
 void free_cands(rt_coverage* c) {
   for (void* q : {(void*)c->keys, (void*)c->keys_sorted, (void*)c->okeys, (void*)c->okeys_sorted, (void*)c->ukeys,
-                  (void*)c->oamps, (void*)c->oamps_sorted, (void*)c->uamps, (void*)c->win, c->tmp})
+                  (void*)c->oamps, (void*)c->oamps_sorted, (void*)c->uamps, (void*)c->win, (void*)c->trx,
+                  (void*)c->list, c->tmp})
     if (q) (void)hipFree(q);
   c->keys = c->keys_sorted = c->okeys = c->okeys_sorted = c->ukeys = nullptr;
   c->oamps = c->oamps_sorted = c->uamps = nullptr;
   c->win = nullptr;
+  c->trx = nullptr;
+  c->list = nullptr;
   c->tmp = nullptr;
   c->tmp_bytes = 0;
   c->cap = 0;
@@ -581,6 +695,8 @@ int alloc_cands(rt_coverage* c, int64_t cap) {
   RT_HIP(hipMalloc(&c->oamps_sorted, cap * 8));
   RT_HIP(hipMalloc(&c->uamps, cap * 8));
   RT_HIP(hipMalloc(&c->win, cap));
+  RT_HIP(hipMalloc(&c->trx, cap * 4));
+  RT_HIP(hipMalloc(&c->list, cap * 8));
   size_t b1 = 0, b2 = 0, b3 = 0;
   RT_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, b1, c->keys, c->keys_sorted, (int)cap, 0, 64));
   RT_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, b2, c->okeys, c->okeys_sorted, c->oamps, c->oamps_sorted,
@@ -590,6 +706,14 @@ int alloc_cands(rt_coverage* c, int64_t cap) {
   c->tmp_bytes = std::max(b1, std::max(b2, b3));
   RT_HIP(hipMalloc(&c->tmp, c->tmp_bytes));
   c->cap = cap;
+  return RT_OK;
+}
+
+int alloc_items(rt_coverage* c, int64_t cap) {
+  if (c->items) (void)hipFree(c->items);
+  c->items = nullptr;
+  RT_HIP(hipMalloc(&c->items, cap * 8));
+  c->item_cap = cap;
   return RT_OK;
 }
 
@@ -633,18 +757,14 @@ int rt_coverage_create(int device, const rt_mesh* env, int max_bounces, int64_t 
   c->nshard = shard_count;
   hipError_t e = hipMalloc(&c->traj, sizeof(float) * 7 * max_bounces * n_rays);
   if (e == hipSuccess) e = hipMalloc(&c->nseg, n_rays);
-  if (e == hipSuccess) e = hipMalloc(&c->count, 8);
+  if (e == hipSuccess) e = hipMalloc(&c->counters, 32);
   if (e == hipSuccess) e = hipMalloc(&c->nuniq, 8);
-  if (e == hipSuccess) e = hipMalloc(&c->ray_count, 8 * n_rays);
-  if (e == hipSuccess) e = hipMalloc(&c->ray_off, 8 * (n_rays + 1));
-  if (e == hipSuccess)
-    e = hipcub::DeviceScan::ExclusiveSum(nullptr, c->scan_bytes, c->ray_count, c->ray_off, (int)n_rays);
-  if (e == hipSuccess) e = hipMalloc(&c->scan_tmp, std::max<size_t>(c->scan_bytes, 16));
   if (e != hipSuccess) {
     rt_coverage_destroy(c);
     return rt::hip_fail(e, "rt_coverage_create");
   }
   rc = alloc_cands(c, std::max<int64_t>(1 << 20, 8 * n_rays));
+  if (!rc) rc = alloc_items(c, std::max<int64_t>(1 << 20, 8 * n_rays));
   if (rc) {
     rt_coverage_destroy(c);
     return rc;
@@ -659,11 +779,9 @@ int rt_coverage_destroy(rt_coverage* c) {
   free_cands(c);
   if (c->traj) (void)hipFree(c->traj);
   if (c->nseg) (void)hipFree(c->nseg);
-  if (c->count) (void)hipFree(c->count);
+  if (c->counters) (void)hipFree(c->counters);
   if (c->nuniq) (void)hipFree(c->nuniq);
-  if (c->ray_count) (void)hipFree(c->ray_count);
-  if (c->ray_off) (void)hipFree(c->ray_off);
-  if (c->scan_tmp) (void)hipFree(c->scan_tmp);
+  if (c->items) (void)hipFree(c->items);
   delete c;
   return RT_OK;
 }
@@ -704,7 +822,8 @@ int rt_coverage_run(rt_coverage* c, const float* tx_pos, double tx_power, double
   p.dz = p.dy + BN;
   p.te = p.dz + BN;
   p.nseg = c->nseg;
-  p.count = c->count;
+  p.count = c->counters;
+  p.item_count = c->counters + 1;
   p.amp0 = tx_power / (double)c->n;
   p.c32 = (float)light_speed;
   p.fs32 = (float)sample_rate;
@@ -716,29 +835,39 @@ int rt_coverage_run(rt_coverage* c, const float* tx_pos, double tx_power, double
   const unsigned grid_rays = (unsigned)std::min<int64_t>((c->n + 255) / 256, 4096);
   hipLaunchKernelGGL(k_traj, dim3(grid_rays), dim3(256), lds, s, p);
   RT_HIP(hipGetLastError());
-  // candidates: count per ray, exclusive scan, write
-  hipLaunchKernelGGL(k_cand, dim3(grid_rays), dim3(256), 0, s, p, c->ray_count, (const int64_t*)nullptr);
-  RT_HIP(hipGetLastError());
-  size_t sb = c->scan_bytes;
-  RT_HIP(hipcub::DeviceScan::ExclusiveSum(c->scan_tmp, sb, c->ray_count, c->ray_off, (int)c->n, s));
-  int64_t last[2] = {0, 0};
-  RT_HIP(hipMemcpyAsync(&last[0], c->ray_off + (c->n - 1), 8, hipMemcpyDeviceToHost, s));
-  RT_HIP(hipMemcpyAsync(&last[1], c->ray_count + (c->n - 1), 8, hipMemcpyDeviceToHost, s));
-  RT_HIP(hipStreamSynchronize(s));
-  const int64_t ncand = last[0] + last[1];
-  if (ncand > c->cap) {
+  // candidates: column items (pass A) then cells (pass B); grow and retry on overflow
+  int64_t ncand = 0;
+  const unsigned grid_items = 4096;
+  for (int attempt = 0;; ++attempt) {
+    p.items = c->items;
+    p.item_cap = c->item_cap;
+    p.keys = c->keys;
+    p.cap = c->cap;
+    RT_HIP(hipMemsetAsync(c->counters, 0, 32, s));
+    hipLaunchKernelGGL(k_cols, dim3(grid_rays), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(k_cells, dim3(grid_items), dim3(256), 0, s, p);
+    RT_HIP(hipGetLastError());
+    unsigned long long h[2] = {0, 0};
+    RT_HIP(hipMemcpyAsync(h, c->counters, 16, hipMemcpyDeviceToHost, s));
+    RT_HIP(hipStreamSynchronize(s));
+    ncand = (int64_t)h[0];
+    const int64_t nitems = (int64_t)h[1];
+    if (ncand <= c->cap && nitems <= c->item_cap) break;
+    if (attempt >= 3) {
+      rt::set_error("rt_coverage_run: candidate buffers keep overflowing");
+      return RT_EHIP;
+    }
+    if (nitems > c->item_cap) {
+      int rc = alloc_items(c, nitems + nitems / 4 + 1024);
+      if (rc) return rc;
+      continue;  // keys were produced from a truncated item list: redo
+    }
     int rc = alloc_cands(c, ncand + ncand / 4 + 1024);
     if (rc) return rc;
   }
   if (ncand > ((int64_t)1 << 31) - 1) {
     rt::set_error("rt_coverage_run: more than 2^31 candidates; shard the rays");
     return RT_EINVAL;
-  }
-  p.keys = c->keys;
-  p.cap = c->cap;
-  if (ncand > 0) {
-    hipLaunchKernelGGL(k_cand, dim3(grid_rays), dim3(256), 0, s, p, (int64_t*)nullptr, (const int64_t*)c->ray_off);
-    RT_HIP(hipGetLastError());
   }
   c->last_candidates = ncand;
   const int64_t ncell = c->grid.nx * c->grid.ny * c->grid.nz;
@@ -759,9 +888,11 @@ int rt_coverage_run(rt_coverage* c, const float* tx_pos, double tx_power, double
   size_t tb = c->tmp_bytes;
   RT_HIP(hipcub::DeviceRadixSort::SortKeys(c->tmp, tb, c->keys, c->keys_sorted, (int)ncand, 0, endbit, s));
   const unsigned grid_c = (unsigned)std::min<int64_t>((ncand + 255) / 256, 8192);
-  hipLaunchKernelGGL(k_win, dim3(grid_c), dim3(256), 0, s, p, c->keys_sorted, ncand, c->win);
-  RT_HIP(hipGetLastError());
-  hipLaunchKernelGGL(k_replay, dim3(grid_c), dim3(256), lds, s, p, c->keys_sorted, ncand, c->win, c->okeys, c->oamps);
+  hipLaunchKernelGGL(k_win, dim3(grid_c), dim3(256), 0, s, p, c->keys_sorted, ncand, c->win, c->trx);
+  hipLaunchKernelGGL(k_first, dim3(grid_c), dim3(256), 0, s, c->keys_sorted, ncand, c->win, c->list, c->counters + 2);
+  RT_HIP(hipMemsetAsync(c->okeys, 0xFF, ncand * 8, s));
+  hipLaunchKernelGGL(k_replay, dim3(grid_c), dim3(256), lds, s, p, c->keys_sorted, c->trx, c->list, c->counters + 2,
+                     c->okeys, c->oamps);
   RT_HIP(hipGetLastError());
   tb = c->tmp_bytes;
   RT_HIP(hipcub::DeviceRadixSort::SortPairs(c->tmp, tb, c->okeys, c->okeys_sorted, c->oamps, c->oamps_sorted,
