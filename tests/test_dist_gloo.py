@@ -1,0 +1,99 @@
+"""World-size-2 runs of the multi-rank logic on CPU (gloo): ray shards and cell shards reduce to
+the single-process result.  The per-rank compute is the CPU oracle here (no GPU); on the GPU the
+same dist.py functions carry the HIP results over RCCL."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from oracle import oracle as orc
+from rf_ray_tracing_warp_amd import dist as rdist
+from rf_ray_tracing_warp_amd.mesh import load_stl, sphere
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TX, RX, B, N_PER = (10.0, 0.0, 5.0), (5.0, 3.0, 4.0), 3, 40_000
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _ray_worker(rank, world, port, out):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    env = load_stl(os.path.join(REPO, "models", "room.stl"))
+    rxm = sphere(RX, 0.1, 1)
+    off, n = rdist.ray_shard(rank, world, N_PER)
+    o = orc.trace(orc.Mesh(env.vertices, env.faces), orc.Mesh(rxm.vertices, rxm.faces), TX, B, off, n,
+                  want_traced=False, nthreads=2)
+    paths = orc.clean_paths(o["received"], o["mask"])
+    ir = torch.from_numpy(orc.cir_from_paths(paths, 1, N_PER * world, 2.998e8, 100e9, 100e-9))
+    rdist.reduce_sum(ir)
+    if rank == 0:
+        out.put(ir.numpy())
+    dist.destroy_process_group()
+
+
+def test_ray_shards_sum_to_single_process():
+    world = 2
+    q = mp.get_context("spawn").SimpleQueue()
+    pc = mp.spawn(_ray_worker, args=(world, _port(), q), nprocs=world, join=False)
+    got = q.get()  # read before join: the child's queue feeder must drain first
+    pc.join()
+    env = load_stl(os.path.join(REPO, "models", "room.stl"))
+    rxm = sphere(RX, 0.1, 1)
+    o = orc.trace(orc.Mesh(env.vertices, env.faces), orc.Mesh(rxm.vertices, rxm.faces), TX, B, 0, N_PER * world,
+                  want_traced=False)
+    ref = orc.cir_from_paths(orc.clean_paths(o["received"], o["mask"]), 1, N_PER * world, 2.998e8, 100e9, 100e-9)
+    assert np.count_nonzero(ref) > 0
+    np.testing.assert_array_equal(np.nonzero(got)[0], np.nonzero(ref)[0])
+    np.testing.assert_allclose(got, ref, rtol=1e-12)
+
+
+def _cell_worker(rank, world, port, out):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    env = load_stl(os.path.join(REPO, "models", "room.stl"))
+    E = orc.Mesh(env.vertices, env.faces)
+    centers = np.array([[x, y, 5.0] for x in (6.0, 8.0, 9.5) for y in (-1.0, 0.5, 2.0)])
+    pm = np.zeros(len(centers))
+    mine = [c for c in range(len(centers)) if rdist.owns_cell(c, rank, world)]
+    p, _ = orc.coverage_loop(E, TX, centers[mine], B, 20_000, nthreads=2)
+    pm[mine] = p
+    t = torch.from_numpy(pm)
+    rdist.reduce_sum(t)
+    if rank == 0:
+        out.put(t.numpy())
+    dist.destroy_process_group()
+
+
+def test_cell_shards_sum_to_single_process():
+    world = 2
+    q = mp.get_context("spawn").SimpleQueue()
+    pc = mp.spawn(_cell_worker, args=(world, _port(), q), nprocs=world, join=False)
+    got = q.get()
+    pc.join()
+    env = load_stl(os.path.join(REPO, "models", "room.stl"))
+    centers = np.array([[x, y, 5.0] for x in (6.0, 8.0, 9.5) for y in (-1.0, 0.5, 2.0)])
+    ref, _ = orc.coverage_loop(orc.Mesh(env.vertices, env.faces), TX, centers, B, 20_000)
+    np.testing.assert_array_equal(np.isnan(got), np.isnan(ref))
+    ok = ~np.isnan(ref)
+    assert ok.sum() >= 3
+    np.testing.assert_array_equal(got[ok], ref[ok])
+
+
+def test_shard_helpers():
+    assert rdist.ray_shard(3, 8, 1000) == (3000, 1000)
+    owners = [sum(rdist.owns_cell(c, r, 8) for r in range(8)) for c in range(100)]
+    assert owners == [1] * 100
