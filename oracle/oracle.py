@@ -52,6 +52,7 @@ def lib():
         L.orc_query_bulk.restype = ctypes.c_int
         L.orc_query_bulk.argtypes = [ctypes.c_void_p, _f32p, _f32p, ctypes.c_int64, ctypes.c_float,
                                      _f32p, _i32p, _f32p]
+        L.orc_set_bvh_min.argtypes = [ctypes.c_int64]
         L.orc_pcg.restype = ctypes.c_uint32
         L.orc_pcg.argtypes = [ctypes.c_uint32]
         _lib = L
@@ -63,12 +64,14 @@ def _p(a, t):
 
 
 class Mesh:
-    """A prepared triangle mesh inside the oracle."""
+    """A prepared triangle mesh inside the oracle (median-split BVH above ``bvh_min`` faces)."""
 
-    def __init__(self, vertices, faces):
+    def __init__(self, vertices, faces, bvh_min=2048):
         self.v = np.ascontiguousarray(np.asarray(vertices, dtype=np.float64).astype(np.float32)).reshape(-1, 3)
         self.f = np.ascontiguousarray(np.asarray(faces).astype(np.int32)).reshape(-1, 3)
+        lib().orc_set_bvh_min(int(bvh_min))
         self.h = lib().orc_mesh_create(_p(self.v, _f32p), len(self.v), _p(self.f, _i32p), len(self.f))
+        lib().orc_set_bvh_min(2048)
 
     def __del__(self):
         if getattr(self, "h", None) and _lib is not None:

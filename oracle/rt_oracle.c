@@ -138,11 +138,95 @@ static inline void cross3(const float* a, const float* b, float* o)
     o[2] = fmaf(a[0], b[1], -(a[1] * b[0]));
 }
 
-/* prepared mesh: per face the three corners (9 floats) and the unit normal (3 floats) */
+/* prepared mesh: per face the three corners (9 floats) and the unit normal (3 floats); meshes
+ * above ORC_BVH_MIN faces also get a simple median-split BVH (double boxes, padded), written
+ * independently of the product's SAH BVH -- the closest hit does not depend on the tree. */
+static int64_t ORC_BVH_MIN = 2048;
+void orc_set_bvh_min(int64_t n) { ORC_BVH_MIN = n; }
+#define ORC_LEAF 8
+typedef struct {
+    double lo[3], hi[3];
+    int64_t left, right; /* internal: child node ids; leaf: left = -1, right unused */
+    int64_t first, count;
+} orc_node;
 typedef struct {
     int64_t nf;
     float* tri; /* nf * 12 */
+    orc_node* nodes;
+    int64_t nnodes;
+    int64_t* order; /* leaf-ordered face ids */
 } orc_mesh;
+
+static double orc_cen(const orc_mesh* m, int64_t f, int k)
+{
+    const float* T = m->tri + 12 * f;
+    return ((double)T[k] + (double)T[3 + k] + (double)T[6 + k]) / 3.0;
+}
+static int64_t orc_build(orc_mesh* m, int64_t first, int64_t count, double pad, int64_t* cap)
+{
+    if (m->nnodes == *cap) {
+        *cap *= 2;
+        m->nodes = (orc_node*)realloc(m->nodes, sizeof(orc_node) * (size_t)(*cap));
+    }
+    const int64_t id = m->nnodes++;
+    orc_node nd;
+    for (int k = 0; k < 3; ++k) {
+        nd.lo[k] = INFINITY;
+        nd.hi[k] = -INFINITY;
+    }
+    for (int64_t i = first; i < first + count; ++i) {
+        const float* T = m->tri + 12 * m->order[i];
+        for (int v = 0; v < 3; ++v)
+            for (int k = 0; k < 3; ++k) {
+                if (T[3 * v + k] < nd.lo[k]) nd.lo[k] = T[3 * v + k];
+                if (T[3 * v + k] > nd.hi[k]) nd.hi[k] = T[3 * v + k];
+            }
+    }
+    for (int k = 0; k < 3; ++k) {
+        nd.lo[k] -= pad;
+        nd.hi[k] += pad;
+    }
+    nd.first = first;
+    nd.count = count;
+    nd.left = nd.right = -1;
+    if (count > ORC_LEAF) {
+        int axis = 0;
+        double ext = nd.hi[0] - nd.lo[0];
+        for (int k = 1; k < 3; ++k)
+            if (nd.hi[k] - nd.lo[k] > ext) {
+                ext = nd.hi[k] - nd.lo[k];
+                axis = k;
+            }
+        /* median split by centroid: simple insertion-free nth-element via qsort on keys */
+        int64_t half = count / 2;
+        /* selection by repeated partition (quickselect) on order[first .. first+count) */
+        int64_t lo = first, hi = first + count - 1, kth = first + half;
+        while (lo < hi) {
+            const double pv = orc_cen(m, m->order[(lo + hi) / 2], axis);
+            int64_t i = lo, j = hi;
+            while (i <= j) {
+                while (orc_cen(m, m->order[i], axis) < pv) ++i;
+                while (orc_cen(m, m->order[j], axis) > pv) --j;
+                if (i <= j) {
+                    int64_t t = m->order[i];
+                    m->order[i] = m->order[j];
+                    m->order[j] = t;
+                    ++i;
+                    --j;
+                }
+            }
+            if (kth <= j) hi = j;
+            else if (kth >= i) lo = i;
+            else break;
+        }
+        const int64_t l = orc_build(m, first, half, pad, cap);
+        const int64_t r = orc_build(m, first + half, count - half, pad, cap);
+        nd.left = l;
+        nd.right = r;
+    }
+    m->nodes[id] = nd;
+    return id;
+}
 
 orc_mesh* orc_mesh_create(const float* verts, int64_t nv, const int32_t* faces, int64_t nf)
 {
@@ -171,12 +255,27 @@ orc_mesh* orc_mesh_create(const float* verts, int64_t nv, const int32_t* faces, 
             T[9] = T[10] = T[11] = 0.0f;
         }
     }
+    m->nodes = NULL;
+    m->nnodes = 0;
+    m->order = NULL;
+    if (nf > ORC_BVH_MIN) {
+        double amax = 0.0;
+        for (int64_t i = 0; i < 12 * nf; ++i)
+            if (i % 12 < 9 && fabs(m->tri[i]) > amax) amax = fabs(m->tri[i]);
+        m->order = (int64_t*)malloc(sizeof(int64_t) * (size_t)nf);
+        for (int64_t f = 0; f < nf; ++f) m->order[f] = f;
+        int64_t cap = 1024;
+        m->nodes = (orc_node*)malloc(sizeof(orc_node) * (size_t)cap);
+        orc_build(m, 0, nf, 1e-4 * (1.0 + amax), &cap);
+    }
     return m;
 }
 void orc_mesh_destroy(orc_mesh* m)
 {
     if (!m) return;
     free(m->tri);
+    free(m->nodes);
+    free(m->order);
     free(m);
 }
 
@@ -243,7 +342,41 @@ static int orc_tri_test(const float* o, const orc_shear* s, const float* a, cons
     return 1;
 }
 
-/* closest hit, brute force over every triangle (mesh_query_ray, kernel.py:71,82) */
+/* double slab test with slack; returns entry t or INFINITY */
+static double orc_slab(const orc_node* nd, const float* o, const float* d)
+{
+    double tn = 0.0, tf = INFINITY;
+    for (int k = 0; k < 3; ++k) {
+        if (d[k] == 0.0f) {
+            if (o[k] < nd->lo[k] || o[k] > nd->hi[k]) return INFINITY;
+            continue;
+        }
+        double a = (nd->lo[k] - o[k]) / (double)d[k], b = (nd->hi[k] - o[k]) / (double)d[k];
+        if (a > b) {
+            double t = a;
+            a = b;
+            b = t;
+        }
+        if (a > tn) tn = a;
+        if (b < tf) tf = b;
+    }
+    return tn <= tf ? tn : INFINITY;
+}
+
+static void orc_consider(const orc_mesh* m, const orc_shear* sh, const float* o, int64_t f, float max_t,
+                         float* best_t, int64_t* best_f)
+{
+    const float* T = m->tri + 12 * f;
+    float t;
+    if (!orc_tri_test(o, sh, T, T + 3, T + 6, &t)) return;
+    if (!(t < max_t && t >= 0.0f)) return;
+    if (*best_f < 0 || t < *best_t || (t == *best_t && f < *best_f)) {
+        *best_t = t;
+        *best_f = f;
+    }
+}
+
+/* closest hit (mesh_query_ray, kernel.py:71,82): brute force, or the oracle BVH when present */
 int orc_query(const orc_mesh* m, const float* o, const float* d, float max_t, float* t_out,
               int32_t* face_out, float* n_out)
 {
@@ -251,6 +384,29 @@ int orc_query(const orc_mesh* m, const float* o, const float* d, float max_t, fl
     orc_shear_init(d, &sh);
     float best_t = 0.0f;
     int64_t best_f = -1;
+    if (m->nodes) {
+        int64_t stack[256];
+        int sp = 0;
+        stack[sp++] = 0;
+        while (sp > 0) {
+            const orc_node* nd = &m->nodes[stack[--sp]];
+            const double te = orc_slab(nd, o, d);
+            if (te == INFINITY) continue;
+            if (best_f >= 0 && te > (double)best_t * (1.0 + 1e-6) + 1e-6) continue;
+            if (nd->left < 0) {
+                for (int64_t i = nd->first; i < nd->first + nd->count; ++i)
+                    orc_consider(m, &sh, o, m->order[i], max_t, &best_t, &best_f);
+            } else {
+                stack[sp++] = nd->left;
+                stack[sp++] = nd->right;
+            }
+        }
+        if (best_f < 0) return 0;
+        *t_out = best_t;
+        *face_out = (int32_t)best_f;
+        memcpy(n_out, m->tri + 12 * best_f + 9, 12);
+        return 1;
+    }
     for (int64_t f = 0; f < m->nf; ++f) {
         const float* T = m->tri + 12 * f;
         float t;

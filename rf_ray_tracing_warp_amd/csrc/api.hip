@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../../include/rfrt.h"
+#include "rt_bvh.h"
 #include "rt_device.h"
 #include "rt_internal.h"
 
@@ -135,7 +136,6 @@ int rt_mesh_destroy(rt_mesh* m) {
   if (m->perm) (void)hipFree(m->perm);
   if (m->nrm) (void)hipFree(m->nrm);
   if (m->nodes) (void)hipFree(m->nodes);
-  if (m->leaf_faces) (void)hipFree(m->leaf_faces);
   delete m;
   return RT_OK;
 }
@@ -162,10 +162,6 @@ int rt_trace(const rt_mesh* env, const float* tx_pos, const rt_mesh* rx, int max
              float* traced, float* received, uint32_t* row_mask, int32_t* hit_kind, int32_t* hit_face, void* stream) {
   if (!env || !tx_pos || max_bounces < 0 || n < 0 || ray_offset < 0) {
     rt::set_error("rt_trace: invalid arguments");
-    return RT_EINVAL;
-  }
-  if (env->nf > RT_BRUTE_MAX_FACES) {
-    rt::set_error("rt_trace: environment meshes above RT_BRUTE_MAX_FACES faces need the BVH kernel");
     return RT_EINVAL;
   }
   if (rx && rx->nf > (int64_t)1 << 24) {
@@ -204,6 +200,16 @@ __global__ void k_dirs(int64_t off, int64_t n, float* out) {
   out[3 * i + 1] = d.y;
   out[3 * i + 2] = d.z;
 }
+__global__ void k_query_bvh(rt::BvhView bv, const float* o, const float* d, int64_t n, float* t, int32_t* face) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float3 oo = make_float3(o[3 * i], o[3 * i + 1], o[3 * i + 2]);
+  const float3 dd = make_float3(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
+  const rt::Shear s = rt::make_shear(oo, dd);
+  const rt::Hit h = rt::bvh_query(bv, s, oo, dd);
+  t[i] = h.face >= 0 ? h.t : __builtin_nanf("");
+  face[i] = h.face;
+}
 __global__ void k_query(const float4* perm, int nf, const float* o, const float* d, int64_t n, float* t, int32_t* face) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -241,8 +247,14 @@ int rt_query(const rt_mesh* m, const float* o, const float* d, int64_t n, float*
     return RT_EINVAL;
   }
   if (n == 0) return RT_OK;
-  hipLaunchKernelGGL(k_query, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, m->perm, (int)m->nf,
-                     o, d, n, t, face);
+  if (m->nodes) {
+    rt::BvhView bv{(const float4*)m->nodes, (const int2*)m->leaves, (const float4*)m->lperm, m->lface};
+    hipLaunchKernelGGL(k_query_bvh, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, bv, o, d, n,
+                       t, face);
+  } else {
+    hipLaunchKernelGGL(k_query, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, m->perm,
+                       (int)m->nf, o, d, n, t, face);
+  }
   RT_HIP(hipGetLastError());
   return RT_OK;
 }

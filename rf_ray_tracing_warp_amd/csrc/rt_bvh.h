@@ -1,0 +1,125 @@
+// rt_bvh.h -- BVH traversal for large environment meshes (the BVH behind wp.Mesh, tracer.py:24,
+// and the traversal inside wp.mesh_query_ray, kernel.py:82).
+//
+// Layout (built on the host by bvh.hip, HBM-resident):
+//   nodes  float4[nnodes][4]: child boxes c0 = (lo.xyz, hi.xyz), c1 = ..., then child ids:
+//          q0 = (c0lo.x, c0lo.y, c0lo.z, c0hi.x)  q1 = (c0hi.y, c0hi.z, c1lo.x, c1lo.y)
+//          q2 = (c1lo.z, c1hi.x, c1hi.y, c1hi.z)  q3 = (child0, child1, -, -) as int bits
+//          child >= 0: internal node index;  child < 0: leaf -1-child into `leaves`
+//   leaves int2[nleaves]: (first, count) into the leaf-ordered face arrays
+//   lperm  float4[nf][6][3]: permuted-corner records (as rt_mesh.perm) in leaf order
+//   lface  int[nf]: original face id of each leaf-ordered face
+// Boxes are padded outward on the host so the f32 slab test below can never cull a face the
+// watertight test would hit; the closest hit is the lexicographic (t, original face id) minimum,
+// so traversal order cannot change a result (bit-exact vs the brute-force oracle).
+#pragma once
+#include "rt_device.h"
+
+namespace rt {
+
+struct BvhView {
+  const float4* nodes;
+  const int2* leaves;
+  const float4* lperm;
+  const int* lface;
+};
+
+#define RT_BVH_STACK 64
+
+struct RayBox {
+  float ox, oy, oz, ix, iy, iz;  // origin and per-axis reciprocal direction (never 0/NaN)
+};
+
+__device__ __forceinline__ float safe_rcp(float d) {
+  const float m = fabsf(d) < 1e-30f ? copysignf(1e-30f, d) : d;
+  return 1.0f / m;
+}
+
+__device__ __forceinline__ RayBox make_raybox(float3 o, float3 d) {
+  RayBox r;
+  r.ox = o.x;
+  r.oy = o.y;
+  r.oz = o.z;
+  r.ix = safe_rcp(d.x);
+  r.iy = safe_rcp(d.y);
+  r.iz = safe_rcp(d.z);
+  return r;
+}
+
+// slab test, returns entry t (clamped at 0) or +inf on a miss; conservative slack on both ends
+__device__ __forceinline__ float slab(const RayBox& r, float lx, float ly, float lz, float hx, float hy, float hz) {
+  const float tx0 = (lx - r.ox) * r.ix, tx1 = (hx - r.ox) * r.ix;
+  const float ty0 = (ly - r.oy) * r.iy, ty1 = (hy - r.oy) * r.iy;
+  const float tz0 = (lz - r.oz) * r.iz, tz1 = (hz - r.oz) * r.iz;
+  const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+  const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+  return tn <= tf * 1.00001f + 1e-6f ? tn : INFINITY;
+}
+
+// closest hit in a BVH mesh (same result as brute force over all faces)
+__device__ __forceinline__ Hit bvh_query(const BvhView& b, const Shear& s, float3 o, float3 d) {
+  Hit h;
+  hit_init(h);
+  const RayBox r = make_raybox(o, d);
+  int stack[RT_BVH_STACK];
+  float stackt[RT_BVH_STACK];
+  int sp = 0;
+  int cur = 0;
+  while (true) {
+    const float4 q0 = b.nodes[4 * cur + 0], q1 = b.nodes[4 * cur + 1];
+    const float4 q2 = b.nodes[4 * cur + 2], q3 = b.nodes[4 * cur + 3];
+    const int c0 = __float_as_int(q3.x), c1 = __float_as_int(q3.y);
+    float t0 = slab(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y);
+    float t1 = slab(r, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w);
+    // leaves are tested on the spot
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+      const int c = side ? c1 : c0;
+      float& tt = side ? t1 : t0;
+      if (c < 0 && tt <= h.t * 1.00001f + 1e-6f) {
+        const int2 lf = b.leaves[-1 - c];
+        for (int j = lf.x; j < lf.x + lf.y; ++j) {
+          const float4* p = b.lperm + (int64_t)j * 18 + s.kcase * 3;
+          float T, det;
+          if (tri_test(s, p[0], p[1], p[2].x, T, det)) hit_consider(h, T, det, b.lface[j]);
+        }
+        tt = INFINITY;
+      } else if (c < 0) {
+        tt = INFINITY;
+      }
+    }
+    const float lim = h.t * 1.00001f + 1e-6f;
+    const bool h0 = t0 <= lim, h1 = t1 <= lim;
+    if (h0 && h1) {
+      const bool first0 = t0 <= t1;
+      if (sp < RT_BVH_STACK) {
+        stack[sp] = first0 ? c1 : c0;
+        stackt[sp] = first0 ? t1 : t0;
+        ++sp;
+      }
+      cur = first0 ? c0 : c1;
+      continue;
+    }
+    if (h0) {
+      cur = c0;
+      continue;
+    }
+    if (h1) {
+      cur = c1;
+      continue;
+    }
+    bool found = false;
+    while (sp > 0) {
+      --sp;
+      if (stackt[sp] <= h.t * 1.00001f + 1e-6f) {
+        cur = stack[sp];
+        found = true;
+        break;
+      }
+    }
+    if (!found) break;
+  }
+  return h;
+}
+
+}  // namespace rt

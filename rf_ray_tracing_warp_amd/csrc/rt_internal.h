@@ -12,7 +12,7 @@
 //                     (p0 p1 p2 q0)(q1 q2 r0 r1)(r2 0 0 0) with 0/1/2 = [kx]/[ky]/[kz]
 //                     -- 288 B per face, read as 2x ds_read_b128 + ds_read_b32
 //   nrm   [nf]        unit geometric normal normalize(cross(q-p, r-p)), w = 0
-//   bvh nodes (optional, large meshes): see bvh.h
+//   bvh nodes (optional, large meshes): see rt_bvh.h
 struct rt_mesh {
   int device = 0;
   int64_t nf = 0;
@@ -22,10 +22,12 @@ struct rt_mesh {
   float center[3] = {0, 0, 0};
   float radius = 0.0f;
   float lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
-  // BVH (built when nf > RT_BRUTE_MAX_FACES)
-  float4* nodes = nullptr;  // [nnodes][4]: child0 box lo/hi, child1 box lo/hi packed, see bvh.h
-  int32_t* leaf_faces = nullptr;
-  int64_t nnodes = 0;
+  // BVH (built when nf > RT_BRUTE_MAX_FACES), layout in rt_bvh.h
+  float* nodes = nullptr;  // [nnodes][16]
+  int* leaves = nullptr;   // [nleaves][2] (first, count)
+  float* lperm = nullptr;  // leaf-ordered copy of perm
+  int* lface = nullptr;    // leaf-ordered original face ids
+  int64_t nnodes = 0, nleaves = 0;
 };
 
 namespace rt {

@@ -13,6 +13,7 @@
 // no t_min (Q3), no renormalisation after reflect (Q4), traced_paths is scratch (Q6).
 #include <math.h>
 
+#include "rt_bvh.h"
 #include "rt_device.h"
 #include "rt_internal.h"
 
@@ -22,6 +23,7 @@ struct TraceArgs {
   const float4* env_perm;
   const float4* env_nrm;
   int env_nf;
+  rt::BvhView env_bvh;  // used when the kernel is instantiated with USE_BVH
   const float4* rx_perm;
   int rx_nf;
   float rx_c[3];
@@ -77,14 +79,31 @@ __device__ __forceinline__ void store_row(float* dst, const float (*pts)[3], int
   }
 }
 
-template <int B>
+// environment closest hit: LDS brute force (small meshes) or BVH (large meshes)
+template <bool USE_BVH>
+__device__ __forceinline__ rt::Hit env_hit_query(const TraceArgs& a, const float4* lds_tab, const rt::Shear& s,
+                                                 float3 o, float3 d) {
+  if constexpr (USE_BVH) {
+    return rt::bvh_query(a.env_bvh, s, o, d);
+  } else {
+    return query_faces(lds_tab, a.env_nf, s);
+  }
+}
+
+template <bool USE_BVH>
+__device__ __forceinline__ void stage_env(const TraceArgs& a, float4* lds_tab) {
+  if constexpr (!USE_BVH) {  // stage the environment table (coalesced float4 copy)
+    const int nvec = a.env_nf * 18;
+    for (int i = threadIdx.x; i < nvec; i += blockDim.x) lds_tab[i] = a.env_perm[i];
+    __syncthreads();
+  }
+}
+
+template <int B, bool USE_BVH>
 __global__ __launch_bounds__(256) void k_trace_bf(TraceArgs a) {
   constexpr int P = B + 1;
   extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
-  // stage the environment table (coalesced float4 copy)
-  const int nvec = a.env_nf * 18;
-  for (int i = threadIdx.x; i < nvec; i += blockDim.x) lds_tab[i] = a.env_perm[i];
-  __syncthreads();
+  stage_env<USE_BVH>(a, lds_tab);
 
   const float qnan = __builtin_nanf("");
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -105,7 +124,7 @@ __global__ __launch_bounds__(256) void k_trace_bf(TraceArgs a) {
       int kind = 0, face = -1;
       if (alive) {
         const rt::Shear s = rt::make_shear(pos, dir);
-        const rt::Hit he = query_faces(lds_tab, a.env_nf, s);
+        const rt::Hit he = env_hit_query<USE_BVH>(a, lds_tab, s, pos, dir);
         const bool env_hit = he.face >= 0;
         rt::Hit hr;
         rt::hit_init(hr);
@@ -162,11 +181,10 @@ __global__ __launch_bounds__(256) void k_trace_bf(TraceArgs a) {
 
 // Generic fallback for B beyond the register-resident instantiations: the path lives in
 // the output rows themselves (same semantics, slower).
+template <bool USE_BVH>
 __global__ __launch_bounds__(256) void k_trace_bf_generic(TraceArgs a, int B) {
   extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
-  const int nvec = a.env_nf * 18;
-  for (int i = threadIdx.x; i < nvec; i += blockDim.x) lds_tab[i] = a.env_perm[i];
-  __syncthreads();
+  stage_env<USE_BVH>(a, lds_tab);
   const int P = B + 1;
   const float qnan = __builtin_nanf("");
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -187,7 +205,7 @@ __global__ __launch_bounds__(256) void k_trace_bf_generic(TraceArgs a, int B) {
       int kind = 0, face = -1;
       if (alive) {
         const rt::Shear s = rt::make_shear(pos, dir);
-        const rt::Hit he = query_faces(lds_tab, a.env_nf, s);
+        const rt::Hit he = env_hit_query<USE_BVH>(a, lds_tab, s, pos, dir);
         const bool env_hit = he.face >= 0;
         rt::Hit hr;
         rt::hit_init(hr);
@@ -244,6 +262,8 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
   a.env_perm = env->perm;
   a.env_nrm = env->nrm;
   a.env_nf = (int)env->nf;
+  a.env_bvh = rt::BvhView{(const float4*)env->nodes, (const int2*)env->leaves, (const float4*)env->lperm, env->lface};
+  const bool bvh = env->nodes != nullptr;
   a.rx_perm = rx ? rx->perm : nullptr;
   a.rx_nf = rx ? (int)rx->nf : 0;
   for (int k = 0; k < 3; ++k) {
@@ -258,7 +278,7 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
   a.mask = mask;
   a.hit_kind = hit_kind;
   a.hit_face = hit_face;
-  const size_t lds = (size_t)env->nf * 18 * sizeof(float4);
+  const size_t lds = bvh ? 0 : (size_t)env->nf * 18 * sizeof(float4);
   int dev_cu = 256;
   const int64_t want = (n + 255) / 256;
   const int64_t cap = (int64_t)dev_cu * 16;
@@ -270,12 +290,20 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
     return -1;
   }
   switch (B) {
-#define RT_CASE(BB) \
-  case BB: hipLaunchKernelGGL(k_trace_bf<BB>, dim3(grid), blk, lds, stream, a); break;
+#define RT_CASE(BB)                                                                     \
+  case BB:                                                                              \
+    if (bvh)                                                                            \
+      hipLaunchKernelGGL((k_trace_bf<BB, true>), dim3(grid), blk, lds, stream, a);      \
+    else                                                                                \
+      hipLaunchKernelGGL((k_trace_bf<BB, false>), dim3(grid), blk, lds, stream, a);     \
+    break;
     RT_CASE(1) RT_CASE(2) RT_CASE(3) RT_CASE(4) RT_CASE(5) RT_CASE(6) RT_CASE(7) RT_CASE(8)
 #undef RT_CASE
     default:
-      hipLaunchKernelGGL(k_trace_bf_generic, dim3(grid), blk, lds, stream, a, B);
+      if (bvh)
+        hipLaunchKernelGGL(k_trace_bf_generic<true>, dim3(grid), blk, lds, stream, a, B);
+      else
+        hipLaunchKernelGGL(k_trace_bf_generic<false>, dim3(grid), blk, lds, stream, a, B);
       break;
   }
   RT_HIP(hipGetLastError());

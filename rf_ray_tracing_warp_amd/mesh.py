@@ -20,7 +20,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-__all__ = ["TriMesh", "load_stl", "load_mesh", "icosahedron", "icosphere", "sphere"]
+__all__ = ["TriMesh", "load_stl", "load_mesh", "icosahedron", "icosphere", "sphere", "synthetic_terrain"]
 
 
 @dataclass
@@ -129,3 +129,33 @@ def sphere(center, radius: float, subdivisions: int = 1) -> TriMesh:
     """``tm.primitives.Sphere(center=, radius=, subdivisions=)`` (``tracer.py:27``)."""
     v, f = icosphere(subdivisions)
     return TriMesh(v * float(radius) + np.asarray(center, dtype=np.float64), f)
+
+
+def synthetic_terrain(n: int = 1024, half_extent: float = 50.0, seed: int = 17, craters: int = 80) -> TriMesh:
+    """Declared stand-in for models/apollo_17_landing_site.stl (absent: .MISSING_LARGE_BLOBS:1).
+
+    An n x n vertex heightfield over [-h, h]^2 (2*(n-1)^2 triangles; n=1024 -> 2.09M)
+    with gentle undulation and seeded bowl craters with raised rims, heights within about
+    [-2, 1] m so the reference scene's TX (10, 0, 4.5) and RX (-10.125, 0, 4.8) (main.py:22-23) sit
+    above the ground.  Deterministic for a given (n, half_extent, seed, craters) on one machine.
+    """
+    rng = np.random.default_rng(seed)
+    xs = np.linspace(-half_extent, half_extent, n)
+    X, Y = np.meshgrid(xs, xs, indexing="xy")
+    Z = 0.25 * np.sin(0.13 * X) * np.cos(0.11 * Y) + 0.15 * np.sin(0.05 * (X + Y))
+    cx = rng.uniform(-half_extent, half_extent, craters)
+    cy = rng.uniform(-half_extent, half_extent, craters)
+    cr = rng.uniform(1.0, 8.0, craters)
+    for x0, y0, r in zip(cx, cy, cr):
+        d2 = ((X - x0) ** 2 + (Y - y0) ** 2) / (r * r)
+        depth = 0.25 * r / 8.0 * 2.0
+        Z -= depth * np.clip(1.0 - d2, 0.0, None)
+        Z += 0.15 * depth * np.exp(-((np.sqrt(d2) - 1.0) / 0.3) ** 2)
+    verts = np.stack([X.ravel(), Y.ravel(), Z.ravel()], axis=1)
+    i = np.arange(n - 1)
+    a = (i[None, :] + n * i[:, None]).ravel()  # lower-left corner of each quad
+    b, c, d = a + 1, a + n, a + n + 1
+    faces = np.empty((2 * len(a), 3), dtype=np.int64)
+    faces[0::2] = np.stack([a, b, d], axis=1)
+    faces[1::2] = np.stack([a, d, c], axis=1)
+    return TriMesh(verts, faces)

@@ -253,3 +253,55 @@ def test_compute_cir_end_to_end(room):
     ref_ir = orc.cir_from_paths(ref_paths, 1, N, 2.998e8, 100e9, 100e-9)
     np.testing.assert_array_equal(np.nonzero(ir)[0], np.nonzero(ref_ir)[0])
     np.testing.assert_allclose(ir, ref_ir, rtol=1e-5, atol=0)
+
+
+# ---------------------------------------------------------------------------- BVH (large meshes)
+@pytest.fixture(scope="module")
+def terrain256():
+    from rf_ray_tracing_warp_amd.mesh import synthetic_terrain
+    return synthetic_terrain(256, 50.0)
+
+
+def test_bvh_query_bitexact(terrain256):
+    t = terrain256
+    rng = np.random.default_rng(11)
+    n = 300_000
+    o = np.c_[rng.uniform(-50, 50, (n, 2)), rng.uniform(-2, 8, n)].astype(np.float32)
+    d = rng.standard_normal((n, 3))
+    d[:, 2] -= 0.3
+    d = (d / np.linalg.norm(d, axis=1)[:, None]).astype(np.float32)
+    om = orc.Mesh(t.vertices, t.faces)
+    tb, fb, _ = om.query(o, d)
+    hit = fb >= 0
+    o = np.concatenate([o, (o[hit] + d[hit] * tb[hit][:, None]).astype(np.float32)])  # rays leaving the surface
+    d = np.concatenate([d, d[hit]])
+    dm = DeviceMesh(t.vertices, t.faces)
+    ot, dt = torch.from_numpy(o).to(DEV), torch.from_numpy(d).to(DEV)
+    tt = torch.empty(len(o), dtype=torch.float32, device=DEV)
+    ff = torch.empty(len(o), dtype=torch.int32, device=DEV)
+    check(lib().rt_query(dm.handle, ptr(ot), ptr(dt), len(o), ptr(tt), ptr(ff), _stream()))
+    rt_, rf_, _ = om.query(o, d)
+    np.testing.assert_array_equal(ff.cpu().numpy(), rf_)
+    np.testing.assert_array_equal(_bits(tt.cpu().numpy()), _bits(rt_))
+
+
+@pytest.mark.parametrize("B,off,n", [(5, 0, 60_000), (3, 5_000_000, 40_000), (12, 7, 10_000)])
+def test_trace_bvh_bitexact(terrain256, B, off, n):
+    tx, rx = (10.0, 0.0, 4.5), (-10.125, 0.0, 4.8)  # main.py:22-23
+    rxm = sphere(rx, 0.1, 1)
+    g = _gpu_trace(terrain256, rxm, tx, B, off, n)
+    o = orc.trace(orc.Mesh(terrain256.vertices, terrain256.faces), orc.Mesh(rxm.vertices, rxm.faces), tx, B, off, n)
+    _assert_trace_equal(g, o)
+    assert (g["hit_kind"] == 1).sum() > n // 4
+
+
+def test_trace_k4_terrain_full_mesh():
+    """K4 shape on one GPU: the 2.09M-triangle terrain, 1M rays, 5 bounces; sampled rows bit-exact."""
+    from rf_ray_tracing_warp_amd.mesh import synthetic_terrain
+    t = synthetic_terrain(1024, 50.0)
+    n, B, tx, rx = 1_000_000, 5, (10.0, 0.0, 4.5), (-10.125, 0.0, 4.8)
+    rxm = sphere(rx, 0.1, 1)
+    g = _gpu_trace(t, rxm, tx, B, 3_000_000, n, want_traced=True)
+    rows = np.union1d(np.arange(0, n, 250), np.nonzero(g["mask"])[0])
+    o = orc.trace_ids(orc.Mesh(t.vertices, t.faces), orc.Mesh(rxm.vertices, rxm.faces), tx, B, rows + 3_000_000)
+    _assert_trace_equal(g, o, rows)
