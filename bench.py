@@ -45,6 +45,10 @@ def parse():
     ap.add_argument("--coverage-grid", type=int, default=256, help="K3: n x n receiver cells at z=5 on room.stl")
     ap.add_argument("--coverage-rays", type=int, default=1_000_000)
     ap.add_argument("--coverage-runs", type=int, default=3)
+    ap.add_argument("--no-k4", action="store_true", help="skip the terrain (apollo stand-in) legs K4/K5")
+    ap.add_argument("--k4-rays", type=int, default=2_097_152, help="rays per GPU (K4: 16.7M over 8 GPUs)")
+    ap.add_argument("--k5-grid", type=int, default=1024)
+    ap.add_argument("--k5-rays", type=int, default=1_000_000)
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_k2.json"),
                     help="per-launch HBM bytes measured by rocprofv3 PMC (profiles/)")
     return ap.parse_args()
@@ -120,6 +124,89 @@ def coverage_leg(args, env_m, env, local, rank, world, dist):
                         f"signal power per cell; cells sharded cyclically x{world} + RCCL sum of the power map",
             "scaling": "strong", "cells_receiving": int(np.isfinite(pm).sum()),
             "candidates": int(cand.item()), "algorithm": "exact shared-trajectory (csrc/coverage.hip)"}
+
+
+def terrain_legs(args, local, rank, world, dist):
+    """K4/K5 on the declared apollo stand-in (mesh.synthetic_terrain: 1024^2 vertices, 2.09M faces, BVH):
+    K4 = TX (10,0,4.5), RX (-10.125,0,4.8) r=0.1 (main.py:22-23), 5 bounces, 16.7M rays / 8 GPUs
+    sharded by ray id; K5 = coverage of k5_grid^2 cells 1 m above the terrain's mean level."""
+    import torch
+    from rf_ray_tracing_warp_amd._lib import DeviceMesh, check, lib, ptr
+    from rf_ray_tracing_warp_amd.coverage import Coverage, CoverageGrid
+    from rf_ray_tracing_warp_amd.mesh import sphere, synthetic_terrain
+
+    dev = f"cuda:{local}"
+    t_build = time.perf_counter()
+    terr = synthetic_terrain(1024, 50.0)
+    env = DeviceMesh(terr.vertices, terr.faces, local)
+    t_build = time.perf_counter() - t_build
+    B, N = 5, args.k4_rays
+    P = B + 1
+    rxm = sphere((-10.125, 0.0, 4.8), 0.1, 1)
+    rx = DeviceMesh(rxm.vertices, rxm.faces, local)
+    tx = np.asarray((10.0, 0.0, 4.5), np.float32)
+    traced = torch.empty((N, P, 3), dtype=torch.float32, device=dev)
+    received = torch.empty((N, P, 3), dtype=torch.float32, device=dev)
+    mask = torch.empty(N, dtype=torch.int32, device=dev)
+    sh = torch.cuda.current_stream().cuda_stream
+    L = lib()
+
+    def step():
+        check(L.rt_trace(env.handle, tx.ctypes.data, rx.handle, B, rank * N, N, ptr(traced), ptr(received), ptr(mask),
+                         None, None, sh), "rt_trace")
+
+    step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    reps = 5
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = (time.perf_counter() - t0) / reps
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt[0])
+    k4 = {"metric": "ray-bounces/sec", "value": world * N * B / dt, "unit": "ray-bounces/s", "ms_per_step": dt * 1e3,
+          "workload": f"K4 on the declared apollo stand-in (synthetic terrain 1024^2 vertices, {len(terr.faces)} faces, "
+                      f"BVH), {N} rays/GPU x {world}, {B} bounces, traced+received+row_mask",
+          "scaling": "weak", "mesh_build_s": t_build}
+    del traced, received, mask
+    grid = CoverageGrid.square(args.k5_grid, 50.0, 2.0)
+    cov = Coverage(terr, 2.998e8, 100e9, 200e-9, 3, args.k5_rays, grid, 0.1, device=local, shard_index=rank,
+                   shard_count=world, env_mesh=env)
+
+    def one():
+        p = cov.run_device((10.0, 0.0, 4.5), 1)
+        if world > 1:
+            dist.all_reduce(p)
+        return p
+
+    one()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    p = one()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt[0])
+    pm = p.cpu().numpy()
+    k5 = {"metric": "coverage cells/sec", "value": grid.num_cells / dt, "unit": "cells/s", "ms_per_map": dt * 1e3,
+          "workload": f"K5 on the terrain stand-in: {grid.nx}x{grid.ny} receivers at z=2 over +-50 m, tx (10,0,4.5), "
+                      f"{args.k5_rays} rays per cell, 3 bounces, 20000 bins; cells sharded x{world} + RCCL sum",
+          "scaling": "strong", "cells_receiving": int(np.isfinite(pm).sum()), "candidates": int(cov.last_candidates)}
+    cov.close()
+    return k4, k5
 
 
 def main():
@@ -207,6 +294,9 @@ def main():
     cov_out = None
     if not args.no_coverage:
         cov_out = coverage_leg(args, env_m, env, local, rank, world, dist)
+    k4_out = k5_out = None
+    if not args.no_k4:
+        k4_out, k5_out = terrain_legs(args, local, rank, world, dist)
 
     if rank == 0:
         bounces = world * N * B * args.steps
@@ -246,6 +336,10 @@ def main():
         }
         if cov_out is not None:
             out["coverage"] = cov_out
+        if k4_out is not None:
+            out["k4_terrain"] = k4_out
+        if k5_out is not None:
+            out["k5_terrain_coverage"] = k5_out
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_sample, B, tx, rx)
         print(json.dumps(out), flush=True)

@@ -32,6 +32,7 @@
 #include <vector>
 
 #include "../../include/rfrt.h"
+#include "rt_bvh.h"
 #include "rt_device.h"
 #include "rt_icosphere1.h"
 #include "rt_internal.h"
@@ -43,6 +44,7 @@ struct CovParams {
   const float4* env_perm;
   const float4* env_nrm;
   int env_nf;
+  rt::BvhView env_bvh;  // large environments (USE_BVH instantiations)
   float tx[3];
   int B;
   int64_t n;           // rays
@@ -79,7 +81,7 @@ __device__ __forceinline__ void cell_center(const rt_grid& g, int64_t cell, doub
 }
 
 // environment closest hit from the LDS table (same code path as the trace kernel)
-__device__ __forceinline__ rt::Hit env_query(const float4* tab, int nf, const rt::Shear& s) {
+__device__ __forceinline__ rt::Hit env_query_lds(const float4* tab, int nf, const rt::Shear& s) {
   rt::Hit h;
   rt::hit_init(h);
   const int off = s.kcase * 3;
@@ -91,6 +93,23 @@ __device__ __forceinline__ rt::Hit env_query(const float4* tab, int nf, const rt
     if (rt::tri_test(s, q0, q1, c2, T, det)) rt::hit_consider(h, T, det, f);
   }
   return h;
+}
+
+template <bool USE_BVH>
+__device__ __forceinline__ rt::Hit env_query(const CovParams& p, const float4* tab, const rt::Shear& s, float3 o,
+                                            float3 d) {
+  if constexpr (USE_BVH) {
+    return rt::bvh_query(p.env_bvh, s, o, d);
+  } else {
+    return env_query_lds(tab, p.env_nf, s);
+  }
+}
+template <bool USE_BVH>
+__device__ __forceinline__ void stage_env(const CovParams& p, float4* lds_tab) {
+  if constexpr (!USE_BVH) {
+    for (int i = threadIdx.x; i < p.env_nf * 18; i += blockDim.x) lds_tab[i] = p.env_perm[i];
+    __syncthreads();
+  }
 }
 
 // The cell's receiver: vertex i = (float)(unit_i * r + centre) in double, exactly mesh.sphere() +
@@ -148,10 +167,10 @@ __device__ __forceinline__ rt::Hit rx_query(const rt_grid& g, int64_t cell, doub
 }
 
 // ------------------------------------------------------------------ 1. environment trajectories
+template <bool USE_BVH>
 __global__ __launch_bounds__(256) void k_traj(CovParams p) {
   extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
-  for (int i = threadIdx.x; i < p.env_nf * 18; i += blockDim.x) lds_tab[i] = p.env_perm[i];
-  __syncthreads();
+  stage_env<USE_BVH>(p, lds_tab);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < p.n; r += stride) {
     float3 dir = rt::ray_dir(p.ray_offset + r);
@@ -159,7 +178,7 @@ __global__ __launch_bounds__(256) void k_traj(CovParams p) {
     int nseg = 0;
     for (int k = 0; k < p.B; ++k) {
       const rt::Shear s = rt::make_shear(pos, dir);
-      const rt::Hit he = env_query(lds_tab, p.env_nf, s);
+      const rt::Hit he = env_query<USE_BVH>(p, lds_tab, s, pos, dir);
       const int64_t o = (int64_t)k * p.n + r;
       p.px[o] = pos.x;
       p.py[o] = pos.y;
@@ -456,12 +475,12 @@ __global__ __launch_bounds__(256) void k_first(const uint64_t* keys, int64_t nke
   }
 }
 
+template <bool USE_BVH>
 __global__ __launch_bounds__(256) void k_replay(CovParams p, const uint64_t* keys, const float* trx,
                                                 const int64_t* list, const unsigned long long* list_count,
                                                 uint64_t* out_key, double* out_amp) {
   extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
-  for (int i = threadIdx.x; i < p.env_nf * 18; i += blockDim.x) lds_tab[i] = p.env_perm[i];
-  __syncthreads();
+  stage_env<USE_BVH>(p, lds_tab);
   const int64_t nl = (int64_t)*list_count;
   for (int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; li < nl; li += (int64_t)gridDim.x * blockDim.x) {
     const int64_t i = list[li];
@@ -487,7 +506,7 @@ __global__ __launch_bounds__(256) void k_replay(CovParams p, const uint64_t* key
     float3 d = dir;
     for (int b = k0 + 1; b < p.B; ++b) {  // kernel.py:57-98 with this cell's receiver
       const rt::Shear s = rt::make_shear(pos, d);
-      const rt::Hit he = env_query(lds_tab, p.env_nf, s);
+      const rt::Hit he = env_query<USE_BVH>(p, lds_tab, s, pos, d);
       const rt::Hit hr = rx_query(p.g, cell, p.r_rx, pos, d);
       const bool env_hit = he.face >= 0, rx_hit = hr.face >= 0;
       if (rx_hit && (!env_hit || he.t > hr.t)) {
@@ -734,10 +753,6 @@ int rt_coverage_create(int device, const rt_mesh* env, int max_bounces, int64_t 
     rt::set_error("rt_coverage_create: invalid arguments (max_bounces 1..15, n_rays 1..2^24 per call)");
     return RT_EINVAL;
   }
-  if (env->nf > RT_BRUTE_MAX_FACES) {
-    rt::set_error("rt_coverage_create: environment above RT_BRUTE_MAX_FACES faces needs the BVH path");
-    return RT_EINVAL;
-  }
   const int64_t nc = grid->nx * grid->ny * grid->nz;
   if (bits_for((uint64_t)nc) > 32) {
     rt::set_error("rt_coverage_create: too many cells");
@@ -798,6 +813,9 @@ int rt_coverage_run(rt_coverage* c, const float* tx_pos, double tx_power, double
   p.env_perm = c->env->perm;
   p.env_nrm = c->env->nrm;
   p.env_nf = (int)c->env->nf;
+  p.env_bvh = rt::BvhView{(const float4*)c->env->nodes, (const int2*)c->env->leaves, (const float4*)c->env->lperm,
+                          c->env->lface};
+  const bool bvh = c->env->nodes != nullptr;
   for (int k = 0; k < 3; ++k) p.tx[k] = tx_pos[k];
   p.B = c->B;
   p.n = c->n;
@@ -831,9 +849,12 @@ int rt_coverage_run(rt_coverage* c, const float* tx_pos, double tx_power, double
   p.fs64 = sample_rate;
   p.flags = flags;
   p.n_bins = n_bins;
-  const size_t lds = (size_t)p.env_nf * 18 * sizeof(float4);
+  const size_t lds = bvh ? 0 : (size_t)p.env_nf * 18 * sizeof(float4);
   const unsigned grid_rays = (unsigned)std::min<int64_t>((c->n + 255) / 256, 4096);
-  hipLaunchKernelGGL(k_traj, dim3(grid_rays), dim3(256), lds, s, p);
+  if (bvh)
+    hipLaunchKernelGGL(k_traj<true>, dim3(grid_rays), dim3(256), lds, s, p);
+  else
+    hipLaunchKernelGGL(k_traj<false>, dim3(grid_rays), dim3(256), lds, s, p);
   RT_HIP(hipGetLastError());
   // candidates: column items (pass A) then cells (pass B); grow and retry on overflow
   int64_t ncand = 0;
@@ -891,8 +912,12 @@ int rt_coverage_run(rt_coverage* c, const float* tx_pos, double tx_power, double
   hipLaunchKernelGGL(k_win, dim3(grid_c), dim3(256), 0, s, p, c->keys_sorted, ncand, c->win, c->trx);
   hipLaunchKernelGGL(k_first, dim3(grid_c), dim3(256), 0, s, c->keys_sorted, ncand, c->win, c->list, c->counters + 2);
   RT_HIP(hipMemsetAsync(c->okeys, 0xFF, ncand * 8, s));
-  hipLaunchKernelGGL(k_replay, dim3(grid_c), dim3(256), lds, s, p, c->keys_sorted, c->trx, c->list, c->counters + 2,
-                     c->okeys, c->oamps);
+  if (bvh)
+    hipLaunchKernelGGL(k_replay<true>, dim3(grid_c), dim3(256), lds, s, p, c->keys_sorted, c->trx, c->list,
+                       c->counters + 2, c->okeys, c->oamps);
+  else
+    hipLaunchKernelGGL(k_replay<false>, dim3(grid_c), dim3(256), lds, s, p, c->keys_sorted, c->trx, c->list,
+                       c->counters + 2, c->okeys, c->oamps);
   RT_HIP(hipGetLastError());
   tb = c->tmp_bytes;
   RT_HIP(hipcub::DeviceRadixSort::SortPairs(c->tmp, tb, c->okeys, c->okeys_sorted, c->oamps, c->oamps_sorted,

@@ -100,3 +100,15 @@ def test_power_dense_matches_numpy():
     np.testing.assert_array_equal(np.isnan(got), np.isnan(ref))
     ok = ~np.isnan(ref)
     np.testing.assert_allclose(got[ok], ref[ok], rtol=1e-9)
+
+
+def test_coverage_on_bvh_terrain():
+    """K5 shape (coverage on the large-mesh BVH path), small: terrain 256^2 vertices, 10x10 cells."""
+    from rf_ray_tracing_warp_amd.mesh import synthetic_terrain
+    t = synthetic_terrain(256, 50.0)
+    grid = CoverageGrid(7.0, -1.0, 2.0, 0.7, 0.25, 1.0, 10, 10, 1)
+    tx, B, N = (10.0, 0.0, 4.5), 3, 20_000
+    cov = Coverage(t, 2.998e8, 100e9, 200e-9, B, N, grid)
+    power, ref = _compare(cov, grid, t, tx, B, N, win=200e-9)
+    assert np.isfinite(ref).sum() >= 3
+    cov.close()
