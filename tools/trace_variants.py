@@ -1,0 +1,66 @@
+"""Time rt_trace on the K2 workload (HIP events) and hash its outputs, once per entry of VARIANTS,
+each in its own process with RFRT_TRACE_VARIANT set.  Used to A/B kernel variants behind a
+temporary env switch in launch_trace (none is compiled in by default); the hashes check that a
+variant is bit-identical to variant 0."""
+import hashlib
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def child(n, B, reps):
+    sys.path.insert(0, ROOT)
+    import numpy as np
+    import torch
+    from rf_ray_tracing_warp_amd._lib import DeviceMesh, check, lib, ptr
+    from rf_ray_tracing_warp_amd.mesh import load_stl, sphere
+    m = load_stl(os.path.join(ROOT, "models/room.stl"))
+    env = DeviceMesh(m.vertices, m.faces, 0)
+    rs = sphere((-10, 0, 5), 0.1, 1)
+    rx = DeviceMesh(rs.vertices, rs.faces, 0)
+    P = B + 1
+    tr = torch.empty((n, P, 3), dtype=torch.float32, device="cuda")
+    rc = torch.empty((n, P, 3), dtype=torch.float32, device="cuda")
+    mk = torch.empty(n, dtype=torch.int32, device="cuda")
+    tx = np.asarray((10, 0, 5), np.float32)
+    st = torch.cuda.current_stream()
+    L = lib()
+
+    def go():
+        check(L.rt_trace(env.handle, tx.ctypes.data, rx.handle, B, 0, n, ptr(tr), ptr(rc), ptr(mk), None, None,
+                         st.cuda_stream), "rt_trace")
+    go()
+    torch.cuda.synchronize()
+    h = hashlib.sha256(tr.cpu().numpy().tobytes() + rc.cpu().numpy().tobytes() + mk.cpu().numpy().tobytes()).hexdigest()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(reps):
+        go()
+    e1.record(st)
+    torch.cuda.synchronize()
+    print(json.dumps({"variant": os.environ.get("RFRT_TRACE_VARIANT", "0"), "us": e0.elapsed_time(e1) * 1e3 / reps,
+                      "hash": h[:16]}))
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "child":
+        child(int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]))
+        sys.exit(0)
+    variants = os.environ.get("VARIANTS", "0 1 3").split()
+    res = []
+    for v in variants:
+        env = dict(os.environ, RFRT_TRACE_VARIANT=v)
+        out = subprocess.run([sys.executable, __file__, "child", "1000000", "3", "50"], env=env, capture_output=True,
+                             text=True, timeout=300)
+        if out.returncode != 0:
+            print(out.stderr[-2000:])
+            sys.exit(out.returncode)
+        r = json.loads(out.stdout.strip().splitlines()[-1])
+        res.append(r)
+        print(json.dumps(r), flush=True)
+    same = all(r["hash"] == res[0]["hash"] for r in res)
+    print("bit-identical outputs across variants:", same)
+    sys.exit(0 if same else 3)
