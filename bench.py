@@ -30,6 +30,7 @@ sys.path.insert(0, REPO)
 
 METRIC = "ray-bounces/sec on room.stl (1 GPU) + coverage cells/sec at 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+VALU_PEAK_GWI = 1024 * 2.4 / 2  # 256 CUs x 4 SIMDs, one wave64 VALU instruction per 2 cycles
 
 
 def parse():
@@ -311,6 +312,21 @@ def main():
                 traffic = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             pass
+        # the binding resource of the brute-force LDS kernel is the VALU issue rate: VALU
+        # instructions per launch come from a PMC pass (profiles/r1_k2_sq_counters.json, a
+        # property of the code and the input), the time from the live HIP events above
+        valu = None
+        try:
+            with open(os.path.join(REPO, "profiles", "r1_k2_sq_counters.json")) as fh:
+                sq = json.load(fh)
+            if N == 1_000_000 and B == 3:
+                rate = sq["SQ_INSTS_VALU"] / (kern_ms * 1e-3) / 1e9  # wave-instructions / ns
+                peak = VALU_PEAK_GWI
+                valu = {"bound": "valu", "achieved": rate, "peak": peak, "unit": "G wave-instr/s", "frac": rate / peak,
+                        "valu_instr_per_launch": sq["SQ_INSTS_VALU"],
+                        "note": "peak = 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction"}
+        except (OSError, ValueError, KeyError):
+            pass
         out = {
             "metric": METRIC,
             "value": value,
@@ -332,6 +348,7 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_trace_bf<3>", "kernel_ms": kern_ms,
                          "algorithmic_bytes_per_launch": bytes_per_launch},
+            "compute_roofline": valu,
             "received_rows_last_step": received_rows,
         }
         if cov_out is not None:

@@ -43,6 +43,10 @@ int rt_mesh_create(int device, const float* vertices, int64_t nv, const int32_t*
 int rt_mesh_destroy(rt_mesh* mesh);
 /* nf, bounds6 = (lo xyz, hi xyz), sphere4 = conservative bounding sphere (centre, radius). Any may be NULL. */
 int rt_mesh_info(const rt_mesh* mesh, int64_t* nf, float* bounds6, float* sphere4);
+/* BVH statistics (all 0 for meshes of <= 192 faces, which are traced by brute force):
+ * info4 = (nodes, leaves, max internal-node depth, max faces in a leaf).  No reference
+ * counterpart: Warp's wp.Mesh BVH (tracer.py:24) is internal. */
+int rt_bvh_info(const rt_mesh* mesh, int64_t* info4);
 
 /* Replaces wp.launch(kernel.trace_paths_kernel, dim=(n,1,1), inputs=[env.id, tx_pos, rx.id,
  * max_bounces, traced_paths, received_paths, row_mask]) -- tracer.py:75-79, kernel.py:38-98.

@@ -39,6 +39,7 @@ def lib():
     L.rt_mesh_create.argtypes = [_int, _vp, _i64, _vp, _i64, ctypes.POINTER(_vp)]
     L.rt_mesh_destroy.argtypes = [_vp]
     L.rt_mesh_info.argtypes = [_vp, _vp, _vp, _vp]
+    L.rt_bvh_info.argtypes = [_vp, _vp]
     L.rt_trace.argtypes = [_vp, _vp, _vp, _int, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp]
     L.rt_compact_workspace_bytes.restype = _i64
     L.rt_compact_workspace_bytes.argtypes = [_i64]
@@ -55,7 +56,7 @@ def lib():
     L.rt_selftest_math.argtypes = [_vp, _i64, _vp, _int, _vp]
     L.rt_ray_dirs.argtypes = [_i64, _i64, _vp, _vp]
     L.rt_query.argtypes = [_vp, _vp, _vp, _i64, _vp, _vp, _vp]
-    for name in ("rt_mesh_create", "rt_mesh_destroy", "rt_mesh_info", "rt_trace", "rt_compact", "rt_cir",
+    for name in ("rt_mesh_create", "rt_mesh_destroy", "rt_mesh_info", "rt_bvh_info", "rt_trace", "rt_compact", "rt_cir",
                  "rt_coverage_create", "rt_coverage_destroy", "rt_coverage_run", "rt_coverage_received",
                  "rt_power_dense", "rt_selftest_math", "rt_ray_dirs", "rt_query"):
         getattr(L, name).restype = _int
@@ -101,6 +102,12 @@ class DeviceMesh:
         s = np.zeros(4, np.float32)
         check(lib().rt_mesh_info(self._h, ctypes.byref(nf), b.ctypes.data, s.ctypes.data), "rt_mesh_info")
         return int(nf.value), b, s
+
+    def bvh_info(self):
+        """{'nodes', 'leaves', 'depth', 'max_leaf'} of the BVH (all 0 for brute-force meshes)."""
+        out = np.zeros(4, np.int64)
+        check(lib().rt_bvh_info(self._h, out.ctypes.data), "rt_bvh_info")
+        return dict(zip(("nodes", "leaves", "depth", "max_leaf"), (int(x) for x in out)))
 
     def close(self):
         if getattr(self, "_h", None) and self._h.value and _lib is not None:

@@ -136,6 +136,8 @@ int rt_mesh_destroy(rt_mesh* m) {
   if (m->perm) (void)hipFree(m->perm);
   if (m->nrm) (void)hipFree(m->nrm);
   if (m->nodes) (void)hipFree(m->nodes);
+  if (m->leaves) (void)hipFree(m->leaves);
+  if (m->lcomp) (void)hipFree(m->lcomp);
   delete m;
   return RT_OK;
 }
@@ -155,6 +157,18 @@ int rt_mesh_info(const rt_mesh* m, int64_t* nf, float* bounds6, float* sphere4) 
     for (int k = 0; k < 3; ++k) sphere4[k] = m->center[k];
     sphere4[3] = m->radius;
   }
+  return RT_OK;
+}
+
+int rt_bvh_info(const rt_mesh* m, int64_t* info4) {
+  if (!m || !info4) {
+    rt::set_error("rt_bvh_info: null argument");
+    return RT_EINVAL;
+  }
+  info4[0] = m->nnodes;
+  info4[1] = m->nleaves;
+  info4[2] = m->bvh_depth;
+  info4[3] = m->bvh_max_leaf;
   return RT_OK;
 }
 
@@ -248,7 +262,7 @@ int rt_query(const rt_mesh* m, const float* o, const float* d, int64_t n, float*
   }
   if (n == 0) return RT_OK;
   if (m->nodes) {
-    rt::BvhView bv{(const float4*)m->nodes, (const int2*)m->leaves, (const float4*)m->lperm, m->lface};
+    rt::BvhView bv{(const float4*)m->nodes, (const int2*)m->leaves, (const float4*)m->lcomp};
     hipLaunchKernelGGL(k_query_bvh, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, bv, o, d, n,
                        t, face);
   } else {

@@ -51,6 +51,7 @@ struct Builder {
   std::vector<float> nodes;  // 16 floats per node
   std::vector<int> leaves;   // 2 ints per leaf
   double pad;
+  int max_depth = 0, max_leaf = 0;
 
   explicit Builder(const std::vector<float>& t) : tri(t) {}
 
@@ -74,6 +75,7 @@ struct Builder {
   }
 
   int make_leaf(int b, int e) {
+    max_leaf = std::max(max_leaf, e - b);
     const int id = (int)(leaves.size() / 2);
     leaves.push_back(b);
     leaves.push_back(e - b);
@@ -83,6 +85,7 @@ struct Builder {
   // returns child encoding for range [b, e)
   int build(int b, int e, int depth) {
     const int n = e - b;
+    max_depth = std::max(max_depth, depth);
     if (n <= kLeaf || depth >= kMaxDepth) return make_leaf(b, e);
     Box cb;
     for (int i = b; i < e; ++i) cb.grow(&cen[3 * idx[i]]);
@@ -224,27 +227,25 @@ int build_bvh(rt_mesh* m, const std::vector<float>& tri) {
     std::memcpy(&q[12], &c0, 4);
     std::memcpy(&q[13], &c1, 4);
   }
-  // leaf-ordered face tables
-  std::vector<float> lperm((size_t)std::max<int64_t>(nf, 1) * 72);
-  std::vector<int> lface((size_t)std::max<int64_t>(nf, 1));
-  std::vector<float> perm_host((size_t)std::max<int64_t>(nf, 1) * 72);
-  RT_HIP(hipMemcpy(perm_host.data(), m->perm, perm_host.size() * sizeof(float), hipMemcpyDeviceToHost));
+  // leaf-ordered compact face table
+  std::vector<float> lcomp((size_t)std::max<int64_t>(nf, 1) * 12, 0.0f);
   for (int64_t i = 0; i < nf; ++i) {
     const int f = bd.idx[i];
-    lface[i] = f;
-    std::memcpy(&lperm[72 * i], &perm_host[72 * (size_t)f], 72 * sizeof(float));
+    float* q = &lcomp[12 * i];
+    for (int k = 0; k < 9; ++k) q[k] = tri[9 * (size_t)f + k];
+    std::memcpy(&q[9], &f, 4);
   }
+  m->bvh_depth = bd.max_depth;
+  m->bvh_max_leaf = bd.max_leaf;
   m->nnodes = (int64_t)(bd.nodes.size() / 16);
   m->nleaves = (int64_t)(bd.leaves.size() / 2);
   RT_HIP(hipMalloc(&m->nodes, bd.nodes.size() * sizeof(float)));
   RT_HIP(hipMalloc(&m->leaves, std::max<size_t>(bd.leaves.size(), 2) * sizeof(int)));
-  RT_HIP(hipMalloc(&m->lperm, lperm.size() * sizeof(float)));
-  RT_HIP(hipMalloc(&m->lface, lface.size() * sizeof(int)));
+  RT_HIP(hipMalloc(&m->lcomp, lcomp.size() * sizeof(float)));
+  RT_HIP(hipMemcpy(m->lcomp, lcomp.data(), lcomp.size() * sizeof(float), hipMemcpyHostToDevice));
   RT_HIP(hipMemcpy(m->nodes, bd.nodes.data(), bd.nodes.size() * sizeof(float), hipMemcpyHostToDevice));
   if (!bd.leaves.empty())
     RT_HIP(hipMemcpy(m->leaves, bd.leaves.data(), bd.leaves.size() * sizeof(int), hipMemcpyHostToDevice));
-  RT_HIP(hipMemcpy(m->lperm, lperm.data(), lperm.size() * sizeof(float), hipMemcpyHostToDevice));
-  RT_HIP(hipMemcpy(m->lface, lface.data(), lface.size() * sizeof(int), hipMemcpyHostToDevice));
   return 0;
 }
 

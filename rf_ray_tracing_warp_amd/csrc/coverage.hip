@@ -813,8 +813,7 @@ int rt_coverage_run(rt_coverage* c, const float* tx_pos, double tx_power, double
   p.env_perm = c->env->perm;
   p.env_nrm = c->env->nrm;
   p.env_nf = (int)c->env->nf;
-  p.env_bvh = rt::BvhView{(const float4*)c->env->nodes, (const int2*)c->env->leaves, (const float4*)c->env->lperm,
-                          c->env->lface};
+  p.env_bvh = rt::BvhView{(const float4*)c->env->nodes, (const int2*)c->env->leaves, (const float4*)c->env->lcomp};
   const bool bvh = c->env->nodes != nullptr;
   for (int k = 0; k < 3; ++k) p.tx[k] = tx_pos[k];
   p.B = c->B;

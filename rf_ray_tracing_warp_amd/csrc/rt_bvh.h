@@ -6,9 +6,12 @@
 //          q0 = (c0lo.x, c0lo.y, c0lo.z, c0hi.x)  q1 = (c0hi.y, c0hi.z, c1lo.x, c1lo.y)
 //          q2 = (c1lo.z, c1hi.x, c1hi.y, c1hi.z)  q3 = (child0, child1, -, -) as int bits
 //          child >= 0: internal node index;  child < 0: leaf -1-child into `leaves`
-//   leaves int2[nleaves]: (first, count) into the leaf-ordered face arrays
-//   lperm  float4[nf][6][3]: permuted-corner records (as rt_mesh.perm) in leaf order
-//   lface  int[nf]: original face id of each leaf-ordered face
+//   leaves int2[nleaves]: (first, count) into the leaf-ordered face table
+//   lcomp  float4[nf][3]: faces in leaf order, un-permuted: (a.xyz b.x)(b.yz c.xy)(c.z, original
+//          face id bits, -, -).  48 B per face, all of it used by every lane; the corners are
+//          permuted to the lane's shear axes with selects.  (A leaf-ordered copy of the 288-B
+//          six-case records of rt_mesh.perm measured 17% slower on K4: a lane reads only the
+//          36 B of its case, so most of every fetched line is wasted.)
 // Boxes are padded outward on the host so the f32 slab test below can never cull a face the
 // watertight test would hit; the closest hit is the lexicographic (t, original face id) minimum,
 // so traversal order cannot change a result (bit-exact vs the brute-force oracle).
@@ -20,8 +23,7 @@ namespace rt {
 struct BvhView {
   const float4* nodes;
   const int2* leaves;
-  const float4* lperm;
-  const int* lface;
+  const float4* lcomp;
 };
 
 #define RT_BVH_STACK 64
@@ -56,7 +58,23 @@ __device__ __forceinline__ float slab(const RayBox& r, float lx, float ly, float
   return tn <= tf * 1.00001f + 1e-6f ? tn : INFINITY;
 }
 
-// closest hit in a BVH mesh (same result as brute force over all faces)
+__device__ __forceinline__ void leaf_faces(const BvhView& b, const Shear& s, int2 lf, Hit& h) {
+  for (int j = lf.x; j < lf.x + lf.y; ++j) {
+    const float4* p = b.lcomp + (int64_t)j * 3;
+    const float4 a = p[0], m = p[1], c = p[2];
+    // corners A = (a.x a.y a.z), B = (a.w m.x m.y), C = (m.z m.w c.x) -> (kx, ky, kz) order
+    const float4 q0 = make_float4(pick(a.x, a.y, a.z, s.kx), pick(a.x, a.y, a.z, s.ky), pick(a.x, a.y, a.z, s.kz),
+                                  pick(a.w, m.x, m.y, s.kx));
+    const float4 q1 = make_float4(pick(a.w, m.x, m.y, s.ky), pick(a.w, m.x, m.y, s.kz), pick(m.z, m.w, c.x, s.kx),
+                                  pick(m.z, m.w, c.x, s.ky));
+    const float c2 = pick(m.z, m.w, c.x, s.kz);
+    float T, det;
+    if (tri_test(s, q0, q1, c2, T, det)) hit_consider(h, T, det, __float_as_int(c.y));
+  }
+}
+
+// closest hit in a BVH mesh (same result as brute force over all faces): near child first,
+// far child on a per-lane (node, entry t) stack, popped entries re-culled against the best t.
 __device__ __forceinline__ Hit bvh_query(const BvhView& b, const Shear& s, float3 o, float3 d) {
   Hit h;
   hit_init(h);
@@ -77,12 +95,7 @@ __device__ __forceinline__ Hit bvh_query(const BvhView& b, const Shear& s, float
       const int c = side ? c1 : c0;
       float& tt = side ? t1 : t0;
       if (c < 0 && tt <= h.t * 1.00001f + 1e-6f) {
-        const int2 lf = b.leaves[-1 - c];
-        for (int j = lf.x; j < lf.x + lf.y; ++j) {
-          const float4* p = b.lperm + (int64_t)j * 18 + s.kcase * 3;
-          float T, det;
-          if (tri_test(s, p[0], p[1], p[2].x, T, det)) hit_consider(h, T, det, b.lface[j]);
-        }
+        leaf_faces(b, s, b.leaves[-1 - c], h);
         tt = INFINITY;
       } else if (c < 0) {
         tt = INFINITY;
@@ -92,7 +105,7 @@ __device__ __forceinline__ Hit bvh_query(const BvhView& b, const Shear& s, float
     const bool h0 = t0 <= lim, h1 = t1 <= lim;
     if (h0 && h1) {
       const bool first0 = t0 <= t1;
-      if (sp < RT_BVH_STACK) {
+      if (sp < RT_BVH_STACK) {  // cannot overflow: tree depth <= RT_BVH_STACK - 4 (bvh.hip)
         stack[sp] = first0 ? c1 : c0;
         stackt[sp] = first0 ? t1 : t0;
         ++sp;

@@ -90,7 +90,11 @@ struct Shear {
   float3 o;  // origin permuted to (o[kx], o[ky], o[kz])
   float Sx, Sy, Sz;
   int kcase;
+  int kx, ky, kz;
 };
+
+// component k of (x, y, z) -- permutes un-permuted corners per lane (compact BVH leaves)
+__device__ __forceinline__ float pick(float x, float y, float z, int k) { return k == 0 ? x : (k == 1 ? y : z); }
 
 __device__ __forceinline__ Shear make_shear(float3 o, float3 d) {
   const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
@@ -112,6 +116,9 @@ __device__ __forceinline__ Shear make_shear(float3 o, float3 d) {
   s.Sy = comp(d, ky) / dkz;
   s.Sz = 1.0f / dkz;
   s.kcase = kz * 2 + swap;
+  s.kx = kx;
+  s.ky = ky;
+  s.kz = kz;
   return s;
 }
 

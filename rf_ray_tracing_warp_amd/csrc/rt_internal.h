@@ -25,9 +25,9 @@ struct rt_mesh {
   // BVH (built when nf > RT_BRUTE_MAX_FACES), layout in rt_bvh.h
   float* nodes = nullptr;  // [nnodes][16]
   int* leaves = nullptr;   // [nleaves][2] (first, count)
-  float* lperm = nullptr;  // leaf-ordered copy of perm
-  int* lface = nullptr;    // leaf-ordered original face ids
+  float* lcomp = nullptr;  // leaf-ordered compact faces: 3 float4 (a.xyz b.x)(b.yz c.xy)(c.z, face bits, 0, 0)
   int64_t nnodes = 0, nleaves = 0;
+  int bvh_depth = 0, bvh_max_leaf = 0;
 };
 
 namespace rt {

@@ -13,6 +13,8 @@
 // no t_min (Q3), no renormalisation after reflect (Q4), traced_paths is scratch (Q6).
 #include <math.h>
 
+#include <hipcub/hipcub.hpp>
+
 #include "rt_bvh.h"
 #include "rt_device.h"
 #include "rt_internal.h"
@@ -36,6 +38,7 @@ struct TraceArgs {
   uint32_t* mask;   // (n) or null
   int32_t* hit_kind;  // (n, B) or null
   int32_t* hit_face;  // (n, B) or null
+  const int32_t* order;  // processing order of the rows (null = identity), see launch_trace
 };
 
 // Closest hit over a brute-force face list whose permuted table lives at `tab`
@@ -107,7 +110,8 @@ __global__ __launch_bounds__(256) void k_trace_bf(TraceArgs a) {
 
   const float qnan = __builtin_nanf("");
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; row < a.n; row += stride) {
+  for (int64_t irow = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; irow < a.n; irow += stride) {
+    const int64_t row = a.order ? (int64_t)a.order[irow] : irow;
     const int64_t gid = a.ray_offset + row;
     float3 dir = rt::ray_dir(gid);
     float3 pos = make_float3(a.tx[0], a.tx[1], a.tx[2]);
@@ -188,7 +192,8 @@ __global__ __launch_bounds__(256) void k_trace_bf_generic(TraceArgs a, int B) {
   const int P = B + 1;
   const float qnan = __builtin_nanf("");
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; row < a.n; row += stride) {
+  for (int64_t irow = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; irow < a.n; irow += stride) {
+    const int64_t row = a.order ? (int64_t)a.order[irow] : irow;
     const int64_t gid = a.ray_offset + row;
     float3 dir = rt::ray_dir(gid);
     float3 pos = make_float3(a.tx[0], a.tx[1], a.tx[2]);
@@ -249,10 +254,35 @@ __global__ __launch_bounds__(256) void k_trace_bf_generic(TraceArgs a, int B) {
   }
 }
 
+// Sort key of a ray: the cell of its initial direction on a 256x256 octahedral map, in Morton
+// order, so that rays traced by one wave start in nearly the same direction.  Only the order in
+// which rows are processed changes; every row is computed exactly as before.
+__global__ __launch_bounds__(256) void k_dir_keys(int64_t ray_offset, int64_t n, uint16_t* keys, int32_t* rows) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float3 d = rt::ray_dir(ray_offset + i);
+  const float s = fabsf(d.x) + fabsf(d.y) + fabsf(d.z);
+  float x = d.x / s, y = d.y / s;
+  if (d.z < 0.0f) {
+    const float ox = x;
+    x = (1.0f - fabsf(y)) * (ox < 0.0f ? -1.0f : 1.0f);
+    y = (1.0f - fabsf(ox)) * (y < 0.0f ? -1.0f : 1.0f);
+  }
+  const uint32_t cx = (uint32_t)fminf(fmaxf((x + 1.0f) * 128.0f, 0.0f), 255.0f);
+  const uint32_t cy = (uint32_t)fminf(fmaxf((y + 1.0f) * 128.0f, 0.0f), 255.0f);
+  uint32_t k = 0;
+#pragma unroll
+  for (int b = 0; b < 8; ++b) k |= ((cx >> b) & 1u) << (2 * b) | ((cy >> b) & 1u) << (2 * b + 1);
+  keys[i] = (uint16_t)k;
+  rows[i] = (int32_t)i;
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------ launch (C++ side of rt_trace)
 namespace rt {
+
+constexpr int64_t kSortMinRays = 1 << 16;
 
 int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B, int64_t ray_offset, int64_t n,
                  float* traced, float* received, uint32_t* mask, int32_t* hit_kind, int32_t* hit_face,
@@ -262,7 +292,7 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
   a.env_perm = env->perm;
   a.env_nrm = env->nrm;
   a.env_nf = (int)env->nf;
-  a.env_bvh = rt::BvhView{(const float4*)env->nodes, (const int2*)env->leaves, (const float4*)env->lperm, env->lface};
+  a.env_bvh = rt::BvhView{(const float4*)env->nodes, (const int2*)env->leaves, (const float4*)env->lcomp};
   const bool bvh = env->nodes != nullptr;
   a.rx_perm = rx ? rx->perm : nullptr;
   a.rx_nf = rx ? (int)rx->nf : 0;
@@ -278,6 +308,7 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
   a.mask = mask;
   a.hit_kind = hit_kind;
   a.hit_face = hit_face;
+  a.order = nullptr;
   const size_t lds = bvh ? 0 : (size_t)env->nf * 18 * sizeof(float4);
   int dev_cu = 256;
   const int64_t want = (n + 255) / 256;
@@ -288,6 +319,24 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
   if (traced == nullptr && B > 8) {
     set_error("rt_trace: max_bounces > 8 requires the traced buffer (scratch rows)");
     return -1;
+  }
+  // BVH meshes: trace the rows in direction-sorted order (K4: 2.98 -> 2.06 ms);
+  // brute-force meshes gain nothing from it (every face is tested anyway) and keep row order.
+  void* sort_ws = nullptr;
+  if (bvh && n >= kSortMinRays && n <= INT32_MAX) {
+    size_t cub_bytes = 0;
+    RT_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (uint16_t*)nullptr, (uint16_t*)nullptr,
+                                              (int32_t*)nullptr, (int32_t*)nullptr, (int)n, 0, 16, stream));
+    const size_t kb = ((size_t)n * 2 + 255) / 256 * 256, rb = (size_t)n * 4;
+    RT_HIP(hipMallocAsync(&sort_ws, 2 * kb + 2 * rb + cub_bytes, stream));
+    uint16_t* k_in = (uint16_t*)sort_ws;
+    uint16_t* k_out = (uint16_t*)((char*)sort_ws + kb);
+    int32_t* r_in = (int32_t*)((char*)sort_ws + 2 * kb);
+    int32_t* r_out = (int32_t*)((char*)sort_ws + 2 * kb + rb);
+    void* tmp = (char*)sort_ws + 2 * kb + 2 * rb;
+    hipLaunchKernelGGL(k_dir_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, ray_offset, n, k_in, r_in);
+    RT_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, cub_bytes, k_in, k_out, r_in, r_out, (int)n, 0, 16, stream));
+    a.order = r_out;
   }
   switch (B) {
 #define RT_CASE(BB)                                                                     \
@@ -307,6 +356,7 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
       break;
   }
   RT_HIP(hipGetLastError());
+  if (sort_ws) RT_HIP(hipFreeAsync(sort_ws, stream));
   return 0;
 }
 

@@ -11,21 +11,27 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def child(n, B, reps):
+def child(n, B, reps, scene="room"):
     sys.path.insert(0, ROOT)
     import numpy as np
     import torch
     from rf_ray_tracing_warp_amd._lib import DeviceMesh, check, lib, ptr
     from rf_ray_tracing_warp_amd.mesh import load_stl, sphere
-    m = load_stl(os.path.join(ROOT, "models/room.stl"))
+    if scene == "terrain":  # K4: the apollo stand-in, TX/RX as main.py:22-23
+        from rf_ray_tracing_warp_amd.mesh import synthetic_terrain
+        m = synthetic_terrain(1024, 50.0)
+        txp, rxp = (10.0, 0.0, 4.5), (-10.125, 0.0, 4.8)
+    else:
+        m = load_stl(os.path.join(ROOT, "models/room.stl"))
+        txp, rxp = (10.0, 0.0, 5.0), (-10.0, 0.0, 5.0)
     env = DeviceMesh(m.vertices, m.faces, 0)
-    rs = sphere((-10, 0, 5), 0.1, 1)
+    rs = sphere(rxp, 0.1, 1)
     rx = DeviceMesh(rs.vertices, rs.faces, 0)
     P = B + 1
     tr = torch.empty((n, P, 3), dtype=torch.float32, device="cuda")
     rc = torch.empty((n, P, 3), dtype=torch.float32, device="cuda")
     mk = torch.empty(n, dtype=torch.int32, device="cuda")
-    tx = np.asarray((10, 0, 5), np.float32)
+    tx = np.asarray(txp, np.float32)
     st = torch.cuda.current_stream()
     L = lib()
 
@@ -41,19 +47,22 @@ def child(n, B, reps):
         go()
     e1.record(st)
     torch.cuda.synchronize()
-    print(json.dumps({"variant": os.environ.get("RFRT_TRACE_VARIANT", "0"), "us": e0.elapsed_time(e1) * 1e3 / reps,
-                      "hash": h[:16]}))
+    print(json.dumps({"variant": os.environ.get(os.environ.get("VAR_ENV", "RFRT_TRACE_VARIANT"), "0"),
+                      "us": e0.elapsed_time(e1) * 1e3 / reps, "hash": h[:16], "bvh": env.bvh_info()}))
 
 
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "child":
-        child(int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]))
+        child(int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), sys.argv[5])
         sys.exit(0)
     variants = os.environ.get("VARIANTS", "0 1 3").split()
     res = []
     for v in variants:
-        env = dict(os.environ, RFRT_TRACE_VARIANT=v)
-        out = subprocess.run([sys.executable, __file__, "child", "1000000", "3", "50"], env=env, capture_output=True,
+        env = dict(os.environ)
+        env[os.environ.get("VAR_ENV", "RFRT_TRACE_VARIANT")] = v
+        scene = os.environ.get("SCENE", "room")
+        n, B, reps = ("2097152", "5", "5") if scene == "terrain" else ("1000000", "3", "50")
+        out = subprocess.run([sys.executable, __file__, "child", n, B, reps, scene], env=env, capture_output=True,
                              text=True, timeout=300)
         if out.returncode != 0:
             print(out.stderr[-2000:])
