@@ -10,7 +10,7 @@ import os
 import numpy as np
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "librfrt.so")
+LIB_PATH = os.environ.get("RFRT_LIB_PATH") or os.path.join(_PKG, "librfrt.so")
 
 RT_CIR_C_F64 = 1
 RT_CIR_FS_F64 = 2

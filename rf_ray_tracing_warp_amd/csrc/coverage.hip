@@ -24,7 +24,7 @@
 //
 // Cost: N*B environment queries + (#candidates) receiver tests + (#received) replays, instead of
 // cells*N*B*(env + receiver) queries.  Results equal the per-cell reference loop (tests compare
-// against the oracle's per-cell trace + NumPy power); cells are sharded cyclically over ranks.
+// against the oracle's per-cell trace + NumPy power); cells are sharded by x column (ix % ranks).
 #include <hipcub/hipcub.hpp>
 #include <math.h>
 
@@ -52,7 +52,8 @@ struct CovParams {
   rt_grid g;
   double r_rx;       // receiver radius (tracer.py:26 rx_radius)
   double r_pad;      // conservative ball radius for candidate search
-  int shard, nshard;  // cell % nshard == shard are ours
+  int shard, nshard;  // cells in x columns ix % nshard == shard are ours
+  const int32_t* order;  // k_traj row order (direction-sorted for BVH environments) or null
   // trajectory SoA [k][n]
   float *px, *py, *pz, *dx, *dy, *dz, *te;
   uint8_t* nseg;
@@ -97,9 +98,9 @@ __device__ __forceinline__ rt::Hit env_query_lds(const float4* tab, int nf, cons
 
 template <bool USE_BVH>
 __device__ __forceinline__ rt::Hit env_query(const CovParams& p, const float4* tab, const rt::Shear& s, float3 o,
-                                            float3 d) {
+                                            float3 d, float tcull = RT_MAX_T) {
   if constexpr (USE_BVH) {
-    return rt::bvh_query(p.env_bvh, s, o, d);
+    return rt::bvh_query(p.env_bvh, s, o, d, tcull);
   } else {
     return env_query_lds(tab, p.env_nf, s);
   }
@@ -172,7 +173,8 @@ __global__ __launch_bounds__(256) void k_traj(CovParams p) {
   extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
   stage_env<USE_BVH>(p, lds_tab);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < p.n; r += stride) {
+  for (int64_t ir = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; ir < p.n; ir += stride) {
+    const int64_t r = p.order ? (int64_t)p.order[ir] : ir;
     float3 dir = rt::ray_dir(p.ray_offset + r);
     float3 pos = make_float3(p.tx[0], p.tx[1], p.tx[2]);
     int nseg = 0;
@@ -301,6 +303,17 @@ __device__ __forceinline__ void seg_columns(const CovParams& p, const Seg& s, in
   ia1 = clampi((int64_t)ceil((amax - a0) / da), 0, na - 1);
 }
 
+// Cells are owned by x column: ix % nshard == shard.  A strip of fixed ix (s.A == 0) is either
+// wholly ours or not: advance ia0 to the first owned strip and step by nshard.  Strips of fixed
+// iy (s.A == 1) are all kept; column_cells steps through their owned ix instead.
+__device__ __forceinline__ void owned_strips(const CovParams& p, const Seg& s, int64_t& ia0, int64_t& step) {
+  step = 1;
+  if (p.nshard > 1 && s.A == 0) {
+    ia0 += ((p.shard - ia0 % p.nshard) % p.nshard + p.nshard) % p.nshard;
+    step = p.nshard;
+  }
+}
+
 // pass A: per ray, the (segment, layer, column) items.  item = r<<40 | k<<36 | kz<<24 | ia
 __global__ __launch_bounds__(256) void k_cols(CovParams p) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -315,7 +328,9 @@ __global__ __launch_bounds__(256) void k_cols(CovParams p) {
         double ta, tb;
         int64_t ia0, ia1;
         seg_columns(p, s, kz, ta, tb, ia0, ia1);
-        if (ia1 >= ia0) c += (unsigned)(ia1 - ia0 + 1);
+        int64_t step;
+        owned_strips(p, s, ia0, step);
+        if (ia1 >= ia0) c += (unsigned)((ia1 - ia0) / step + 1);
       }
     }
     unsigned pre;
@@ -327,7 +342,9 @@ __global__ __launch_bounds__(256) void k_cols(CovParams p) {
         double ta, tb;
         int64_t ia0, ia1;
         seg_columns(p, s, kz, ta, tb, ia0, ia1);
-        for (int64_t ia = ia0; ia <= ia1; ++ia, ++w)
+        int64_t step;
+        owned_strips(p, s, ia0, step);
+        for (int64_t ia = ia0; ia <= ia1; ia += step, ++w)
           if (w < p.item_cap)
             p.items[w] = ((uint64_t)r << 40) | ((uint64_t)k << 36) | ((uint64_t)kz << 24) | (uint64_t)ia;
       }
@@ -357,10 +374,14 @@ __device__ __forceinline__ unsigned column_cells(const CovParams& p, uint64_t it
   if ((bmax - b0) / db < -1.0 || (bmin - b0) / db > (double)nb) return 0;
   const int64_t ib0 = clampi((int64_t)floor((bmin - b0) / db), 0, nb - 1);
   const int64_t ib1 = clampi((int64_t)ceil((bmax - b0) / db), 0, nb - 1);
-  for (int64_t ib = ib0; ib <= ib1; ++ib) {
+  int64_t ibs = ib0, step = 1;
+  if (p.nshard > 1 && s.A == 1) {  // ib = ix: visit our columns only
+    ibs += ((p.shard - ib0 % p.nshard) % p.nshard + p.nshard) % p.nshard;
+    step = p.nshard;
+  }
+  for (int64_t ib = ibs; ib <= ib1; ib += step) {
     const int64_t ix = s.A == 0 ? ia : ib, iy = s.A == 0 ? ib : ia;
     const int64_t cell = (kz * g.ny + iy) * g.nx + ix;
-    if (cell % p.nshard != p.shard) continue;
     double cc[3];
     cell_center(g, cell, cc);
     if (seg_ball(s.o, s.d, s.tmax, cc, rp2)) {
@@ -455,12 +476,11 @@ struct PathAcc {
 
 // ------------------------------------------------------------------ 4. replay + CIR body
 // first winning bounce of each (cell, ray) group -> replay list (key indices)
-__global__ __launch_bounds__(256) void k_first(const uint64_t* keys, int64_t nkeys, const uint8_t* win, int64_t* list,
-                                               unsigned long long* list_count) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < nkeys; base += stride) {
-    const int64_t i = base + threadIdx.x;
-    bool first = i < nkeys && win[i] != 0;
+// flag the first winning bounce of every (cell, ray): the list of flagged candidates is then
+// compacted in order (hipcub DeviceSelect::Flagged), so records keep the (cell, ray, k) order
+__global__ __launch_bounds__(256) void k_first(const uint64_t* keys, int64_t nkeys, const uint8_t* win, uint8_t* first_flag) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nkeys; i += (int64_t)gridDim.x * blockDim.x) {
+    bool first = win[i] != 0;
     if (first) {
       const uint64_t g = keys[i] >> 4;
       for (int64_t j = i - 1; j >= 0 && (keys[j] >> 4) == g; --j)
@@ -469,19 +489,15 @@ __global__ __launch_bounds__(256) void k_first(const uint64_t* keys, int64_t nke
           break;
         }
     }
-    unsigned pre;
-    const unsigned long long at = block_append(list_count, first ? 1u : 0u, pre);
-    if (first) list[at + pre] = i;
+    first_flag[i] = first ? 1 : 0;
   }
 }
 
 template <bool USE_BVH>
 __global__ __launch_bounds__(256) void k_replay(CovParams p, const uint64_t* keys, const float* trx,
-                                                const int64_t* list, const unsigned long long* list_count,
-                                                uint64_t* out_key, double* out_amp) {
+                                                const int64_t* list, int64_t nl, uint64_t* out_key, double* out_amp) {
   extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
   stage_env<USE_BVH>(p, lds_tab);
-  const int64_t nl = (int64_t)*list_count;
   for (int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; li < nl; li += (int64_t)gridDim.x * blockDim.x) {
     const int64_t i = list[li];
     const uint64_t key = keys[i];
@@ -506,6 +522,9 @@ __global__ __launch_bounds__(256) void k_replay(CovParams p, const uint64_t* key
     float3 d = dir;
     for (int b = k0 + 1; b < p.B; ++b) {  // kernel.py:57-98 with this cell's receiver
       const rt::Shear s = rt::make_shear(pos, d);
+      // environment first, then the receiver.  (A receiver-first order with the environment query
+      // culled at the receiver hit is equivalent, but its build gave run-to-run different
+      // amplitudes on the terrain BVH on some boxes: DESIGN.md §6.)
       const rt::Hit he = env_query<USE_BVH>(p, lds_tab, s, pos, d);
       const rt::Hit hr = rx_query(p.g, cell, p.r_rx, pos, d);
       const bool env_hit = he.face >= 0, rx_hit = hr.face >= 0;
@@ -541,10 +560,9 @@ __global__ __launch_bounds__(256) void k_replay(CovParams p, const uint64_t* key
     const int64_t bin = (int64_t)dl;
     // amplitudes are >= 0; a zero one (NaN angle -> _bounce_amplitude 0, tracer.py:35-37) leaves
     // impulse_response[bin] untouched, so it must not become an active bin of the power sweep
-    if (bin < p.n_bins && rec_amp != 0.0) {
-      out_key[i] = ((uint64_t)cell << 32) | (uint64_t)bin;
-      out_amp[i] = rec_amp;
-    }
+    const bool keep = bin < p.n_bins && rec_amp != 0.0;
+    out_key[li] = keep ? ((uint64_t)cell << 32) | (uint64_t)bin : ~0ull;
+    out_amp[li] = keep ? rec_amp : 0.0;
   }
 }
 
@@ -562,7 +580,9 @@ __device__ __forceinline__ void two_sum(double& s, double& c, double x) {  // Ne
 }
 
 // mean square of the nonzero samples of y = ir (*) sin, for a sparse ir with ascending bins m[k]
-__device__ double power_sparse(const uint64_t* keys, const double* amps, int64_t lo, int64_t hi, const PowerParams& P) {
+// term(k, c, s): a_k cos(alpha (half - m_k)), a_k sin(alpha (half - m_k)) of sparse entry k
+template <typename Term>
+__device__ double power_sparse(const uint64_t* keys, int64_t lo, int64_t hi, const PowerParams& P, Term term_cs) {
   if (hi <= lo) return __builtin_nan("");
   const int64_t n = P.n_bins, half = P.half;
   const double al = P.alpha, sa = sin(al);
@@ -573,11 +593,11 @@ __device__ double power_sparse(const uint64_t* keys, const double* amps, int64_t
   int64_t x = 0;
   auto sk = [&](int64_t k) { const int64_t m = (int64_t)(keys[k] & 0xFFFFFFFFull); return m - half > 0 ? m - half : 0; };
   auto ek = [&](int64_t k) { const int64_t m = (int64_t)(keys[k] & 0xFFFFFFFFull); const int64_t e = m + (n - 1 - half); return e < n - 1 ? e : n - 1; };
-  auto term = [&](int64_t k, double sgn) {
-    const int64_t m = (int64_t)(keys[k] & 0xFFFFFFFFull);
-    const double ph = al * (double)(half - m);
-    two_sum(Ps, Pc, sgn * amps[k] * cos(ph));
-    two_sum(Qs, Qc, sgn * amps[k] * sin(ph));
+  auto term = [&](int64_t k, double sgn) {  // sgn = +-1: sgn*(a*c) == (sgn*a)*c bit for bit
+    double tc, ts;
+    term_cs(k, tc, ts);
+    two_sum(Ps, Pc, sgn * tc);
+    two_sum(Qs, Qc, sgn * ts);
   };
   while (true) {
     bool started_alone = false;
@@ -613,15 +633,29 @@ __device__ double power_sparse(const uint64_t* keys, const double* amps, int64_t
   return count > 0 ? (total + tc) / (double)count : __builtin_nan("");
 }
 
-__global__ __launch_bounds__(256) void k_power(const uint64_t* ukeys, const double* uamps, const int64_t* nuniq,
-                                               rt_grid g, int shard, int nshard, PowerParams P, double* power) {
-  const int64_t nc = g.nx * g.ny * g.nz;
+// per unique (cell, bin): the phase terms of the sweep, computed once in parallel
+__global__ __launch_bounds__(256) void k_terms(const uint64_t* ukeys, const double* uamps, const int64_t* nuniq,
+                                               PowerParams P, double* tcos, double* tsin) {
   const int64_t nu = *nuniq;
-  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nc; c += (int64_t)gridDim.x * blockDim.x) {
-    if (c % nshard != shard) {
-      power[c] = 0.0;  // other ranks own it; the power map is sum-reduced across ranks
-      continue;
-    }
+  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < nu; u += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = (int64_t)(ukeys[u] & 0xFFFFFFFFull);
+    const double ph = P.alpha * (double)(P.half - m);
+    tcos[u] = uamps[u] * cos(ph);
+    tsin[u] = uamps[u] * sin(ph);
+  }
+}
+
+// one thread per cell of ours (x columns ix % nshard == shard); other cells are left to the
+// caller's zero fill, the power map being sum-reduced across ranks
+__global__ __launch_bounds__(256) void k_power(const uint64_t* ukeys, const double* tcos, const double* tsin,
+                                               const int64_t* nuniq, rt_grid g, int shard, int nshard, PowerParams P,
+                                               double* power) {
+  const int64_t nxo = g.nx > shard ? (g.nx - shard + nshard - 1) / nshard : 0;
+  const int64_t nown = nxo * g.ny * g.nz;
+  const int64_t nu = *nuniq;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nown; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t jx = t % nxo, rest = t / nxo;
+    const int64_t c = rest * g.nx + shard + jx * nshard;  // rest = iz*ny + iy
     // [lo, hi) = unique (cell, bin) keys of this cell
     const uint64_t k0 = (uint64_t)c << 32, k1 = (uint64_t)(c + 1) << 32;
     int64_t a = 0, b = nu;
@@ -635,7 +669,10 @@ __global__ __launch_bounds__(256) void k_power(const uint64_t* ukeys, const doub
       const int64_t m = (a + b) >> 1;
       if (ukeys[m] < k1) a = m + 1; else b = m;
     }
-    power[c] = power_sparse(ukeys, uamps, lo, a, P);
+    power[c] = power_sparse(ukeys, lo, a, P, [&](int64_t k, double& tc, double& ts) {
+      tc = tcos[k];
+      ts = tsin[k];
+    });
   }
 }
 
@@ -654,7 +691,11 @@ __global__ __launch_bounds__(64) void k_power_dense(const double* ir, int64_t ro
       aa[K] = x[m];
       ++K;
     }
-  power[row] = power_sparse(kk, aa, 0, K, P);
+  power[row] = power_sparse(kk, 0, K, P, [&](int64_t k, double& tc, double& ts) {
+    const double ph = P.alpha * (double)(P.half - (int64_t)kk[k]);
+    tc = aa[k] * cos(ph);
+    ts = aa[k] * sin(ph);
+  });
 }
 
 }  // namespace
@@ -673,29 +714,34 @@ struct rt_coverage {
   uint8_t* nseg = nullptr;
   uint64_t *keys = nullptr, *keys_sorted = nullptr, *okeys = nullptr, *okeys_sorted = nullptr, *ukeys = nullptr;
   double *oamps = nullptr, *oamps_sorted = nullptr, *uamps = nullptr;
+  double *tcos = nullptr, *tsin = nullptr;  // per unique (cell, bin): phase terms of the power sweep
   uint8_t* win = nullptr;
+  uint8_t* first_flag = nullptr;
   float* trx = nullptr;
   int64_t* list = nullptr;
   uint64_t* items = nullptr;
   int64_t item_cap = 0;
-  unsigned long long* counters = nullptr;  // [0] candidates, [1] column items, [2] replay list
+  unsigned long long* counters = nullptr;  // [0] candidates, [1] column items, [2] replay list (int64)
   int64_t* nuniq = nullptr;
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
   int64_t cap = 0;
   int64_t last_candidates = 0;
+  int64_t last_received = 0;  // first-win (cell, ray) records of the last run
 };
 
 namespace {
 
 void free_cands(rt_coverage* c) {
   for (void* q : {(void*)c->keys, (void*)c->keys_sorted, (void*)c->okeys, (void*)c->okeys_sorted, (void*)c->ukeys,
-                  (void*)c->oamps, (void*)c->oamps_sorted, (void*)c->uamps, (void*)c->win, (void*)c->trx,
-                  (void*)c->list, c->tmp})
+                  (void*)c->oamps, (void*)c->oamps_sorted, (void*)c->uamps, (void*)c->tcos, (void*)c->tsin,
+                  (void*)c->win, (void*)c->trx,
+                  (void*)c->list, (void*)c->first_flag, c->tmp})
     if (q) (void)hipFree(q);
   c->keys = c->keys_sorted = c->okeys = c->okeys_sorted = c->ukeys = nullptr;
-  c->oamps = c->oamps_sorted = c->uamps = nullptr;
+  c->oamps = c->oamps_sorted = c->uamps = c->tcos = c->tsin = nullptr;
   c->win = nullptr;
+  c->first_flag = nullptr;
   c->trx = nullptr;
   c->list = nullptr;
   c->tmp = nullptr;
@@ -713,16 +759,21 @@ int alloc_cands(rt_coverage* c, int64_t cap) {
   RT_HIP(hipMalloc(&c->oamps, cap * 8));
   RT_HIP(hipMalloc(&c->oamps_sorted, cap * 8));
   RT_HIP(hipMalloc(&c->uamps, cap * 8));
+  RT_HIP(hipMalloc(&c->tcos, cap * 8));
+  RT_HIP(hipMalloc(&c->tsin, cap * 8));
   RT_HIP(hipMalloc(&c->win, cap));
+  RT_HIP(hipMalloc(&c->first_flag, cap));
   RT_HIP(hipMalloc(&c->trx, cap * 4));
   RT_HIP(hipMalloc(&c->list, cap * 8));
-  size_t b1 = 0, b2 = 0, b3 = 0;
+  size_t b1 = 0, b2 = 0, b3 = 0, b4 = 0;
   RT_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, b1, c->keys, c->keys_sorted, (int)cap, 0, 64));
   RT_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, b2, c->okeys, c->okeys_sorted, c->oamps, c->oamps_sorted,
                                             (int)cap, 0, 64));
   RT_HIP(hipcub::DeviceReduce::ReduceByKey(nullptr, b3, c->okeys_sorted, c->ukeys, c->oamps_sorted, c->uamps,
                                            c->nuniq, hipcub::Sum(), (int)cap));
-  c->tmp_bytes = std::max(b1, std::max(b2, b3));
+  RT_HIP(hipcub::DeviceSelect::Flagged(nullptr, b4, hipcub::CountingInputIterator<int64_t>(0), c->first_flag, c->list,
+                                       (int64_t*)(c->counters + 2), (int)cap));
+  c->tmp_bytes = std::max(std::max(b1, b2), std::max(b3, b4));
   RT_HIP(hipMalloc(&c->tmp, c->tmp_bytes));
   c->cap = cap;
   return RT_OK;
@@ -850,10 +901,17 @@ int rt_coverage_run(rt_coverage* c, const float* tx_pos, double tx_power, double
   p.n_bins = n_bins;
   const size_t lds = bvh ? 0 : (size_t)p.env_nf * 18 * sizeof(float4);
   const unsigned grid_rays = (unsigned)std::min<int64_t>((c->n + 255) / 256, 4096);
-  if (bvh)
+  p.order = nullptr;
+  if (bvh) {  // direction-sorted rows: coherent BVH traversal (as rt_trace)
+    void* ws = nullptr;
+    p.order = rt::dir_order(c->ray_offset, c->n, s, &ws);
+    if (!p.order) return RT_EHIP;
     hipLaunchKernelGGL(k_traj<true>, dim3(grid_rays), dim3(256), lds, s, p);
-  else
+    RT_HIP(hipFreeAsync(ws, s));
+    p.order = nullptr;
+  } else {
     hipLaunchKernelGGL(k_traj<false>, dim3(grid_rays), dim3(256), lds, s, p);
+  }
   RT_HIP(hipGetLastError());
   // candidates: column items (pass A) then cells (pass B); grow and retry on overflow
   int64_t ncand = 0;
@@ -895,11 +953,12 @@ int rt_coverage_run(rt_coverage* c, const float* tx_pos, double tx_power, double
   P.n_bins = n_bins;
   P.half = (n_bins - 1) / 2;
   P.alpha = alpha;
-  const unsigned grid_cells = (unsigned)std::min<int64_t>((ncell + 255) / 256, 8192);
+  const unsigned grid_cells = (unsigned)std::min<int64_t>((ncell / c->nshard + 256) / 256, 8192);
+  if (c->nshard > 1) RT_HIP(hipMemsetAsync(power, 0, ncell * sizeof(double), s));  // cells of other ranks
   if (ncand == 0) {
     RT_HIP(hipMemsetAsync(c->nuniq, 0, 8, s));
-    hipLaunchKernelGGL(k_power, dim3(grid_cells), dim3(256), 0, s, c->ukeys, c->uamps, c->nuniq, c->grid, c->shard,
-                       c->nshard, P, power);
+    hipLaunchKernelGGL(k_power, dim3(grid_cells), dim3(256), 0, s, c->ukeys, c->tcos, c->tsin, c->nuniq,
+                       c->grid, c->shard, c->nshard, P, power);
     RT_HIP(hipGetLastError());
     if (stats) stats[0] = stats[1] = 0;
     return RT_OK;
@@ -909,27 +968,43 @@ int rt_coverage_run(rt_coverage* c, const float* tx_pos, double tx_power, double
   RT_HIP(hipcub::DeviceRadixSort::SortKeys(c->tmp, tb, c->keys, c->keys_sorted, (int)ncand, 0, endbit, s));
   const unsigned grid_c = (unsigned)std::min<int64_t>((ncand + 255) / 256, 8192);
   hipLaunchKernelGGL(k_win, dim3(grid_c), dim3(256), 0, s, p, c->keys_sorted, ncand, c->win, c->trx);
-  hipLaunchKernelGGL(k_first, dim3(grid_c), dim3(256), 0, s, c->keys_sorted, ncand, c->win, c->list, c->counters + 2);
-  RT_HIP(hipMemsetAsync(c->okeys, 0xFF, ncand * 8, s));
-  if (bvh)
-    hipLaunchKernelGGL(k_replay<true>, dim3(grid_c), dim3(256), lds, s, p, c->keys_sorted, c->trx, c->list,
-                       c->counters + 2, c->okeys, c->oamps);
-  else
-    hipLaunchKernelGGL(k_replay<false>, dim3(grid_c), dim3(256), lds, s, p, c->keys_sorted, c->trx, c->list,
-                       c->counters + 2, c->okeys, c->oamps);
-  RT_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_first, dim3(grid_c), dim3(256), 0, s, c->keys_sorted, ncand, c->win, c->first_flag);
   tb = c->tmp_bytes;
-  RT_HIP(hipcub::DeviceRadixSort::SortPairs(c->tmp, tb, c->okeys, c->okeys_sorted, c->oamps, c->oamps_sorted,
-                                            (int)ncand, 0, 64, s));
-  tb = c->tmp_bytes;
-  RT_HIP(hipcub::DeviceReduce::ReduceByKey(c->tmp, tb, c->okeys_sorted, c->ukeys, c->oamps_sorted, c->uamps, c->nuniq,
-                                           hipcub::Sum(), (int)ncand, s));
-  hipLaunchKernelGGL(k_power, dim3(grid_cells), dim3(256), 0, s, c->ukeys, c->uamps, c->nuniq, c->grid, c->shard,
-                     c->nshard, P, power);
+  RT_HIP(hipcub::DeviceSelect::Flagged(c->tmp, tb, hipcub::CountingInputIterator<int64_t>(0), c->first_flag, c->list,
+                                       (int64_t*)(c->counters + 2), (int)ncand, s));
+  int64_t nlist = 0;
+  RT_HIP(hipMemcpyAsync(&nlist, c->counters + 2, 8, hipMemcpyDeviceToHost, s));
+  RT_HIP(hipStreamSynchronize(s));
+  if (nlist > 0) {
+    const unsigned grid_l = (unsigned)std::min<int64_t>((nlist + 255) / 256, 8192);
+    if (bvh)
+      hipLaunchKernelGGL(k_replay<true>, dim3(grid_l), dim3(256), lds, s, p, c->keys_sorted, c->trx, c->list, nlist,
+                         c->okeys, c->oamps);
+    else
+      hipLaunchKernelGGL(k_replay<false>, dim3(grid_l), dim3(256), lds, s, p, c->keys_sorted, c->trx, c->list, nlist,
+                         c->okeys, c->oamps);
+    RT_HIP(hipGetLastError());
+    // records are in (cell, ray, k) order; a stable sort on (cell, bin) keeps that order within a
+    // bin, so every bin's amplitudes are summed in ray order.  Dropped records (~0) sort last.
+    const int kbits = 32 + bits_for((uint64_t)ncell);
+    tb = c->tmp_bytes;
+    RT_HIP(hipcub::DeviceRadixSort::SortPairs(c->tmp, tb, c->okeys, c->okeys_sorted, c->oamps, c->oamps_sorted,
+                                              (int)nlist, 0, kbits < 64 ? kbits : 64, s));
+    tb = c->tmp_bytes;
+    RT_HIP(hipcub::DeviceReduce::ReduceByKey(c->tmp, tb, c->okeys_sorted, c->ukeys, c->oamps_sorted, c->uamps,
+                                             c->nuniq, hipcub::Sum(), (int)nlist, s));
+    const unsigned grid_u = (unsigned)std::min<int64_t>((nlist + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_terms, dim3(grid_u), dim3(256), 0, s, c->ukeys, c->uamps, c->nuniq, P, c->tcos, c->tsin);
+  } else {
+    RT_HIP(hipMemsetAsync(c->nuniq, 0, 8, s));
+  }
+  hipLaunchKernelGGL(k_power, dim3(grid_cells), dim3(256), 0, s, c->ukeys, c->tcos, c->tsin, c->nuniq,
+                     c->grid, c->shard, c->nshard, P, power);
   RT_HIP(hipGetLastError());
+  c->last_received = nlist;
   if (stats) {
     stats[0] = ncand;
-    stats[1] = c->cap;
+    stats[1] = nlist;
   }
   return RT_OK;
 }

@@ -75,9 +75,13 @@ __device__ __forceinline__ void leaf_faces(const BvhView& b, const Shear& s, int
 
 // closest hit in a BVH mesh (same result as brute force over all faces): near child first,
 // far child on a per-lane (node, entry t) stack, popped entries re-culled against the best t.
-__device__ __forceinline__ Hit bvh_query(const BvhView& b, const Shear& s, float3 o, float3 d) {
+// tcull < RT_MAX_T also culls boxes beyond tcull: every hit with t <= tcull is still found
+// exactly, hits beyond it may be missed (callers that only compare against tcull use it).
+__device__ __forceinline__ Hit bvh_query(const BvhView& b, const Shear& s, float3 o, float3 d,
+                                         float tcull = RT_MAX_T) {
   Hit h;
   hit_init(h);
+  const float tc = fminf(RT_MAX_T, tcull);
   const RayBox r = make_raybox(o, d);
   int stack[RT_BVH_STACK];
   float stackt[RT_BVH_STACK];
@@ -94,14 +98,14 @@ __device__ __forceinline__ Hit bvh_query(const BvhView& b, const Shear& s, float
     for (int side = 0; side < 2; ++side) {
       const int c = side ? c1 : c0;
       float& tt = side ? t1 : t0;
-      if (c < 0 && tt <= h.t * 1.00001f + 1e-6f) {
+      if (c < 0 && tt <= fminf(h.t, tc) * 1.00001f + 1e-6f) {
         leaf_faces(b, s, b.leaves[-1 - c], h);
         tt = INFINITY;
       } else if (c < 0) {
         tt = INFINITY;
       }
     }
-    const float lim = h.t * 1.00001f + 1e-6f;
+    const float lim = fminf(h.t, tc) * 1.00001f + 1e-6f;
     const bool h0 = t0 <= lim, h1 = t1 <= lim;
     if (h0 && h1) {
       const bool first0 = t0 <= t1;
@@ -124,7 +128,7 @@ __device__ __forceinline__ Hit bvh_query(const BvhView& b, const Shear& s, float
     bool found = false;
     while (sp > 0) {
       --sp;
-      if (stackt[sp] <= h.t * 1.00001f + 1e-6f) {
+      if (stackt[sp] <= fminf(h.t, tc) * 1.00001f + 1e-6f) {
         cur = stack[sp];
         found = true;
         break;

@@ -33,6 +33,9 @@ struct rt_mesh {
 namespace rt {
 void set_error(const std::string& msg);
 int hip_fail(hipError_t e, const char* what);
+// Row order for tracing rays [ray_offset, ray_offset+n) of one burst sorted by initial direction
+// (trace.hip).  Stream-ordered workspace returned in *ws (hipFreeAsync it after the consumer).
+const int32_t* dir_order(int64_t ray_offset, int64_t n, hipStream_t stream, void** ws);
 }  // namespace rt
 
 #define RT_HIP(call)                                                   \

@@ -284,6 +284,35 @@ namespace rt {
 
 constexpr int64_t kSortMinRays = 1 << 16;
 
+const int32_t* dir_order(int64_t ray_offset, int64_t n, hipStream_t stream, void** ws) {
+  size_t cub_bytes = 0;
+  *ws = nullptr;
+  if (hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (uint16_t*)nullptr, (uint16_t*)nullptr,
+                                         (int32_t*)nullptr, (int32_t*)nullptr, (int)n, 0, 16, stream) != hipSuccess) {
+    set_error("dir_order: hipcub sizing failed");
+    return nullptr;
+  }
+  const size_t kb = ((size_t)n * 2 + 255) / 256 * 256, rb = ((size_t)n * 4 + 255) / 256 * 256;
+  hipError_t e = hipMallocAsync(ws, 2 * kb + 2 * rb + cub_bytes, stream);
+  if (e != hipSuccess) {
+    hip_fail(e, "dir_order workspace");
+    *ws = nullptr;
+    return nullptr;
+  }
+  uint16_t* k_in = (uint16_t*)*ws;
+  uint16_t* k_out = (uint16_t*)((char*)*ws + kb);
+  int32_t* r_in = (int32_t*)((char*)*ws + 2 * kb);
+  int32_t* r_out = (int32_t*)((char*)*ws + 2 * kb + rb);
+  void* tmp = (char*)*ws + 2 * kb + 2 * rb;
+  hipLaunchKernelGGL(k_dir_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, ray_offset, n, k_in, r_in);
+  e = hipcub::DeviceRadixSort::SortPairs(tmp, cub_bytes, k_in, k_out, r_in, r_out, (int)n, 0, 16, stream);
+  if (e != hipSuccess) {
+    hip_fail(e, "dir_order sort");
+    return nullptr;
+  }
+  return r_out;
+}
+
 int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B, int64_t ray_offset, int64_t n,
                  float* traced, float* received, uint32_t* mask, int32_t* hit_kind, int32_t* hit_face,
                  hipStream_t stream) {
@@ -324,19 +353,8 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
   // brute-force meshes gain nothing from it (every face is tested anyway) and keep row order.
   void* sort_ws = nullptr;
   if (bvh && n >= kSortMinRays && n <= INT32_MAX) {
-    size_t cub_bytes = 0;
-    RT_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (uint16_t*)nullptr, (uint16_t*)nullptr,
-                                              (int32_t*)nullptr, (int32_t*)nullptr, (int)n, 0, 16, stream));
-    const size_t kb = ((size_t)n * 2 + 255) / 256 * 256, rb = (size_t)n * 4;
-    RT_HIP(hipMallocAsync(&sort_ws, 2 * kb + 2 * rb + cub_bytes, stream));
-    uint16_t* k_in = (uint16_t*)sort_ws;
-    uint16_t* k_out = (uint16_t*)((char*)sort_ws + kb);
-    int32_t* r_in = (int32_t*)((char*)sort_ws + 2 * kb);
-    int32_t* r_out = (int32_t*)((char*)sort_ws + 2 * kb + rb);
-    void* tmp = (char*)sort_ws + 2 * kb + 2 * rb;
-    hipLaunchKernelGGL(k_dir_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, ray_offset, n, k_in, r_in);
-    RT_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, cub_bytes, k_in, k_out, r_in, r_out, (int)n, 0, 16, stream));
-    a.order = r_out;
+    a.order = dir_order(ray_offset, n, stream, &sort_ws);
+    if (!a.order) return -1;
   }
   switch (B) {
 #define RT_CASE(BB)                                                                     \

@@ -4,8 +4,10 @@ Two decompositions:
 * rays  -- rank r traces global ray ids [r*n, (r+1)*n) (Warp tid = global id, kernel.py:48-51, so
   every ray's path is independent of the shard); the impulse response is the sum over shards,
   amplitude tx_power / (n * world) per ray (tracer.py:103): ``reduce_sum``.
-* cells -- coverage cells with index % world == rank belong to rank; every other rank leaves 0 in
-  its power map and the maps are sum-reduced: ``reduce_sum`` again (NaN of an owner survives).
+* cells -- coverage cells whose x column ix = cell % nx satisfies ix % world == rank belong to
+  rank (x-column cyclic: a strip of constant ix is wholly one rank's, so the candidate passes
+  shrink with the rank count); every other rank leaves 0 in its power map and the maps are
+  sum-reduced: ``reduce_sum`` again (NaN of an owner survives).
 """
 from __future__ import annotations
 
@@ -22,9 +24,9 @@ def ray_shard(rank: int, world: int, rays_per_rank: int):
     return rank * rays_per_rank, rays_per_rank
 
 
-def owns_cell(cell: int, rank: int, world: int) -> bool:
-    """Cyclic cell ownership used by rt_coverage_run (csrc/coverage.hip: cell % nshard == shard)."""
-    return cell % world == rank
+def owns_cell(cell: int, rank: int, world: int, nx: int) -> bool:
+    """Cell ownership used by rt_coverage_run (csrc/coverage.hip: ix % nshard == shard, ix = cell % nx)."""
+    return (cell % nx) % world == rank
 
 
 def reduce_sum(t, group=None):

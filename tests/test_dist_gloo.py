@@ -68,7 +68,7 @@ def _cell_worker(rank, world, port, out):
     E = orc.Mesh(env.vertices, env.faces)
     centers = np.array([[x, y, 5.0] for x in (6.0, 8.0, 9.5) for y in (-1.0, 0.5, 2.0)])
     pm = np.zeros(len(centers))
-    mine = [c for c in range(len(centers)) if rdist.owns_cell(c, rank, world)]
+    mine = [c for c in range(len(centers)) if rdist.owns_cell(c, rank, world, 3)]
     p, _ = orc.coverage_loop(E, TX, centers[mine], B, 20_000, nthreads=2)
     pm[mine] = p
     t = torch.from_numpy(pm)
@@ -95,5 +95,7 @@ def test_cell_shards_sum_to_single_process():
 
 def test_shard_helpers():
     assert rdist.ray_shard(3, 8, 1000) == (3000, 1000)
-    owners = [sum(rdist.owns_cell(c, r, 8) for r in range(8)) for c in range(100)]
+    owners = [sum(rdist.owns_cell(c, r, 8, 10) for r in range(8)) for c in range(100)]
     assert owners == [1] * 100
+    # a whole x column belongs to one rank
+    assert all(rdist.owns_cell(c, (c % 10) % 8, 8, 10) for c in range(100))

@@ -68,6 +68,22 @@ def test_coverage_matches_per_cell_loop(room, grid, tx, B, N):
     cov.close()
 
 
+def test_coverage_sharded_ownership(room):
+    """Each rank fills exactly the cells of its x columns (dist.owns_cell); the rest stay 0."""
+    from rf_ray_tracing_warp_amd.dist import owns_cell
+    grid, tx, B, N = CoverageGrid(-7.0, -6.0, 2.0, 1.3, 1.1, 2.5, 11, 7, 2), (10, 0, 5), 3, 20_000
+    whole = Coverage(room, 2.998e8, 100e9, 100e-9, B, N, grid).run_device(tx).cpu().numpy()
+    for S in (2, 4, 8, 13):
+        for r in range(S):
+            part = Coverage(room, 2.998e8, 100e9, 100e-9, B, N, grid, shard_index=r, shard_count=S).run_device(tx)
+            part = part.cpu().numpy()
+            mine = np.array([owns_cell(c, r, S, grid.nx) for c in range(grid.num_cells)])
+            assert (part[~mine] == 0).all()
+            np.testing.assert_array_equal(np.isnan(part[mine]), np.isnan(whole[mine]))
+            ok = mine & ~np.isnan(whole)
+            np.testing.assert_array_equal(part[ok], whole[ok])
+
+
 def test_coverage_sharded_sum_equals_whole(room):
     grid, tx, B, N = CoverageGrid.square(16, 15, 5), (10, 0, 5), 3, 20_000
     whole = Coverage(room, 2.998e8, 100e9, 100e-9, B, N, grid).run(tx)
