@@ -567,10 +567,19 @@ __global__ __launch_bounds__(256) void k_replay(CovParams p, const uint64_t* key
 }
 
 // ------------------------------------------------------------------ 5. closed-form signal power
+// sin and cos of 2*pi*turns, reduced in turns (|2*pi*frac| <= pi keeps ocml on its short path;
+// the arguments here reach thousands of radians, where the general reduction is slow)
+__device__ __forceinline__ void sincos_turns(double turns, double& s, double& c) {
+  const double f = turns - rint(turns);
+  sincos(6.283185307179586 * f, &s, &c);
+}
+
 struct PowerParams {
   int64_t n_bins;
   int64_t half;   // (n-1)//2 : np.convolve 'same' offset
   double alpha;   // phase per sample: (2*pi*2.4e9) * (window/(n-1))
+  double turns;   // alpha / (2*pi)
+  double sin_a, cos_a;
 };
 
 __device__ __forceinline__ void two_sum(double& s, double& c, double x) {  // Neumaier running sum
@@ -579,100 +588,343 @@ __device__ __forceinline__ void two_sum(double& s, double& c, double x) {  // Ne
   s = t;
 }
 
-// mean square of the nonzero samples of y = ir (*) sin, for a sparse ir with ascending bins m[k]
-// term(k, c, s): a_k cos(alpha (half - m_k)), a_k sin(alpha (half - m_k)) of sparse entry k
-template <typename Term>
-__device__ double power_sparse(const uint64_t* keys, int64_t lo, int64_t hi, const PowerParams& P, Term term_cs) {
-  if (hi <= lo) return __builtin_nan("");
+// Terms accessor T of a sparse impulse response with ascending bins m_k:
+//   T.m(k)            m_k
+//   T.cs(k, c, s)     a_k cos(alpha (half - m_k)), a_k sin(alpha (half - m_k))
+//   T.start(k, s, c)  sin, cos of alpha * s_k      (s_k = first sample where term k is active)
+//   T.stop(k, s, c)   sin, cos of alpha * (e_k + 1) (e_k = last one)
+// Sweep of the sample range [xb, xe): the active terms at xb (those with s_k <= xb <= e_k, a
+// contiguous run [ie, is) because s_k and e_k both ascend with k) are summed directly, then each
+// interval of constant active set is closed in form, clipped at xe.  Every interval boundary is
+// xb, xe or some s_k / e_k + 1, so the interval's sin(L alpha) and sin/cos((u+v) alpha) follow
+// from the boundaries' precomputed sines by angle addition (no per-interval sincos).
+// Adds sum(y^2) into (total, tc) and the number of nonzero samples into count.
+template <typename Terms>
+__device__ void power_range(int64_t lo, int64_t hi, const PowerParams& P, const Terms& T, int64_t xb, int64_t xe,
+                            double& total, double& tc, int64_t& count) {
   const int64_t n = P.n_bins, half = P.half;
-  const double al = P.alpha, sa = sin(al);
   double Ps = 0, Pc = 0, Qs = 0, Qc = 0;  // running sums of a_k cos(alpha c_k), a_k sin(alpha c_k)
-  double total = 0.0, tc = 0.0;
-  int64_t count = 0;
-  int64_t is = lo, ie = lo;  // active terms = [ie, is)
-  int64_t x = 0;
-  auto sk = [&](int64_t k) { const int64_t m = (int64_t)(keys[k] & 0xFFFFFFFFull); return m - half > 0 ? m - half : 0; };
-  auto ek = [&](int64_t k) { const int64_t m = (int64_t)(keys[k] & 0xFFFFFFFFull); const int64_t e = m + (n - 1 - half); return e < n - 1 ? e : n - 1; };
+  auto mk = [&](int64_t k) { return T.m(k); };
+  auto sk = [&](int64_t k) { const int64_t m = mk(k); return m - half > 0 ? m - half : 0; };
+  auto ek = [&](int64_t k) { const int64_t m = mk(k); const int64_t e = m + (n - 1 - half); return e < n - 1 ? e : n - 1; };
   auto term = [&](int64_t k, double sgn) {  // sgn = +-1: sgn*(a*c) == (sgn*a)*c bit for bit
-    double tc, ts;
-    term_cs(k, tc, ts);
-    two_sum(Ps, Pc, sgn * tc);
-    two_sum(Qs, Qc, sgn * ts);
+    double c, s;
+    T.cs(k, c, s);
+    two_sum(Ps, Pc, sgn * c);
+    two_sum(Qs, Qc, sgn * s);
   };
+  int64_t is = lo, ie = lo;  // active terms = [ie, is)
+  int64_t x = xb;
+  double sx, cx;  // sin, cos of alpha * x
+  sincos_turns(P.turns * (double)xb, sx, cx);
+  if (xb > 0) {  // first term starting after xb, first term ending at or after xb
+    int64_t a = lo, b = hi;
+    while (a < b) {
+      const int64_t m = (a + b) >> 1;
+      if (sk(m) <= xb) a = m + 1; else b = m;
+    }
+    is = a;
+    a = lo;
+    b = is;
+    while (a < b) {
+      const int64_t m = (a + b) >> 1;
+      if (ek(m) < xb) a = m + 1; else b = m;
+    }
+    ie = a;
+  }
+  const double sa = P.sin_a, ca = P.cos_a;
+  bool first = true;
   while (true) {
     bool started_alone = false;
     int64_t nstart = 0;
-    while (is < hi && sk(is) <= x) {
-      term(is, 1.0);
-      ++is;
-      ++nstart;
+    if (first && xb > 0) {
+      for (int64_t k = ie; k < is; ++k) {
+        term(k, 1.0);
+        nstart += sk(k) == x ? 1 : 0;
+      }
+    } else {
+      while (is < hi && sk(is) <= x) {
+        term(is, 1.0);
+        ++is;
+        ++nstart;
+      }
+      while (ie < is && ek(ie) < x) {
+        term(ie, -1.0);
+        ++ie;
+      }
     }
-    while (ie < is && ek(ie) < x) {
-      term(ie, -1.0);
-      ++ie;
+    first = false;
+    if (is - ie == 1 && nstart == 1) started_alone = (mk(is - 1) - half == x);  // sin(0) = 0 exactly
+    int64_t nx = xe;
+    double snx, cnx;
+    int src = 0;  // 0: xe, 1: start of term is, 2: end of term ie
+    if (is < hi && sk(is) < nx) {
+      nx = sk(is);
+      src = 1;
     }
-    if (is - ie == 1 && nstart == 1) {
-      const int64_t m = (int64_t)(keys[is - 1] & 0xFFFFFFFFull);
-      started_alone = (m - half == x);  // its sample index i + c_k = 0 -> sin(0) = 0 exactly
+    if (ie < is && ek(ie) + 1 < nx) {
+      nx = ek(ie) + 1;
+      src = 2;
     }
-    int64_t nx = n;
-    if (is < hi && sk(is) < nx) nx = sk(is);
-    if (ie < is && ek(ie) + 1 < nx) nx = ek(ie) + 1;
+    if (src == 1) T.start(is, snx, cnx);
+    else if (src == 2) T.stop(ie, snx, cnx);
+    else sincos_turns(P.turns * (double)nx, snx, cnx);
     if (ie < is) {
       const double Pv = Ps + Pc, Qv = Qs + Qc;
-      const int64_t u = x, v = nx - 1, L = v - u + 1;
-      const double sl = sin((double)L * al), su = (double)(u + v) * al;
-      const double D = sl * cos(su) / sa, E = sl * sin(su) / sa;
+      const int64_t L = nx - x;
+      // sin(L a) = sin(a nx - a x); (u + v) a = a x + a nx - a
+      const double sl = snx * cx - cnx * sx;
+      const double s2 = sx * cnx + cx * snx, c2 = cx * cnx - sx * snx;  // of a x + a nx
+      const double ssu = s2 * ca - c2 * sa, csu = c2 * ca + s2 * sa;
+      const double D = sl * csu / sa, E = sl * ssu / sa;
       const double sss = 0.5 * ((double)L - D), scc = 0.5 * ((double)L + D), ssc = 0.5 * E;
       two_sum(total, tc, Pv * Pv * sss + Qv * Qv * scc + 2.0 * Pv * Qv * ssc);
       count += L - (started_alone ? 1 : 0);
     }
-    if (nx >= n) break;
+    if (nx >= xe) break;
     x = nx;
+    sx = snx;
+    cx = cnx;
   }
+}
+
+// terms from precomputed arrays (k_terms), indexed like the unique keys
+struct TermArrays {
+  const uint64_t* keys;
+  const double *tcos, *tsin, *ev;  // ev: [sin s, cos s, sin e1, cos e1] per key
+  __device__ __forceinline__ int64_t m(int64_t k) const { return (int64_t)(keys[k] & 0xFFFFFFFFull); }
+  __device__ __forceinline__ void cs(int64_t k, double& c, double& s) const {
+    c = tcos[k];
+    s = tsin[k];
+  }
+  __device__ __forceinline__ void start(int64_t k, double& s, double& c) const {
+    s = ev[4 * k];
+    c = ev[4 * k + 1];
+  }
+  __device__ __forceinline__ void stop(int64_t k, double& s, double& c) const {
+    s = ev[4 * k + 2];
+    c = ev[4 * k + 3];
+  }
+};
+
+// mean square of the nonzero samples of y = ir (*) sin, for a sparse ir with ascending bins m[k]
+template <typename Terms>
+__device__ double power_sparse(int64_t lo, int64_t hi, const PowerParams& P, const Terms& T) {
+  if (hi <= lo) return __builtin_nan("");
+  double total = 0.0, tc = 0.0;
+  int64_t count = 0;
+  power_range(lo, hi, P, T, 0, P.n_bins, total, tc, count);
   return count > 0 ? (total + tc) / (double)count : __builtin_nan("");
 }
 
 // per unique (cell, bin): the phase terms of the sweep, computed once in parallel
 __global__ __launch_bounds__(256) void k_terms(const uint64_t* ukeys, const double* uamps, const int64_t* nuniq,
-                                               PowerParams P, double* tcos, double* tsin) {
+                                               PowerParams P, double* tcos, double* tsin, double* ev) {
   const int64_t nu = *nuniq;
   for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < nu; u += (int64_t)gridDim.x * blockDim.x) {
     const int64_t m = (int64_t)(ukeys[u] & 0xFFFFFFFFull);
-    const double ph = P.alpha * (double)(P.half - m);
-    tcos[u] = uamps[u] * cos(ph);
-    tsin[u] = uamps[u] * sin(ph);
+    double sp, cp;
+    sincos_turns(P.turns * (double)(P.half - m), sp, cp);
+    tcos[u] = uamps[u] * cp;
+    tsin[u] = uamps[u] * sp;
+    const int64_t st = m - P.half > 0 ? m - P.half : 0;
+    const int64_t e = m + (P.n_bins - 1 - P.half), e1 = (e < P.n_bins - 1 ? e : P.n_bins - 1) + 1;
+    sincos_turns(P.turns * (double)st, ev[4 * u], ev[4 * u + 1]);
+    sincos_turns(P.turns * (double)e1, ev[4 * u + 2], ev[4 * u + 3]);
   }
 }
 
 // one thread per cell of ours (x columns ix % nshard == shard); other cells are left to the
 // caller's zero fill, the power map being sum-reduced across ranks
-__global__ __launch_bounds__(256) void k_power(const uint64_t* ukeys, const double* tcos, const double* tsin,
-                                               const int64_t* nuniq, rt_grid g, int shard, int nshard, PowerParams P,
-                                               double* power) {
+// [start, end) of every cell's run in the sorted unique keys (cells without keys keep 0, 0)
+__global__ __launch_bounds__(256) void k_cell_ranges(const uint64_t* ukeys, const int64_t* nuniq, int64_t ncell,
+                                                     int32_t* cstart, int32_t* cend) {
+  const int64_t nu = *nuniq;
+  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < nu; u += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t c = ukeys[u] >> 32;
+    if (c >= (uint64_t)ncell) continue;  // dropped records (~0) sort last
+    if (u == 0 || (ukeys[u - 1] >> 32) != c) cstart[c] = (int32_t)u;
+    if (u == nu - 1 || (ukeys[u + 1] >> 32) != c) cend[c] = (int32_t)(u + 1);
+  }
+}
+
+constexpr int kPowLds = 192;  // terms per wave staged in LDS (3 per lane); larger cells read global memory
+constexpr int kPowSmall = 16;  // cells with at most this many terms: one thread each (k_power_small)
+
+// cells of ours with 0..kPowSmall terms: one thread per cell, serial sweep (most cells of a large
+// map receive a handful of bins; a wave per such cell costs more than its whole sweep)
+__global__ __launch_bounds__(256) void k_power_small(TermArrays G, const int32_t* cstart, const int32_t* cend, rt_grid g,
+                                                     int shard, int nshard, PowerParams P, double* power) {
   const int64_t nxo = g.nx > shard ? (g.nx - shard + nshard - 1) / nshard : 0;
   const int64_t nown = nxo * g.ny * g.nz;
-  const int64_t nu = *nuniq;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nown; t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t jx = t % nxo, rest = t / nxo;
+    const int64_t c = rest * g.nx + shard + jx * nshard;
+    const int64_t lo = cstart[c], hi = cend[c];
+    if (hi - lo <= kPowSmall) power[c] = power_sparse(lo, hi, P, G);  // NaN when empty
+  }
+}
+
+// double-double helpers for the compensated prefix sums
+__device__ __forceinline__ void dd_add(double& h, double& l, double bh, double bl) {
+  const double s = h + bh, bb = s - h, e = (h - (s - bb)) + (bh - bb);
+  const double t = l + bl + e;
+  h = s + t;
+  l = t - (h - s);
+}
+
+// sum(y^2) over one interval [x, nx) with active sums P, Q, given sin/cos at x and nx
+__device__ __forceinline__ double interval_sq(double Pv, double Qv, int64_t L, double sx, double cx, double snx,
+                                              double cnx, const PowerParams& P) {
+  const double sa = P.sin_a, ca = P.cos_a;
+  const double sl = snx * cx - cnx * sx;                            // sin(L a)
+  const double s2 = sx * cnx + cx * snx, c2 = cx * cnx - sx * snx;  // of a x + a nx
+  const double ssu = s2 * ca - c2 * sa, csu = c2 * ca + s2 * sa;    // of a (x + nx - 1)
+  const double D = sl * csu / sa, E = sl * ssu / sa;
+  return Pv * Pv * (0.5 * ((double)L - D)) + Qv * Qv * (0.5 * ((double)L + D)) + 2.0 * Pv * Qv * (0.5 * E);
+}
+
+// One wave per cell of ours (x columns ix % nshard == shard; the caller zero-fills the rest, the
+// map being sum-reduced across ranks).  Up to kPowLds terms: the terms are staged in LDS with
+// compensated (double-double) prefix sums of a cos / a sin, and every lane closes the intervals
+// that start at its events (a term's first sample, or the sample after its last): the active
+// run [ie, is) comes from two binary searches and P, Q from prefix differences, so no lane
+// walks the active set.  Larger cells: the sample axis is split into 64 ranges swept by
+// power_range.  Either way equal to the serial sweep up to the order of summation.  (One
+// thread per cell was a chain of dependent global loads per interval: the kernel lasted as long
+// as its slowest cell whatever the cell count.)
+__global__ __launch_bounds__(256) void k_power(TermArrays G, const int32_t* cstart, const int32_t* cend, rt_grid g,
+                                               int shard, int nshard, PowerParams P, double* power) {
+  __shared__ int32_t s_st[4][kPowLds], s_e1[4][kPowLds], s_m[4][kPowLds];
+  __shared__ double s_pch[4][kPowLds + 1], s_pcl[4][kPowLds + 1], s_psh[4][kPowLds + 1], s_psl[4][kPowLds + 1];
+  __shared__ double s_ev[4][4 * kPowLds];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t n = P.n_bins, half = P.half;
+  const int64_t nxo = g.nx > shard ? (g.nx - shard + nshard - 1) / nshard : 0;
+  const int64_t nown = nxo * g.ny * g.nz;
+  double sn, cn;  // sin/cos at the sweep end
+  sincos_turns(P.turns * (double)n, sn, cn);
+  for (int64_t t = (int64_t)blockIdx.x * 4 + w; t < nown; t += (int64_t)gridDim.x * 4) {
+    const int64_t jx = t % nxo, rest = t / nxo;
     const int64_t c = rest * g.nx + shard + jx * nshard;  // rest = iz*ny + iy
-    // [lo, hi) = unique (cell, bin) keys of this cell
-    const uint64_t k0 = (uint64_t)c << 32, k1 = (uint64_t)(c + 1) << 32;
-    int64_t a = 0, b = nu;
-    while (a < b) {
-      const int64_t m = (a + b) >> 1;
-      if (ukeys[m] < k0) a = m + 1; else b = m;
+    const int64_t lo = cstart[c], hi = cend[c], K = hi - lo;
+    if (K <= kPowSmall) continue;  // k_power_small's (wave-uniform branch)
+    double total = 0.0, tcomp = 0.0;
+    int64_t count = 0;
+    if (K <= kPowLds) {
+      const int K32 = (int)K;
+      // stage: 3 consecutive terms per lane, local compensated sums, then a wave scan
+      double lch = 0, lcl = 0, lsh = 0, lsl = 0;
+      for (int q = 0; q < 3; ++q) {
+        const int k = lane * 3 + q;
+        if (k < K32) {
+          const int64_t m = G.m(lo + k);
+          s_m[w][k] = (int32_t)m;
+          s_st[w][k] = (int32_t)(m - half > 0 ? m - half : 0);
+          const int64_t e = m + (n - 1 - half);
+          s_e1[w][k] = (int32_t)((e < n - 1 ? e : n - 1) + 1);
+          for (int r = 0; r < 4; ++r) s_ev[w][4 * k + r] = G.ev[4 * (lo + k) + r];
+          dd_add(lch, lcl, G.tcos[lo + k], 0.0);
+          dd_add(lsh, lsl, G.tsin[lo + k], 0.0);
+        }
+      }
+      // exclusive scan of the lanes' (double-double) sums
+      double ech = lch, ecl = lcl, esh = lsh, esl = lsl;  // inclusive first
+      for (int o = 1; o < 64; o <<= 1) {
+        const double a = __shfl_up(ech, o, 64), b = __shfl_up(ecl, o, 64);
+        const double a2 = __shfl_up(esh, o, 64), b2 = __shfl_up(esl, o, 64);
+        if (lane >= o) {
+          dd_add(ech, ecl, a, b);
+          dd_add(esh, esl, a2, b2);
+        }
+      }
+      // to exclusive: subtract own sum
+      dd_add(ech, ecl, -lch, -lcl);
+      dd_add(esh, esl, -lsh, -lsl);
+      for (int q = 0; q < 3; ++q) {
+        const int k = lane * 3 + q;
+        if (k < K32) {
+          s_pch[w][k] = ech;
+          s_pcl[w][k] = ecl;
+          s_psh[w][k] = esh;
+          s_psl[w][k] = esl;
+          dd_add(ech, ecl, G.tcos[lo + k], 0.0);
+          dd_add(esh, esl, G.tsin[lo + k], 0.0);
+          if (k == K32 - 1) {
+            s_pch[w][K32] = ech;
+            s_pcl[w][K32] = ecl;
+            s_psh[w][K32] = esh;
+            s_psl[w][K32] = esl;
+          }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const int32_t* st = s_st[w];
+      const int32_t* e1 = s_e1[w];
+      auto upper = [&](const int32_t* a, int32_t x) {  // first index with a[i] > x
+        int l = 0, r = K32;
+        while (l < r) {
+          const int mm = (l + r) >> 1;
+          if (a[mm] <= x) l = mm + 1; else r = mm;
+        }
+        return l;
+      };
+      auto lower = [&](const int32_t* a, int32_t x) {  // first index with a[i] >= x
+        int l = 0, r = K32;
+        while (l < r) {
+          const int mm = (l + r) >> 1;
+          if (a[mm] < x) l = mm + 1; else r = mm;
+        }
+        return l;
+      };
+      for (int ev = lane; ev < 2 * K32; ev += 64) {
+        const bool is_start = ev < K32;
+        const int k = is_start ? ev : ev - K32;
+        const int32_t x = is_start ? st[k] : e1[k];
+        if (x >= n) continue;  // the sweep ends at n
+        // one lane per distinct event position: starts first, an end only where no start is
+        if (k > 0 && (is_start ? st[k - 1] : e1[k - 1]) == x) continue;
+        if (!is_start && upper(st, x) != lower(st, x)) continue;
+        const int is = upper(st, x), ie = upper(e1, x);
+        if (ie >= is) continue;  // nothing active
+        const int nstart = is - lower(st, x);
+        const bool alone = (is - ie == 1) && nstart == 1 && ((int64_t)s_m[w][is - 1] - half == (int64_t)x);
+        int64_t nx = n;
+        double snx = sn, cnx = cn;
+        if (is < K32 && st[is] < nx) {
+          nx = st[is];
+          snx = s_ev[w][4 * is];
+          cnx = s_ev[w][4 * is + 1];
+        }
+        if (e1[ie] < nx) {
+          nx = e1[ie];
+          snx = s_ev[w][4 * ie + 2];
+          cnx = s_ev[w][4 * ie + 3];
+        }
+        const double sx = is_start ? s_ev[w][4 * k] : s_ev[w][4 * k + 2];
+        const double cx = is_start ? s_ev[w][4 * k + 1] : s_ev[w][4 * k + 3];
+        double Ph = s_pch[w][is], Pl = s_pcl[w][is], Qh = s_psh[w][is], Ql = s_psl[w][is];
+        dd_add(Ph, Pl, -s_pch[w][ie], -s_pcl[w][ie]);
+        dd_add(Qh, Ql, -s_psh[w][ie], -s_psl[w][ie]);
+        two_sum(total, tcomp, interval_sq(Ph + Pl, Qh + Ql, nx - x, sx, cx, snx, cnx, P));
+        count += nx - x - (alone ? 1 : 0);
+      }
+    } else if (K > kPowLds) {
+      const int64_t xb = n * lane / 64, xe = n * (lane + 1) / 64;
+      if (xe > xb) power_range(lo, hi, P, G, xb, xe, total, tcomp, count);
     }
-    int64_t lo = a;
-    b = nu;
-    while (a < b) {
-      const int64_t m = (a + b) >> 1;
-      if (ukeys[m] < k1) a = m + 1; else b = m;
+    for (int o = 32; o >= 1; o >>= 1) {
+      const double t2 = __shfl_down(total, o, 64), c2 = __shfl_down(tcomp, o, 64);
+      const int64_t n2 = __shfl_down(count, o, 64);
+      if (lane < o) {
+        two_sum(total, tcomp, t2);
+        tcomp += c2;
+        count += n2;
+      }
     }
-    power[c] = power_sparse(ukeys, lo, a, P, [&](int64_t k, double& tc, double& ts) {
-      tc = tcos[k];
-      ts = tsin[k];
-    });
+    if (lane == 0) power[c] = count > 0 ? (total + tcomp) / (double)count : __builtin_nan("");
+    __builtin_amdgcn_wave_barrier();  // LDS slots are reused by the wave's next cell
   }
 }
 
@@ -691,11 +943,27 @@ __global__ __launch_bounds__(64) void k_power_dense(const double* ir, int64_t ro
       aa[K] = x[m];
       ++K;
     }
-  power[row] = power_sparse(kk, 0, K, P, [&](int64_t k, double& tc, double& ts) {
-    const double ph = P.alpha * (double)(P.half - (int64_t)kk[k]);
-    tc = aa[k] * cos(ph);
-    ts = aa[k] * sin(ph);
-  });
+  struct {
+    const uint64_t* kk;
+    const double* aa;
+    PowerParams P;
+    __device__ int64_t m(int64_t k) const { return (int64_t)kk[k]; }
+    __device__ void cs(int64_t k, double& c, double& s) const {
+      double sp, cp;
+      sincos_turns(P.turns * (double)(P.half - (int64_t)kk[k]), sp, cp);
+      c = aa[k] * cp;
+      s = aa[k] * sp;
+    }
+    __device__ void start(int64_t k, double& s, double& c) const {
+      const int64_t m = (int64_t)kk[k], st = m - P.half > 0 ? m - P.half : 0;
+      sincos_turns(P.turns * (double)st, s, c);
+    }
+    __device__ void stop(int64_t k, double& s, double& c) const {
+      const int64_t m = (int64_t)kk[k], e = m + (P.n_bins - 1 - P.half);
+      sincos_turns(P.turns * (double)((e < P.n_bins - 1 ? e : P.n_bins - 1) + 1), s, c);
+    }
+  } T{kk, aa, P};
+  power[row] = power_sparse(0, K, P, T);
 }
 
 }  // namespace
@@ -715,6 +983,8 @@ struct rt_coverage {
   uint64_t *keys = nullptr, *keys_sorted = nullptr, *okeys = nullptr, *okeys_sorted = nullptr, *ukeys = nullptr;
   double *oamps = nullptr, *oamps_sorted = nullptr, *uamps = nullptr;
   double *tcos = nullptr, *tsin = nullptr;  // per unique (cell, bin): phase terms of the power sweep
+  double* ev = nullptr;                      // per unique (cell, bin): sin/cos at its start and end sample
+  int32_t *cstart = nullptr, *cend = nullptr;  // per cell: its run in the unique keys
   uint8_t* win = nullptr;
   uint8_t* first_flag = nullptr;
   float* trx = nullptr;
@@ -734,12 +1004,12 @@ namespace {
 
 void free_cands(rt_coverage* c) {
   for (void* q : {(void*)c->keys, (void*)c->keys_sorted, (void*)c->okeys, (void*)c->okeys_sorted, (void*)c->ukeys,
-                  (void*)c->oamps, (void*)c->oamps_sorted, (void*)c->uamps, (void*)c->tcos, (void*)c->tsin,
+                  (void*)c->oamps, (void*)c->oamps_sorted, (void*)c->uamps, (void*)c->tcos, (void*)c->tsin, (void*)c->ev,
                   (void*)c->win, (void*)c->trx,
                   (void*)c->list, (void*)c->first_flag, c->tmp})
     if (q) (void)hipFree(q);
   c->keys = c->keys_sorted = c->okeys = c->okeys_sorted = c->ukeys = nullptr;
-  c->oamps = c->oamps_sorted = c->uamps = c->tcos = c->tsin = nullptr;
+  c->oamps = c->oamps_sorted = c->uamps = c->tcos = c->tsin = c->ev = nullptr;
   c->win = nullptr;
   c->first_flag = nullptr;
   c->trx = nullptr;
@@ -761,6 +1031,7 @@ int alloc_cands(rt_coverage* c, int64_t cap) {
   RT_HIP(hipMalloc(&c->uamps, cap * 8));
   RT_HIP(hipMalloc(&c->tcos, cap * 8));
   RT_HIP(hipMalloc(&c->tsin, cap * 8));
+  RT_HIP(hipMalloc(&c->ev, cap * 32));
   RT_HIP(hipMalloc(&c->win, cap));
   RT_HIP(hipMalloc(&c->first_flag, cap));
   RT_HIP(hipMalloc(&c->trx, cap * 4));
@@ -825,6 +1096,8 @@ int rt_coverage_create(int device, const rt_mesh* env, int max_bounces, int64_t 
   if (e == hipSuccess) e = hipMalloc(&c->nseg, n_rays);
   if (e == hipSuccess) e = hipMalloc(&c->counters, 32);
   if (e == hipSuccess) e = hipMalloc(&c->nuniq, 8);
+  if (e == hipSuccess) e = hipMalloc(&c->cstart, sizeof(int32_t) * nc);
+  if (e == hipSuccess) e = hipMalloc(&c->cend, sizeof(int32_t) * nc);
   if (e != hipSuccess) {
     rt_coverage_destroy(c);
     return rt::hip_fail(e, "rt_coverage_create");
@@ -847,6 +1120,8 @@ int rt_coverage_destroy(rt_coverage* c) {
   if (c->nseg) (void)hipFree(c->nseg);
   if (c->counters) (void)hipFree(c->counters);
   if (c->nuniq) (void)hipFree(c->nuniq);
+  if (c->cstart) (void)hipFree(c->cstart);
+  if (c->cend) (void)hipFree(c->cend);
   if (c->items) (void)hipFree(c->items);
   delete c;
   return RT_OK;
@@ -953,12 +1228,20 @@ int rt_coverage_run(rt_coverage* c, const float* tx_pos, double tx_power, double
   P.n_bins = n_bins;
   P.half = (n_bins - 1) / 2;
   P.alpha = alpha;
-  const unsigned grid_cells = (unsigned)std::min<int64_t>((ncell / c->nshard + 256) / 256, 8192);
+  P.turns = alpha / 6.283185307179586;
+  P.sin_a = sin(alpha);
+  P.cos_a = cos(alpha);
+  // one wave per owned cell, 4 per block
+  const unsigned grid_cells = (unsigned)std::min<int64_t>((ncell / c->nshard + 4) / 4, 4096);
+  const unsigned grid_small = (unsigned)std::min<int64_t>((ncell / c->nshard + 256) / 256, 8192);
+  const TermArrays terms{c->ukeys, c->tcos, c->tsin, c->ev};
   if (c->nshard > 1) RT_HIP(hipMemsetAsync(power, 0, ncell * sizeof(double), s));  // cells of other ranks
+  RT_HIP(hipMemsetAsync(c->cstart, 0, ncell * sizeof(int32_t), s));
+  RT_HIP(hipMemsetAsync(c->cend, 0, ncell * sizeof(int32_t), s));
   if (ncand == 0) {
     RT_HIP(hipMemsetAsync(c->nuniq, 0, 8, s));
-    hipLaunchKernelGGL(k_power, dim3(grid_cells), dim3(256), 0, s, c->ukeys, c->tcos, c->tsin, c->nuniq,
-                       c->grid, c->shard, c->nshard, P, power);
+    hipLaunchKernelGGL(k_power_small, dim3(grid_small), dim3(256), 0, s, terms, c->cstart, c->cend, c->grid, c->shard,
+                       c->nshard, P, power);
     RT_HIP(hipGetLastError());
     if (stats) stats[0] = stats[1] = 0;
     return RT_OK;
@@ -994,12 +1277,16 @@ int rt_coverage_run(rt_coverage* c, const float* tx_pos, double tx_power, double
     RT_HIP(hipcub::DeviceReduce::ReduceByKey(c->tmp, tb, c->okeys_sorted, c->ukeys, c->oamps_sorted, c->uamps,
                                              c->nuniq, hipcub::Sum(), (int)nlist, s));
     const unsigned grid_u = (unsigned)std::min<int64_t>((nlist + 255) / 256, 8192);
-    hipLaunchKernelGGL(k_terms, dim3(grid_u), dim3(256), 0, s, c->ukeys, c->uamps, c->nuniq, P, c->tcos, c->tsin);
+    hipLaunchKernelGGL(k_terms, dim3(grid_u), dim3(256), 0, s, c->ukeys, c->uamps, c->nuniq, P, c->tcos, c->tsin, c->ev);
   } else {
     RT_HIP(hipMemsetAsync(c->nuniq, 0, 8, s));
   }
-  hipLaunchKernelGGL(k_power, dim3(grid_cells), dim3(256), 0, s, c->ukeys, c->tcos, c->tsin, c->nuniq,
-                     c->grid, c->shard, c->nshard, P, power);
+  hipLaunchKernelGGL(k_cell_ranges, dim3((unsigned)std::min<int64_t>((nlist + 255) / 256 + 1, 8192)), dim3(256), 0, s,
+                     c->ukeys, c->nuniq, ncell, c->cstart, c->cend);
+  hipLaunchKernelGGL(k_power_small, dim3(grid_small), dim3(256), 0, s, terms, c->cstart, c->cend, c->grid, c->shard,
+                     c->nshard, P, power);
+  hipLaunchKernelGGL(k_power, dim3(grid_cells), dim3(256), 0, s, terms, c->cstart, c->cend, c->grid, c->shard,
+                     c->nshard, P, power);
   RT_HIP(hipGetLastError());
   c->last_received = nlist;
   if (stats) {
@@ -1039,6 +1326,9 @@ int rt_power_dense(const double* impulse_responses, int64_t rows, int64_t n_bins
   P.n_bins = n_bins;
   P.half = (n_bins - 1) / 2;
   P.alpha = alpha;
+  P.turns = alpha / 6.283185307179586;
+  P.sin_a = sin(alpha);
+  P.cos_a = cos(alpha);
   uint64_t* kk = (uint64_t*)scratch;
   double* aa = (double*)(kk + rows * n_bins);
   hipLaunchKernelGGL(k_power_dense, dim3((unsigned)rows), dim3(64), 0, (hipStream_t)stream, impulse_responses, rows, P,

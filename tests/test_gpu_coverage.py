@@ -68,6 +68,15 @@ def test_coverage_matches_per_cell_loop(room, grid, tx, B, N):
     cov.close()
 
 
+def test_coverage_cell_at_transmitter(room):
+    """The cell centred on the TX: every ray starts inside its receiver sphere (Q3: and leaves it
+    at t = radius), and its neighbours at 0.3 m receive dense direct bursts."""
+    grid = CoverageGrid(9.7, -0.3, 5.0, 0.3, 0.3, 1.0, 3, 3, 1)
+    cov = Coverage(room, 2.998e8, 100e9, 100e-9, 3, 20_000, grid)
+    power, ref = _compare(cov, grid, room, (10.0, 0.0, 5.0), 3, 20_000)
+    cov.close()
+
+
 def test_coverage_sharded_ownership(room):
     """Each rank fills exactly the cells of its x columns (dist.owns_cell); the rest stay 0."""
     from rf_ray_tracing_warp_amd.dist import owns_cell
