@@ -167,6 +167,38 @@ __device__ __forceinline__ rt::Hit rx_query(const rt_grid& g, int64_t cell, doub
   return h;
 }
 
+// rx_query with the vertices computed per face instead of held in registers: the same double
+// arithmetic (unit * r + centre, rounded once to float) on the same values, so every bit agrees
+// with rx_query; about twice its VALU but ~130 fewer VGPRs, for the latency-bound replay kernel
+// whose occupancy the 126 live vertex floats would otherwise set at one wave per SIMD.
+__device__ __forceinline__ double pickd(double x, double y, double z, int k) { return k == 0 ? x : (k == 1 ? y : z); }
+__device__ __forceinline__ rt::Hit rx_query_lean(const rt_grid& g, int64_t cell, double r, float3 o, float3 d) {
+  const rt::Shear s = rt::make_shear(o, d);
+  double c[3];
+  cell_center(g, cell, c);
+  const double cx = pickd(c[0], c[1], c[2], s.kx), cy = pickd(c[0], c[1], c[2], s.ky),
+               cz = pickd(c[0], c[1], c[2], s.kz);
+  rt::Hit h;
+  rt::hit_init(h);
+#pragma unroll 1
+  for (int f = 0; f < RT_ICO1_NF; ++f) {
+    float q[9];
+#pragma unroll
+    for (int v = 0; v < 3; ++v) {
+      const int vi = rt_ico1_f[f][v];
+      const double ux = rt_ico1_v[vi][0], uy = rt_ico1_v[vi][1], uz = rt_ico1_v[vi][2];
+      const double mx = pickd(ux, uy, uz, s.kx) * r, my = pickd(ux, uy, uz, s.ky) * r, mz = pickd(ux, uy, uz, s.kz) * r;
+      q[3 * v + 0] = (float)(mx + cx);
+      q[3 * v + 1] = (float)(my + cy);
+      q[3 * v + 2] = (float)(mz + cz);
+    }
+    float T, det;
+    if (rt::tri_test(s, make_float4(q[0], q[1], q[2], q[3]), make_float4(q[4], q[5], q[6], q[7]), q[8], T, det))
+      rt::hit_consider(h, T, det, f);
+  }
+  return h;
+}
+
 // ------------------------------------------------------------------ 1. environment trajectories
 template <bool USE_BVH>
 __global__ __launch_bounds__(256) void k_traj(CovParams p) {
@@ -353,8 +385,9 @@ __global__ __launch_bounds__(256) void k_cols(CovParams p) {
 }
 
 // pass B: one column item per lane -> candidate keys (cell, ray, k) for the cells of our shard
-template <bool WRITE>
-__device__ __forceinline__ unsigned column_cells(const CovParams& p, uint64_t item, uint64_t* dst) {
+// sink(j, key) receives the item's j-th candidate key
+template <typename Sink>
+__device__ __forceinline__ unsigned column_cells(const CovParams& p, uint64_t item, Sink sink) {
   const rt_grid& g = p.g;
   const double rp = p.r_pad, rp2 = rp * rp;
   const int64_t r = (int64_t)(item >> 40), ia = (int64_t)(item & 0xFFFFFF), kz = (int64_t)((item >> 24) & 0xFFF);
@@ -385,24 +418,39 @@ __device__ __forceinline__ unsigned column_cells(const CovParams& p, uint64_t it
     double cc[3];
     cell_center(g, cell, cc);
     if (seg_ball(s.o, s.d, s.tmax, cc, rp2)) {
-      if (WRITE) dst[c] = ((uint64_t)cell << 28) | ((uint64_t)r << 4) | (uint64_t)k;
+      sink(c, ((uint64_t)cell << 28) | ((uint64_t)r << 4) | (uint64_t)k);
       ++c;
     }
   }
   return c;
 }
 
+// One pass: an item's keys are kept in the thread's LDS slots while the block reserves its
+// output range; only items with more than kCellBuf candidates run the geometry a second time.
+constexpr int kCellBuf = 16;
+
 __global__ __launch_bounds__(256) void k_cells(CovParams p) {
+  __shared__ uint64_t sbuf[kCellBuf][256];
   const int64_t nitems = (int64_t)min(*p.item_count, (unsigned long long)p.item_cap);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int tid = threadIdx.x;
   for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < nitems; base += stride) {
-    const int64_t i = base + threadIdx.x;
+    const int64_t i = base + tid;
     const bool active = i < nitems;
     const uint64_t item = active ? p.items[i] : 0;
-    const unsigned c = active ? column_cells<false>(p, item, nullptr) : 0;
+    const unsigned c = active ? column_cells(p, item, [&](unsigned j, uint64_t key) {
+      if (j < kCellBuf) sbuf[j][tid] = key;
+    }) : 0;
     unsigned pre;
     const unsigned long long at = block_append(p.count, c, pre);
-    if (c && (int64_t)(at + pre + c) <= p.cap) column_cells<true>(p, item, p.keys + at + pre);
+    if (c && (int64_t)(at + pre + c) <= p.cap) {
+      uint64_t* dst = p.keys + at + pre;
+      if (c <= (unsigned)kCellBuf) {
+        for (unsigned j = 0; j < c; ++j) dst[j] = sbuf[j][tid];
+      } else {
+        column_cells(p, item, [&](unsigned j, uint64_t key) { dst[j] = key; });
+      }
+    }
   }
 }
 
@@ -526,7 +574,9 @@ __global__ __launch_bounds__(256) void k_replay(CovParams p, const uint64_t* key
       // culled at the receiver hit is equivalent, but its build gave run-to-run different
       // amplitudes on the terrain BVH on some boxes: DESIGN.md §6.)
       const rt::Hit he = env_query<USE_BVH>(p, lds_tab, s, pos, d);
-      const rt::Hit hr = rx_query(p.g, cell, p.r_rx, pos, d);
+      // BVH scenes: the replay waits on node fetches, so occupancy (lean receiver) pays; on the
+      // LDS brute-force path it is VALU-bound and the register-held receiver is faster
+      const rt::Hit hr = USE_BVH ? rx_query_lean(p.g, cell, p.r_rx, pos, d) : rx_query(p.g, cell, p.r_rx, pos, d);
       const bool env_hit = he.face >= 0, rx_hit = hr.face >= 0;
       if (rx_hit && (!env_hit || he.t > hr.t)) {
         pos.x = fmaf(d.x, hr.t, pos.x);
