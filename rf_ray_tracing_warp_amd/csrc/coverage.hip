@@ -465,7 +465,7 @@ __global__ __launch_bounds__(256) void k_win(CovParams p, const uint64_t* keys, 
     const float3 o = make_float3(p.px[o_], p.py[o_], p.pz[o_]);
     const float3 d = make_float3(p.dx[o_], p.dy[o_], p.dz[o_]);
     const float te = p.te[o_];
-    const rt::Hit hr = rx_query(p.g, cell, p.r_rx, o, d);
+    const rt::Hit hr = rx_query(p.g, cell, p.r_rx, o, d);  // (lean variant measured no faster here)
     // kernel.py:85 -- receiver wins if hit and (env missed or env strictly farther)
     win[i] = (hr.face >= 0 && (isinf(te) || te > hr.t)) ? 1 : 0;
     trx[i] = hr.t;
