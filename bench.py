@@ -84,7 +84,7 @@ def cpu_baseline(sample_rays, B, tx, rx, min_s=10.0, max_rays=400_000_000):
 
 def coverage_leg(args, env_m, env, local, rank, world, dist):
     """K3: coverage.py on room.stl, n x n cells at z = 5, tx (10,0,5), 1M rays per cell, 3 bounces.
-    Cells are sharded cyclically over the ranks; the power map is sum-reduced (RCCL)."""
+    Cells are sharded by x column (ix % world) over the ranks; the power map is sum-reduced (RCCL)."""
     import torch
     from rf_ray_tracing_warp_amd.coverage import Coverage, CoverageGrid
 
@@ -122,7 +122,7 @@ def coverage_leg(args, env_m, env, local, rank, world, dist):
     return {"metric": "coverage cells/sec", "value": grid.num_cells / dt, "unit": "cells/s", "ms_per_map": dt * 1e3,
             "workload": f"K3: room.stl, {grid.nx}x{grid.ny} receivers at z=5 (centres -15+(i+1/2)*30/{grid.nx}), "
                         f"tx (10,0,5), {args.coverage_rays} rays per cell, {args.bounces} bounces, 10000 bins, "
-                        f"signal power per cell; cells sharded cyclically x{world} + RCCL sum of the power map",
+                        f"signal power per cell; cells sharded by x column (ix % {world}) + RCCL sum of the power map",
             "scaling": "strong", "cells_receiving": int(np.isfinite(pm).sum()),
             "candidates": int(cand.item()), "algorithm": "exact shared-trajectory (csrc/coverage.hip)"}
 
@@ -204,7 +204,7 @@ def terrain_legs(args, local, rank, world, dist):
     pm = p.cpu().numpy()
     k5 = {"metric": "coverage cells/sec", "value": grid.num_cells / dt, "unit": "cells/s", "ms_per_map": dt * 1e3,
           "workload": f"K5 on the terrain stand-in: {grid.nx}x{grid.ny} receivers at z=2 over +-50 m, tx (10,0,4.5), "
-                      f"{args.k5_rays} rays per cell, 3 bounces, 20000 bins; cells sharded x{world} + RCCL sum",
+                      f"{args.k5_rays} rays per cell, 3 bounces, 20000 bins; cells sharded by x column (ix % {world}) + RCCL sum",
           "scaling": "strong", "cells_receiving": int(np.isfinite(pm).sum()), "candidates": int(cov.last_candidates)}
     cov.close()
     return k4, k5
