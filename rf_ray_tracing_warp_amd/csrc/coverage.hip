@@ -55,7 +55,9 @@ struct CovParams {
   int shard, nshard;  // cells in x columns ix % nshard == shard are ours
   const int32_t* order;  // k_traj row order (direction-sorted for BVH environments) or null
   // trajectory SoA [k][n]
-  float *px, *py, *pz, *dx, *dy, *dz, *te;
+  // trajectories, [ray][bounce] x 2 float4: (p.xyz, t_env), (d.xyz, 0) -- 32 B per ray-bounce,
+  // so a random (ray, bounce) read or a direction-sorted write touches one or two lines
+  float4* traj;
   uint8_t* nseg;
   // column items and candidates (wave-aggregated appends; counts on the device)
   uint64_t* items;
@@ -71,6 +73,8 @@ struct CovParams {
   int flags;
   int64_t n_bins;
 };
+__device__ __forceinline__ float4 traj_p(const CovParams& p, int64_t r, int k) { return p.traj[2 * (r * p.B + k)]; }
+__device__ __forceinline__ float4 traj_d(const CovParams& p, int64_t r, int k) { return p.traj[2 * (r * p.B + k) + 1]; }
 
 __device__ __forceinline__ int64_t ncells(const rt_grid& g) { return g.nx * g.ny * g.nz; }
 
@@ -213,19 +217,11 @@ __global__ __launch_bounds__(256) void k_traj(CovParams p) {
     for (int k = 0; k < p.B; ++k) {
       const rt::Shear s = rt::make_shear(pos, dir);
       const rt::Hit he = env_query<USE_BVH>(p, lds_tab, s, pos, dir);
-      const int64_t o = (int64_t)k * p.n + r;
-      p.px[o] = pos.x;
-      p.py[o] = pos.y;
-      p.pz[o] = pos.z;
-      p.dx[o] = dir.x;
-      p.dy[o] = dir.y;
-      p.dz[o] = dir.z;
+      float4* tp = p.traj + 2 * (r * p.B + k);
+      tp[0] = make_float4(pos.x, pos.y, pos.z, he.face < 0 ? INFINITY : he.t);
+      tp[1] = make_float4(dir.x, dir.y, dir.z, 0.0f);
       nseg = k + 1;
-      if (he.face < 0) {  // escapes: this segment is infinite, later iterations repeat the miss
-        p.te[o] = INFINITY;
-        break;
-      }
-      p.te[o] = he.t;
+      if (he.face < 0) break;  // escapes: this segment is infinite, later iterations repeat the miss
       pos.x = fmaf(dir.x, he.t, pos.x);
       pos.y = fmaf(dir.y, he.t, pos.y);
       pos.z = fmaf(dir.z, he.t, pos.z);
@@ -303,14 +299,14 @@ struct Seg {
 };
 __device__ __forceinline__ Seg load_seg(const CovParams& p, int64_t r, int k) {
   Seg s;
-  const int64_t o_ = (int64_t)k * p.n + r;
-  s.o[0] = p.px[o_];
-  s.o[1] = p.py[o_];
-  s.o[2] = p.pz[o_];
-  s.d[0] = p.dx[o_];
-  s.d[1] = p.dy[o_];
-  s.d[2] = p.dz[o_];
-  const double te = p.te[o_];
+  const float4 tp = traj_p(p, r, k), td = traj_d(p, r, k);
+  s.o[0] = tp.x;
+  s.o[1] = tp.y;
+  s.o[2] = tp.z;
+  s.d[0] = td.x;
+  s.d[1] = td.y;
+  s.d[2] = td.z;
+  const double te = tp.w;
   s.tmax = te < (double)RT_MAX_T ? te : (double)RT_MAX_T;
   s.A = fabs(s.d[0]) >= fabs(s.d[1]) ? 0 : 1;
   s.Bx = 1 - s.A;
@@ -461,10 +457,10 @@ __global__ __launch_bounds__(256) void k_win(CovParams p, const uint64_t* keys, 
     const uint64_t key = keys[i];
     const int64_t cell = (int64_t)(key >> 28), r = (int64_t)((key >> 4) & 0xFFFFFF);
     const int k = (int)(key & 15);
-    const int64_t o_ = (int64_t)k * p.n + r;
-    const float3 o = make_float3(p.px[o_], p.py[o_], p.pz[o_]);
-    const float3 d = make_float3(p.dx[o_], p.dy[o_], p.dz[o_]);
-    const float te = p.te[o_];
+    const float4 tp = traj_p(p, r, k), td = traj_d(p, r, k);
+    const float3 o = make_float3(tp.x, tp.y, tp.z);
+    const float3 d = make_float3(td.x, td.y, td.z);
+    const float te = tp.w;
     const rt::Hit hr = rx_query(p.g, cell, p.r_rx, o, d);  // (lean variant measured no faster here)
     // kernel.py:85 -- receiver wins if hit and (env missed or env strictly farther)
     win[i] = (hr.face >= 0 && (isinf(te) || te > hr.t)) ? 1 : 0;
@@ -552,14 +548,15 @@ __global__ __launch_bounds__(256) void k_replay(CovParams p, const uint64_t* key
     const int64_t cell = (int64_t)(key >> 28), r = (int64_t)((key >> 4) & 0xFFFFFF);
     const int k0 = (int)(key & 15);
     PathAcc acc;
-    acc.start(p.px[r], p.py[r], p.pz[r], p.amp0);  // p_0 = tx
+    const float4 t0 = traj_p(p, r, 0);
+    acc.start(t0.x, t0.y, t0.z, p.amp0);  // p_0 = tx
     for (int q = 1; q <= k0; ++q) {                 // environment prefix p_1 .. p_k0
-      const int64_t o_ = (int64_t)q * p.n + r;
-      acc.add(p.px[o_], p.py[o_], p.pz[o_]);
+      const float4 tq = traj_p(p, r, q);
+      acc.add(tq.x, tq.y, tq.z);
     }
-    const int64_t o0 = (int64_t)k0 * p.n + r;
-    float3 pos = make_float3(p.px[o0], p.py[o0], p.pz[o0]);
-    const float3 dir = make_float3(p.dx[o0], p.dy[o0], p.dz[o0]);
+    const float4 tk = traj_p(p, r, k0), tdk = traj_d(p, r, k0);
+    float3 pos = make_float3(tk.x, tk.y, tk.z);
+    const float3 dir = make_float3(tdk.x, tdk.y, tdk.z);
     // bounce k0: the receiver wins (k_win) at t = trx[i]
     pos.x = fmaf(dir.x, trx[i], pos.x);
     pos.y = fmaf(dir.y, trx[i], pos.y);
@@ -1028,7 +1025,7 @@ struct rt_coverage {
   double r_rx = 0.1;
   int shard = 0, nshard = 1;
   // buffers
-  float* traj = nullptr;  // 7 * B * n floats
+  float4* traj = nullptr;  // n * B * 2 float4
   uint8_t* nseg = nullptr;
   uint64_t *keys = nullptr, *keys_sorted = nullptr, *okeys = nullptr, *okeys_sorted = nullptr, *ukeys = nullptr;
   double *oamps = nullptr, *oamps_sorted = nullptr, *uamps = nullptr;
@@ -1142,7 +1139,7 @@ int rt_coverage_create(int device, const rt_mesh* env, int max_bounces, int64_t 
   c->r_rx = rx_radius;
   c->shard = shard_index;
   c->nshard = shard_count;
-  hipError_t e = hipMalloc(&c->traj, sizeof(float) * 7 * max_bounces * n_rays);
+  hipError_t e = hipMalloc(&c->traj, sizeof(float4) * 2 * max_bounces * n_rays);
   if (e == hipSuccess) e = hipMalloc(&c->nseg, n_rays);
   if (e == hipSuccess) e = hipMalloc(&c->counters, 32);
   if (e == hipSuccess) e = hipMalloc(&c->nuniq, 8);
@@ -1206,14 +1203,7 @@ int rt_coverage_run(rt_coverage* c, const float* tx_pos, double tx_power, double
   }
   p.shard = c->shard;
   p.nshard = c->nshard;
-  const int64_t BN = (int64_t)c->B * c->n;
-  p.px = c->traj;
-  p.py = p.px + BN;
-  p.pz = p.py + BN;
-  p.dx = p.pz + BN;
-  p.dy = p.dx + BN;
-  p.dz = p.dy + BN;
-  p.te = p.dz + BN;
+  p.traj = c->traj;
   p.nseg = c->nseg;
   p.count = c->counters;
   p.item_count = c->counters + 1;
