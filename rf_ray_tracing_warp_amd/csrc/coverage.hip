@@ -537,12 +537,43 @@ __global__ __launch_bounds__(256) void k_first(const uint64_t* keys, int64_t nke
   }
 }
 
+// BVH scenes: replay order key of list entry li -- the ray's direction at its first win (8x8
+// octahedral cell) over the cell's coarse position (32x32 Morton), so the lanes of a wave walk
+// nearby BVH paths.  Only the processing order changes: records are written at li.
+__global__ __launch_bounds__(256) void k_replay_keys(CovParams p, const uint64_t* keys, const int64_t* list, int64_t nl,
+                                                     uint16_t* okey, int32_t* oval) {
+  for (int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; li < nl; li += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t key = keys[list[li]];
+    const int64_t cell = (int64_t)(key >> 28), r = (int64_t)((key >> 4) & 0xFFFFFF);
+    const int k0 = (int)(key & 15);
+    const float4 d = traj_d(p, r, k0);
+    const float sabs = fabsf(d.x) + fabsf(d.y) + fabsf(d.z);
+    float x = d.x / sabs, y = d.y / sabs;
+    if (d.z < 0.0f) {
+      const float ox = x;
+      x = (1.0f - fabsf(y)) * (ox < 0.0f ? -1.0f : 1.0f);
+      y = (1.0f - fabsf(ox)) * (y < 0.0f ? -1.0f : 1.0f);
+    }
+    const uint32_t dx = (uint32_t)fminf(fmaxf((x + 1.0f) * 4.0f, 0.0f), 7.0f);
+    const uint32_t dy = (uint32_t)fminf(fmaxf((y + 1.0f) * 4.0f, 0.0f), 7.0f);
+    const int64_t ix = cell % p.g.nx, iy = (cell / p.g.nx) % p.g.ny;
+    const uint32_t cx = (uint32_t)(ix * 32 / p.g.nx), cy = (uint32_t)(iy * 32 / p.g.ny);
+    uint32_t mz = 0;
+#pragma unroll
+    for (int b = 0; b < 5; ++b) mz |= ((cx >> b) & 1u) << (2 * b) | ((cy >> b) & 1u) << (2 * b + 1);
+    okey[li] = (uint16_t)((dy * 8 + dx) << 10 | mz);
+    oval[li] = (int32_t)li;
+  }
+}
+
 template <bool USE_BVH>
 __global__ __launch_bounds__(256) void k_replay(CovParams p, const uint64_t* keys, const float* trx,
-                                                const int64_t* list, int64_t nl, uint64_t* out_key, double* out_amp) {
+                                                const int64_t* list, int64_t nl, const int32_t* order,
+                                                uint64_t* out_key, double* out_amp) {
   extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
   stage_env<USE_BVH>(p, lds_tab);
-  for (int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; li < nl; li += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t jl = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; jl < nl; jl += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t li = order ? (int64_t)order[jl] : jl;
     const int64_t i = list[li];
     const uint64_t key = keys[i];
     const int64_t cell = (int64_t)(key >> 28), r = (int64_t)((key >> 4) & 0xFFFFFF);
@@ -1300,12 +1331,28 @@ int rt_coverage_run(rt_coverage* c, const float* tx_pos, double tx_power, double
   RT_HIP(hipStreamSynchronize(s));
   if (nlist > 0) {
     const unsigned grid_l = (unsigned)std::min<int64_t>((nlist + 255) / 256, 8192);
-    if (bvh)
+    if (bvh) {
+      // coherent processing order (16-bit keys through hipCUB, workspace stream-ordered)
+      size_t cub_bytes = 0;
+      RT_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (uint16_t*)nullptr, (uint16_t*)nullptr,
+                                                (int32_t*)nullptr, (int32_t*)nullptr, (int)nlist, 0, 16, s));
+      const size_t kb = ((size_t)nlist * 2 + 255) / 256 * 256, rb = ((size_t)nlist * 4 + 255) / 256 * 256;
+      void* ws = nullptr;
+      RT_HIP(hipMallocAsync(&ws, 2 * kb + 2 * rb + cub_bytes, s));
+      uint16_t* k_in = (uint16_t*)ws;
+      uint16_t* k_out = (uint16_t*)((char*)ws + kb);
+      int32_t* v_in = (int32_t*)((char*)ws + 2 * kb);
+      int32_t* v_out = (int32_t*)((char*)ws + 2 * kb + rb);
+      hipLaunchKernelGGL(k_replay_keys, dim3(grid_l), dim3(256), 0, s, p, c->keys_sorted, c->list, nlist, k_in, v_in);
+      RT_HIP(hipcub::DeviceRadixSort::SortPairs((char*)ws + 2 * kb + 2 * rb, cub_bytes, k_in, k_out, v_in, v_out,
+                                                (int)nlist, 0, 16, s));
       hipLaunchKernelGGL(k_replay<true>, dim3(grid_l), dim3(256), lds, s, p, c->keys_sorted, c->trx, c->list, nlist,
-                         c->okeys, c->oamps);
-    else
+                         v_out, c->okeys, c->oamps);
+      RT_HIP(hipFreeAsync(ws, s));
+    } else {
       hipLaunchKernelGGL(k_replay<false>, dim3(grid_l), dim3(256), lds, s, p, c->keys_sorted, c->trx, c->list, nlist,
-                         c->okeys, c->oamps);
+                         (const int32_t*)nullptr, c->okeys, c->oamps);
+    }
     RT_HIP(hipGetLastError());
     // records are in (cell, ray, k) order; a stable sort on (cell, bin) keeps that order within a
     // bin, so every bin's amplitudes are summed in ray order.  Dropped records (~0) sort last.
