@@ -103,7 +103,7 @@ __device__ __forceinline__ void stage_env(const TraceArgs& a, float4* lds_tab) {
 }
 
 template <int B, bool USE_BVH>
-__global__ __launch_bounds__(256) void k_trace_bf(TraceArgs a) {
+__device__ __forceinline__ void trace_body(const TraceArgs& a) {
   constexpr int P = B + 1;
   extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
   stage_env<USE_BVH>(a, lds_tab);
@@ -181,6 +181,20 @@ __global__ __launch_bounds__(256) void k_trace_bf(TraceArgs a) {
     }
     if (a.mask) a.mask[row] = last_rx >= 0 ? 1u : 0u;
   }
+}
+
+template <int B, bool USE_BVH>
+__global__ __launch_bounds__(256) void k_trace_bf(TraceArgs a) {
+  trace_body<B, USE_BVH>(a);
+}
+// BVH meshes: traversal is latency-bound (dependent node fetches), so the kernel is built for
+// RT_BVH_WAVES waves per SIMD
+#ifndef RT_BVH_WAVES
+#define RT_BVH_WAVES 6
+#endif
+template <int B>
+__global__ __launch_bounds__(256, RT_BVH_WAVES) void k_trace_bvh(TraceArgs a) {
+  trace_body<B, true>(a);
 }
 
 // Generic fallback for B beyond the register-resident instantiations: the path lives in
@@ -360,7 +374,7 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
 #define RT_CASE(BB)                                                                     \
   case BB:                                                                              \
     if (bvh)                                                                            \
-      hipLaunchKernelGGL((k_trace_bf<BB, true>), dim3(grid), blk, lds, stream, a);      \
+      hipLaunchKernelGGL((k_trace_bvh<BB>), dim3(grid), blk, lds, stream, a);           \
     else                                                                                \
       hipLaunchKernelGGL((k_trace_bf<BB, false>), dim3(grid), blk, lds, stream, a);     \
     break;

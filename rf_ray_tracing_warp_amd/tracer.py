@@ -151,3 +151,53 @@ class Tracer:
             print(f"Traced {len(cleaned_paths)} paths in {time.perf_counter() - start_time} seconds")
         rx_mesh.close()
         return cleaned_paths, impulse_response
+
+    def compute_cir_distributed(self, tx_pos, tx_power, rx_pos, rx_radius, group=None):
+        """``compute_cir`` with the burst sharded over the ranks of ``group``.
+
+        Rank r traces the global ray ids [N*r/world, N*(r+1)/world): ids are global (kernel.py:48-51),
+        so every ray's path is the one the single-GPU call traces, and each path keeps amplitude
+        tx_power / N.  The impulse responses are sum-reduced (RCCL on an "nccl" group, host tensors on
+        gloo) and the received rows are gathered in rank order, which is ray-id order.  Every rank
+        returns the same (cleaned_paths, impulse_response) as ``compute_cir`` (bins exactly; each
+        bin's amplitude up to the order of its f64 sum).
+        """
+        import torch
+        import torch.distributed as dist
+
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        dev = f"cuda:{self.device}"
+        N, P = self.tx_num_rays, self.max_bounces + 1
+        lo, hi = N * rank // world, N * (rank + 1) // world
+        n = hi - lo
+        rx_mesh = self._generate_rx_mesh(rx_pos, rx_radius)
+        received = torch.empty((max(n, 1), P, 3), dtype=torch.float32, device=dev)
+        mask = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        ir = torch.zeros(self.n_bins(), dtype=torch.float64, device=dev)
+        traced = torch.empty((max(n, 1), P, 3), dtype=torch.float32, device=dev) if self.max_bounces > 8 else None
+        k = 0
+        rows = np.zeros((0, P, 3), np.float32)
+        if n > 0:
+            self.trace_device(tx_pos, rx_mesh, received, mask, traced=traced, ray_offset=lo, n=n)
+            index, count = self.cir_device(received, mask, tx_power, ir, n=n)
+            k = int(count.item())
+            if k:
+                rows = received.index_select(0, index[:k]).cpu().numpy()
+        if dist.get_backend(group) == "nccl":
+            dist.all_reduce(ir, group=group)
+            impulse_response = ir.cpu().numpy()
+        else:
+            host = ir.cpu()
+            dist.all_reduce(host, group=group)
+            impulse_response = host.numpy()
+        parts = [None] * world
+        dist.all_gather_object(parts, rows, group=group)
+        cleaned_paths = []
+        for part in parts:
+            for row in part:  # tracer.py:90-97
+                bad = np.isnan(row).any(axis=1)
+                L = int(np.argmax(bad)) if bad.any() else P
+                cleaned_paths.append(np.array(row[:L]))
+        rx_mesh.close()
+        return cleaned_paths, impulse_response
+
