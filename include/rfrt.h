@@ -39,6 +39,14 @@ int rt_version(void);
  * vertices: host float32 (nv,3); faces: host int32 (nf,3).  Builds the device tables (and a BVH
  * for large meshes) on `device`; the library owns the handle. */
 int rt_mesh_create(int device, const float* vertices, int64_t nv, const int32_t* faces, int64_t nf, rt_mesh** out);
+/* rt_mesh_create with builder flags: 0 = host binned-SAH BVH (default, best trees),
+ * RT_MESH_BVH_GPU = device LBVH over Morton codes (milliseconds for millions of
+ * faces; falls back to the host build if its tree is deeper than the traversal stack).  Meshes
+ * of <= 192 faces are traced by brute force and have no BVH either way; results never depend on
+ * the tree (closest hit = lexicographic (t, face) minimum). */
+#define RT_MESH_BVH_GPU 1
+int rt_mesh_create_ex(int device, const float* vertices, int64_t nv, const int32_t* faces, int64_t nf, int flags,
+                      rt_mesh** out);
 /* Replaces the wp.Mesh destructor (freed on Python GC in the reference). */
 int rt_mesh_destroy(rt_mesh* mesh);
 /* nf, bounds6 = (lo xyz, hi xyz), sphere4 = conservative bounding sphere (centre, radius). Any may be NULL. */
@@ -57,7 +65,8 @@ int rt_bvh_info(const rt_mesh* mesh, int64_t* info4);
  *   row_mask (n) u32          kernel.py:91
  *   hit_kind (n, B) i32       per bounce 0 miss / 1 env / 2 receiver   (diagnostic, not in reference)
  *   hit_face (n, B) i32       per bounce face id of the chosen hit, -1 on miss (diagnostic)
- * rx may be NULL (no receiver).  max_bounces > 8 requires `traced` (it holds the path). */
+ * rx may be NULL (no receiver); it is queried by brute force, so at most 65536 faces (RT_EINVAL
+ * otherwise, before any launch).  max_bounces > 8 requires `traced` (it holds the path). */
 int rt_trace(const rt_mesh* env, const float* tx_pos, const rt_mesh* rx, int max_bounces, int64_t ray_offset,
              int64_t n, float* traced, float* received, uint32_t* row_mask, int32_t* hit_kind, int32_t* hit_face,
              void* stream);
@@ -89,7 +98,7 @@ typedef struct {
 typedef struct rt_coverage rt_coverage;
 
 /* Plan a coverage run: env mesh, bounces (1..15), rays per cell (global ids ray_offset + [0,n)),
- * receiver radius; cells with index % shard_count == shard_index are computed (multi-GPU). */
+ * receiver radius; cells in x columns ix % shard_count == shard_index are computed (multi-GPU). */
 int rt_coverage_create(int device, const rt_mesh* env, int max_bounces, int64_t n_rays, int64_t ray_offset,
                        const rt_grid* grid, double rx_radius, int shard_index, int shard_count, rt_coverage** out);
 int rt_coverage_destroy(rt_coverage* cov);

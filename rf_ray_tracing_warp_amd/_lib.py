@@ -12,6 +12,7 @@ import numpy as np
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RFRT_LIB_PATH") or os.path.join(_PKG, "librfrt.so")
 
+RT_MESH_BVH_GPU = 1
 RT_CIR_C_F64 = 1
 RT_CIR_FS_F64 = 2
 
@@ -37,6 +38,7 @@ def lib():
     L.rt_last_error.restype = ctypes.c_char_p
     L.rt_version.restype = _int
     L.rt_mesh_create.argtypes = [_int, _vp, _i64, _vp, _i64, ctypes.POINTER(_vp)]
+    L.rt_mesh_create_ex.argtypes = [_int, _vp, _i64, _vp, _i64, _int, ctypes.POINTER(_vp)]
     L.rt_mesh_destroy.argtypes = [_vp]
     L.rt_mesh_info.argtypes = [_vp, _vp, _vp, _vp]
     L.rt_bvh_info.argtypes = [_vp, _vp]
@@ -56,7 +58,7 @@ def lib():
     L.rt_selftest_math.argtypes = [_vp, _i64, _vp, _int, _vp]
     L.rt_ray_dirs.argtypes = [_i64, _i64, _vp, _vp]
     L.rt_query.argtypes = [_vp, _vp, _vp, _i64, _vp, _vp, _vp]
-    for name in ("rt_mesh_create", "rt_mesh_destroy", "rt_mesh_info", "rt_bvh_info", "rt_trace", "rt_compact", "rt_cir",
+    for name in ("rt_mesh_create", "rt_mesh_create_ex", "rt_mesh_destroy", "rt_mesh_info", "rt_bvh_info", "rt_trace", "rt_compact", "rt_cir",
                  "rt_coverage_create", "rt_coverage_destroy", "rt_coverage_run", "rt_coverage_received",
                  "rt_power_dense", "rt_selftest_math", "rt_ray_dirs", "rt_query"):
         getattr(L, name).restype = _int
@@ -83,14 +85,19 @@ def stream_handle(device) -> int:
 class DeviceMesh:
     """A triangle mesh resident on one GPU (the wp.Mesh of tracer.py:24,30)."""
 
-    def __init__(self, vertices, faces, device: int = 0):
+    def __init__(self, vertices, faces, device: int = 0, builder: str = "sah"):
+        """builder: "sah" (host binned-SAH BVH, default) or "gpu" (device LBVH, RT_MESH_BVH_GPU);
+        only meshes of more than 192 faces get a BVH, and results do not depend on it."""
         v = np.ascontiguousarray(np.asarray(vertices, dtype=np.float64).astype(np.float32)).reshape(-1, 3)
         f = np.ascontiguousarray(np.asarray(faces).astype(np.int32)).reshape(-1, 3)
+        if builder not in ("sah", "gpu"):
+            raise ValueError(f"builder must be 'sah' or 'gpu', not {builder!r}")
         self.device = int(device)
         self.num_faces = len(f)
         self._h = _vp()
-        check(lib().rt_mesh_create(self.device, v.ctypes.data, len(v), f.ctypes.data, len(f), ctypes.byref(self._h)),
-              "rt_mesh_create")
+        flags = RT_MESH_BVH_GPU if builder == "gpu" else 0
+        check(lib().rt_mesh_create_ex(self.device, v.ctypes.data, len(v), f.ctypes.data, len(f), flags,
+                                      ctypes.byref(self._h)), "rt_mesh_create_ex")
 
     @property
     def handle(self):

@@ -26,7 +26,8 @@ int hip_fail(hipError_t e, const char* what) {
 int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B, int64_t ray_offset, int64_t n,
                  float* traced, float* received, uint32_t* mask, int32_t* hit_kind, int32_t* hit_face,
                  hipStream_t stream);
-int build_bvh(rt_mesh* m, const std::vector<float>& tri);  // bvh.hip
+int build_bvh(rt_mesh* m, const std::vector<float>& tri);      // bvh.hip (host, binned SAH)
+int build_bvh_gpu(rt_mesh* m, const std::vector<float>& tri);  // bvh_gpu.hip (device LBVH)
 }  // namespace rt
 
 extern "C" {
@@ -41,7 +42,12 @@ static inline float h_dot(const float* a, const float* b) {
 }
 
 int rt_mesh_create(int device, const float* vertices, int64_t nv, const int32_t* faces, int64_t nf, rt_mesh** out) {
-  if (!out || (nf > 0 && (!vertices || !faces)) || nv < 0 || nf < 0) {
+  return rt_mesh_create_ex(device, vertices, nv, faces, nf, 0, out);
+}
+
+int rt_mesh_create_ex(int device, const float* vertices, int64_t nv, const int32_t* faces, int64_t nf, int flags,
+                      rt_mesh** out) {
+  if (!out || (nf > 0 && (!vertices || !faces)) || nv < 0 || nf < 0 || (flags & ~RT_MESH_BVH_GPU) != 0) {
     rt::set_error("rt_mesh_create: invalid arguments");
     return RT_EINVAL;
   }
@@ -53,7 +59,12 @@ int rt_mesh_create(int device, const float* vertices, int64_t nv, const int32_t*
     }
   }
   RT_HIP(hipSetDevice(device));
-  std::vector<float> perm((size_t)std::max<int64_t>(nf, 1) * 72, 0.0f);
+  // the permuted-corner table feeds the brute-force queries: environments of <= 192 faces
+  // (staged in LDS) and receivers (read from HBM, rt_trace).  BVH environments read lcomp, so the
+  // table (288 B/face) is skipped for meshes too large to serve as a brute-force receiver.
+  const bool brute = nf <= RT_BRUTE_MAX_FACES;
+  const bool want_perm = nf <= RT_PERM_MAX_FACES;
+  std::vector<float> perm(want_perm ? (size_t)std::max<int64_t>(nf, 1) * 72 : 0, 0.0f);
   std::vector<float> nrm((size_t)std::max<int64_t>(nf, 1) * 4, 0.0f);
   std::vector<float> tri((size_t)std::max<int64_t>(nf, 1) * 9, 0.0f);
   double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -66,7 +77,7 @@ int rt_mesh_create(int device, const float* vertices, int64_t nv, const int32_t*
         lo[k] = std::min(lo[k], (double)c[v][k]);
         hi[k] = std::max(hi[k], (double)c[v][k]);
       }
-    for (int kz = 0; kz < 3; ++kz)
+    for (int kz = 0; kz < 3 && want_perm; ++kz)
       for (int sw = 0; sw < 2; ++sw) {
         int kx = kz + 1;
         if (kx == 3) kx = 0;
@@ -111,16 +122,19 @@ int rt_mesh_create(int device, const float* vertices, int64_t nv, const int32_t*
     m->hi[k] = nf > 0 ? (float)hi[k] : 0.0f;
   }
   m->radius = (float)(rmax * (1.0 + 1e-3) + 1e-5 * (1.0 + amax));
-  hipError_t e = hipMalloc(&m->perm, perm.size() * sizeof(float));
+  hipError_t e = want_perm ? hipMalloc(&m->perm, perm.size() * sizeof(float)) : hipSuccess;
   if (e == hipSuccess) e = hipMalloc(&m->nrm, nrm.size() * sizeof(float));
-  if (e == hipSuccess) e = hipMemcpy(m->perm, perm.data(), perm.size() * sizeof(float), hipMemcpyHostToDevice);
+  if (e == hipSuccess && want_perm)
+    e = hipMemcpy(m->perm, perm.data(), perm.size() * sizeof(float), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(m->nrm, nrm.data(), nrm.size() * sizeof(float), hipMemcpyHostToDevice);
   if (e != hipSuccess) {
     rt_mesh_destroy(m);
     return rt::hip_fail(e, "rt_mesh_create upload");
   }
-  if (nf > RT_BRUTE_MAX_FACES) {
-    int rc = rt::build_bvh(m, tri);
+  if (!brute) {
+    int rc = 1;
+    if (flags & RT_MESH_BVH_GPU) rc = rt::build_bvh_gpu(m, tri);  // 1: too deep for the stack
+    if (rc == 1) rc = rt::build_bvh(m, tri);
     if (rc) {
       rt_mesh_destroy(m);
       return rc;
@@ -178,8 +192,8 @@ int rt_trace(const rt_mesh* env, const float* tx_pos, const rt_mesh* rx, int max
     rt::set_error("rt_trace: invalid arguments");
     return RT_EINVAL;
   }
-  if (rx && rx->nf > (int64_t)1 << 24) {
-    rt::set_error("rt_trace: receiver mesh too large (max 2^24 faces, brute force)");
+  if (rx && (rx->nf > RT_PERM_MAX_FACES || !rx->perm)) {
+    rt::set_error("rt_trace: receiver mesh too large (max 65536 faces, queried by brute force)");
     return RT_EINVAL;
   }
   if (max_bounces == 0) return RT_OK;

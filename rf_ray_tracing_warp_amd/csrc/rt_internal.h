@@ -46,3 +46,4 @@ const int32_t* dir_order(int64_t ray_offset, int64_t n, hipStream_t stream, void
 
 // faces at or below this count are traced by the brute-force LDS kernel (whole mesh in LDS)
 #define RT_BRUTE_MAX_FACES 192
+#define RT_PERM_MAX_FACES (1 << 16)  // largest mesh given the permuted table (receivers are brute-forced)

@@ -111,8 +111,8 @@ def test_query_bitexact(which, room):
     assert (rf >= 0).mean() > 0.05
 
 
-def _gpu_trace(env, rxm, tx, B, off, n, want_traced=True):
-    e = DeviceMesh(env.vertices, env.faces)
+def _gpu_trace(env, rxm, tx, B, off, n, want_traced=True, builder="sah"):
+    e = DeviceMesh(env.vertices, env.faces, builder=builder)
     r = DeviceMesh(rxm.vertices, rxm.faces) if rxm is not None else None
     P = B + 1
     out = {
@@ -262,7 +262,8 @@ def terrain256():
     return synthetic_terrain(256, 50.0)
 
 
-def test_bvh_query_bitexact(terrain256):
+@pytest.mark.parametrize("builder", ["sah", "gpu"])
+def test_bvh_query_bitexact(terrain256, builder):
     t = terrain256
     rng = np.random.default_rng(11)
     n = 300_000
@@ -275,7 +276,9 @@ def test_bvh_query_bitexact(terrain256):
     hit = fb >= 0
     o = np.concatenate([o, (o[hit] + d[hit] * tb[hit][:, None]).astype(np.float32)])  # rays leaving the surface
     d = np.concatenate([d, d[hit]])
-    dm = DeviceMesh(t.vertices, t.faces)
+    dm = DeviceMesh(t.vertices, t.faces, builder=builder)
+    info = dm.bvh_info()
+    assert info["nodes"] > 0 and 0 < info["depth"] <= 60 and info["max_leaf"] <= 4
     ot, dt = torch.from_numpy(o).to(DEV), torch.from_numpy(d).to(DEV)
     tt = torch.empty(len(o), dtype=torch.float32, device=DEV)
     ff = torch.empty(len(o), dtype=torch.int32, device=DEV)
@@ -285,14 +288,57 @@ def test_bvh_query_bitexact(terrain256):
     np.testing.assert_array_equal(_bits(tt.cpu().numpy()), _bits(rt_))
 
 
-@pytest.mark.parametrize("B,off,n", [(5, 0, 60_000), (3, 5_000_000, 40_000), (12, 7, 10_000)])
-def test_trace_bvh_bitexact(terrain256, B, off, n):
+@pytest.mark.parametrize("B,off,n,builder", [(5, 0, 60_000, "sah"), (3, 5_000_000, 40_000, "sah"),
+                                             (12, 7, 10_000, "sah"), (5, 0, 80_000, "gpu")])
+def test_trace_bvh_bitexact(terrain256, B, off, n, builder):
     tx, rx = (10.0, 0.0, 4.5), (-10.125, 0.0, 4.8)  # main.py:22-23
     rxm = sphere(rx, 0.1, 1)
-    g = _gpu_trace(terrain256, rxm, tx, B, off, n)
+    g = _gpu_trace(terrain256, rxm, tx, B, off, n, builder=builder)
     o = orc.trace(orc.Mesh(terrain256.vertices, terrain256.faces), orc.Mesh(rxm.vertices, rxm.faces), tx, B, off, n)
     _assert_trace_equal(g, o)
     assert (g["hit_kind"] == 1).sum() > n // 4
+
+
+def test_receiver_too_large_rejected(terrain256):
+    """Receivers are queried by brute force: a mesh beyond 65536 faces is refused before launch."""
+    from rf_ray_tracing_warp_amd._lib import RfrtError
+    from rf_ray_tracing_warp_amd.mesh import icosphere
+    v, f = icosphere(6)  # 81920 faces
+    big = DeviceMesh(v * 0.1, f)
+    env = DeviceMesh(terrain256.vertices, terrain256.faces)
+    n = 1024
+    rec = torch.empty((n, 4, 3), dtype=torch.float32, device=DEV)
+    mask = torch.empty(n, dtype=torch.int32, device=DEV)
+    tx = np.asarray((0.0, 0.0, 5.0), np.float32)
+    rc = lib().rt_trace(env.handle, tx.ctypes.data, big.handle, 3, 0, n, None, ptr(rec), ptr(mask), None, None,
+                        _stream())
+    assert rc != 0 and b"receiver mesh too large" in lib().rt_last_error()
+    with pytest.raises(RfrtError):
+        check(rc, "rt_trace")
+
+
+def test_gpu_bvh_build_k4_mesh():
+    """the device LBVH builds the 2.09M-face K4 mesh in well under the host SAH time,
+    and traces on it equal the oracle (sampled rows of a 200k-ray, 5-bounce burst)."""
+    import time
+    from rf_ray_tracing_warp_amd.mesh import synthetic_terrain
+    t = synthetic_terrain(1024, 50.0)
+    t0 = time.perf_counter()
+    dm = DeviceMesh(t.vertices, t.faces, builder="gpu")
+    t_gpu = time.perf_counter() - t0
+    info = dm.bvh_info()
+    dm.close()
+    t0 = time.perf_counter()
+    DeviceMesh(t.vertices, t.faces, builder="sah").close()
+    t_sah = time.perf_counter() - t0
+    print(f"mesh create: gpu LBVH {t_gpu:.3f} s, host SAH {t_sah:.3f} s, {info}")
+    assert t_gpu < t_sah and info["depth"] <= 60
+    n, B, tx, rx = 200_000, 5, (10.0, 0.0, 4.5), (-10.125, 0.0, 4.8)
+    rxm = sphere(rx, 0.1, 1)
+    g = _gpu_trace(t, rxm, tx, B, 0, n, builder="gpu")
+    rows = np.union1d(np.arange(0, n, 100), np.nonzero(g["mask"])[0])
+    o = orc.trace_ids(orc.Mesh(t.vertices, t.faces), orc.Mesh(rxm.vertices, rxm.faces), tx, B, rows)
+    _assert_trace_equal(g, o, rows)
 
 
 def test_trace_k4_terrain_full_mesh():

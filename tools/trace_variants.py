@@ -24,7 +24,7 @@ def child(n, B, reps, scene="room"):
     else:
         m = load_stl(os.path.join(ROOT, "models/room.stl"))
         txp, rxp = (10.0, 0.0, 5.0), (-10.0, 0.0, 5.0)
-    env = DeviceMesh(m.vertices, m.faces, 0)
+    env = DeviceMesh(m.vertices, m.faces, 0, builder=os.environ.get("BUILDER", "sah"))
     rs = sphere(rxp, 0.1, 1)
     rx = DeviceMesh(rs.vertices, rs.faces, 0)
     P = B + 1
