@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--coverage-grid", type=int, default=256, help="K3: n x n receiver cells at z=5 on room.stl")
     ap.add_argument("--coverage-rays", type=int, default=1_000_000)
     ap.add_argument("--coverage-runs", type=int, default=3)
+    ap.add_argument("--coverage-shard", choices=("rays", "cells"), default="rays",
+                    help="N>1 coverage decomposition: ray shards + record all-to-all, or x-column cell shards")
     ap.add_argument("--no-k4", action="store_true", help="skip the terrain (apollo stand-in) legs K4/K5")
     ap.add_argument("--k4-rays", type=int, default=2_097_152, help="rays per GPU (K4: 16.7M over 8 GPUs)")
     ap.add_argument("--k5-grid", type=int, default=1024)
@@ -82,15 +84,27 @@ def cpu_baseline(sample_rays, B, tx, rx, min_s=10.0, max_rays=400_000_000):
                       f"{dt:.1f} s"}
 
 
+def shard_desc(mode, world):
+    if world == 1:
+        return "1 GPU"
+    if mode == "rays":
+        return (f"rays sharded x{world} (1/{world} of every cell's rays per GPU), (cell, bin, amplitude) records "
+                f"to the cells' owners (ix % {world}) by one RCCL all-to-all, RCCL sum of the power map")
+    return f"cells sharded by x column (ix % {world}), every GPU traces all rays, RCCL sum of the power map"
+
+
 def coverage_leg(args, env_m, env, local, rank, world, dist):
     """K3: coverage.py on room.stl, n x n cells at z = 5, tx (10,0,5), 1M rays per cell, 3 bounces.
-    Cells are sharded by x column (ix % world) over the ranks; the power map is sum-reduced (RCCL)."""
+    N > 1: each rank traces 1/N of every cell's rays and sends its (cell, bin, amplitude) records to
+    the cells' owners (x columns, ix % world) in one RCCL all-to-all, or (--coverage-shard cells)
+    each rank computes its x columns from all rays; the power map is sum-reduced (RCCL)."""
     import torch
     from rf_ray_tracing_warp_amd.coverage import Coverage, CoverageGrid
 
     grid = CoverageGrid.square(args.coverage_grid, 15.0, 5.0)
+    mode = args.coverage_shard if world > 1 else "cells"
     cov = Coverage(env_m, 2.998e8, 100e9, 100e-9, args.bounces, args.coverage_rays, grid, 0.1, device=local,
-                   shard_index=rank, shard_count=world, env_mesh=env)
+                   shard_index=rank, shard_count=world, env_mesh=env, shard_mode=mode)
     tx = (10.0, 0.0, 5.0)
 
     def one():
@@ -122,7 +136,7 @@ def coverage_leg(args, env_m, env, local, rank, world, dist):
     return {"metric": "coverage cells/sec", "value": grid.num_cells / dt, "unit": "cells/s", "ms_per_map": dt * 1e3,
             "workload": f"K3: room.stl, {grid.nx}x{grid.ny} receivers at z=5 (centres -15+(i+1/2)*30/{grid.nx}), "
                         f"tx (10,0,5), {args.coverage_rays} rays per cell, {args.bounces} bounces, 10000 bins, "
-                        f"signal power per cell; cells sharded by x column (ix % {world}) + RCCL sum of the power map",
+                        f"signal power per cell; {shard_desc(mode, world)}",
             "scaling": "strong", "cells_receiving": int(np.isfinite(pm).sum()),
             "candidates": int(cand.item()), "algorithm": "exact shared-trajectory (csrc/coverage.hip)"}
 
@@ -178,8 +192,9 @@ def terrain_legs(args, local, rank, world, dist):
           "scaling": "weak", "mesh_build_s": t_build}
     del traced, received, mask
     grid = CoverageGrid.square(args.k5_grid, 50.0, 2.0)
+    mode = args.coverage_shard if world > 1 else "cells"
     cov = Coverage(terr, 2.998e8, 100e9, 200e-9, 3, args.k5_rays, grid, 0.1, device=local, shard_index=rank,
-                   shard_count=world, env_mesh=env)
+                   shard_count=world, env_mesh=env, shard_mode=mode)
 
     def one():
         p = cov.run_device((10.0, 0.0, 4.5), 1)
@@ -204,7 +219,7 @@ def terrain_legs(args, local, rank, world, dist):
     pm = p.cpu().numpy()
     k5 = {"metric": "coverage cells/sec", "value": grid.num_cells / dt, "unit": "cells/s", "ms_per_map": dt * 1e3,
           "workload": f"K5 on the terrain stand-in: {grid.nx}x{grid.ny} receivers at z=2 over +-50 m, tx (10,0,4.5), "
-                      f"{args.k5_rays} rays per cell, 3 bounces, 20000 bins; cells sharded by x column (ix % {world}) + RCCL sum",
+                      f"{args.k5_rays} rays per cell, 3 bounces, 20000 bins; {shard_desc(mode, world)}",
           "scaling": "strong", "cells_receiving": int(np.isfinite(pm).sum()), "candidates": int(cov.last_candidates)}
     cov.close()
     return k4, k5

@@ -109,7 +109,32 @@ int rt_coverage_destroy(rt_coverage* cov);
  * triples.  Synchronises the stream once (candidate count). */
 int rt_coverage_run(rt_coverage* cov, const float* tx_pos, double tx_power, double light_speed, double sample_rate,
                     int flags, int64_t n_bins, double alpha, double* power, int64_t* stats, void* stream);
-/* Sparse per-cell impulse responses of the last run: keys (cell << 32 | bin) ascending, amplitudes. */
+/* ---- ray-sharded coverage (multi-GPU, SURVEY §8 E1 with F2): rank r of `world` traces global ray
+ * ids [ray_offset, ray_offset + n_rays) of a burst of n_rays_total rays per cell (amplitude
+ * tx_power / n_rays_total, tracer.py:103) for EVERY cell, sums its first-win records per
+ * (cell, bin) in ray order, and sends each cell's records to the cell's owner, the rank with
+ * ix % world == rank (ix = cell % nx).  The owner sums the runs it receives (in rank order, i.e.
+ * ray order) and computes the power of its cells.  Replaces the per-cell loop of coverage.py:38-57
+ * split over ranks; every rank's trajectory, candidate and replay work shrinks with the rank
+ * count, and the exchange is a sparse all-to-all of (cell, bin, amplitude) records.
+ *   1. rt_coverage_create_rays                         (once)
+ *   2. rt_coverage_trace_records -> counts[world]      (records for each destination rank; syncs)
+ *   3. rt_coverage_records -> caller device buffers    (grouped by destination, rank 0 first)
+ *   4. all-to-all of the records (the caller's collective: RCCL via torch.distributed)
+ *   5. rt_coverage_power_records on the received records, concatenated in source-rank order
+ *   6. sum-reduce of the power maps (other ranks' cells are 0 here). */
+int rt_coverage_create_rays(int device, const rt_mesh* env, int max_bounces, int64_t n_rays_total, int64_t ray_offset,
+                            int64_t n_rays, const rt_grid* grid, double rx_radius, int rank, int world,
+                            rt_coverage** out);
+int rt_coverage_trace_records(rt_coverage* cov, const float* tx_pos, double tx_power, double light_speed,
+                              double sample_rate, int flags, int64_t n_bins, int64_t* counts, int64_t* stats,
+                              void* stream);
+/* keys_out (cell << 32 | bin), amps_out: device, max_out >= sum(counts). */
+int rt_coverage_records(rt_coverage* cov, uint64_t* keys_out, double* amps_out, int64_t max_out, void* stream);
+int rt_coverage_power_records(rt_coverage* cov, const uint64_t* keys, const double* amps, int64_t n, int64_t n_bins,
+                              double alpha, double* power, void* stream);
+/* Sparse per-cell impulse responses of the last rt_coverage_run (or, ray-sharded, of this rank's cells
+ * after rt_coverage_power_records): keys (cell << 32 | bin) ascending, amplitudes. */
 int rt_coverage_received(rt_coverage* cov, uint64_t* keys_out, double* amps_out, int64_t max_out, int64_t* n_out,
                          void* stream);
 /* Signal power (same definition) of `rows` dense impulse responses (rows, n_bins) f64 on the device.

@@ -53,6 +53,12 @@ def lib():
     L.rt_coverage_destroy.argtypes = [_vp]
     L.rt_coverage_run.argtypes = [_vp, _vp, ctypes.c_double, ctypes.c_double, ctypes.c_double, _int, _i64,
                                   ctypes.c_double, _vp, _vp, _vp]
+    L.rt_coverage_create_rays.argtypes = [_int, _vp, _int, _i64, _i64, _i64, _vp, ctypes.c_double, _int, _int,
+                                          ctypes.POINTER(_vp)]
+    L.rt_coverage_trace_records.argtypes = [_vp, _vp, ctypes.c_double, ctypes.c_double, ctypes.c_double, _int, _i64,
+                                            _vp, _vp, _vp]
+    L.rt_coverage_records.argtypes = [_vp, _vp, _vp, _i64, _vp]
+    L.rt_coverage_power_records.argtypes = [_vp, _vp, _vp, _i64, _i64, ctypes.c_double, _vp, _vp]
     L.rt_coverage_received.argtypes = [_vp, _vp, _vp, _i64, ctypes.POINTER(_i64), _vp]
     L.rt_power_dense.argtypes = [_vp, _i64, _i64, ctypes.c_double, _vp, _i64, _vp, _vp]
     L.rt_selftest_math.argtypes = [_vp, _i64, _vp, _int, _vp]
@@ -60,6 +66,8 @@ def lib():
     L.rt_query.argtypes = [_vp, _vp, _vp, _i64, _vp, _vp, _vp]
     for name in ("rt_mesh_create", "rt_mesh_create_ex", "rt_mesh_destroy", "rt_mesh_info", "rt_bvh_info", "rt_trace", "rt_compact", "rt_cir",
                  "rt_coverage_create", "rt_coverage_destroy", "rt_coverage_run", "rt_coverage_received",
+                 "rt_coverage_create_rays", "rt_coverage_trace_records", "rt_coverage_records",
+                 "rt_coverage_power_records",
                  "rt_power_dense", "rt_selftest_math", "rt_ray_dirs", "rt_query"):
         getattr(L, name).restype = _int
     _lib = L

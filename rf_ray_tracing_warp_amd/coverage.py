@@ -3,8 +3,11 @@
 coverage.py:38-57 loops over receiver positions, runs ``Tracer.compute_cir`` for each and turns the
 impulse response into a received signal power (coverage.py:45-52), then dBm.  ``Coverage`` computes
 the same per-cell power for a whole lattice of receivers in one shot (csrc/coverage.hip, exact
-shared-trajectory algorithm).  Cells can be sharded across ranks (one process per GPU); the power
-map is then sum-reduced over the process group (RCCL over xGMI with the "nccl" backend).
+shared-trajectory algorithm).  Across ranks (one process per GPU) the work is split either by rays
+(``shard_mode="rays"``, the default of ``coverage_map``: every rank traces its share of each cell's
+rays, records go to the cells' owners in one sparse all-to-all) or by cells (``"cells"``: every
+rank traces all rays for its x columns); the power map is then sum-reduced over the process group
+(RCCL over xGMI with the "nccl" backend).
 
     grid = CoverageGrid.from_ranges(range(-15, 16, 2), range(-15, 16, 2), range(0, 16, 2))  # coverage.py:38-40
     cov = Coverage(mesh, 2.998e8, 100e9, 100e-9, max_bounces=2, tx_num_rays=1_000_000, grid=grid)
@@ -19,6 +22,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import _lib
+from . import dist as rdist
 from ._lib import DeviceMesh, check, lib, ptr
 from .power import CARRIER_HZ, to_dbm
 from .tracer import cir_flags
@@ -96,7 +100,11 @@ class Coverage:
 
     def __init__(self, environment_trimesh, light_speed_mps, sample_rate_hz, sample_window_s, max_bounces,
                  tx_num_rays, grid: CoverageGrid, rx_radius=0.1, device: int | None = None, shard_index: int = 0,
-                 shard_count: int = 1, env_mesh: DeviceMesh | None = None):
+                 shard_count: int = 1, env_mesh: DeviceMesh | None = None, shard_mode: str = "cells"):
+        """shard_index / shard_count: this rank of the job.  shard_mode "cells": this rank traces all
+        tx_num_rays rays for the cells of its x columns (ix % shard_count == shard_index); "rays":
+        it traces its contiguous share of the rays (dist.ray_range) for every cell and exchanges
+        records with the other ranks in run() (dist.exchange_records)."""
         import torch
 
         if not torch.cuda.is_available():
@@ -111,17 +119,69 @@ class Coverage:
         self.rx_radius = float(rx_radius)
         self.n_bins = int(sample_window_s * sample_rate_hz)
         self.shard_index, self.shard_count = int(shard_index), int(shard_count)
+        if shard_mode not in ("cells", "rays"):
+            raise ValueError(f"shard_mode must be 'cells' or 'rays', not {shard_mode!r}")
+        self.shard_mode = shard_mode
         self.env = env_mesh or DeviceMesh(environment_trimesh.vertices, environment_trimesh.faces, self.device)
         self._h = _lib._vp()
         g = grid._c()
-        check(lib().rt_coverage_create(self.device, self.env.handle, self.max_bounces, self.tx_num_rays, 0,
-                                       ctypes.byref(g), self.rx_radius, self.shard_index, self.shard_count,
-                                       ctypes.byref(self._h)), "rt_coverage_create")
+        if shard_mode == "rays":
+            self.ray_offset, self.ray_count = rdist.ray_range(self.shard_index, self.shard_count, self.tx_num_rays)
+            check(lib().rt_coverage_create_rays(self.device, self.env.handle, self.max_bounces, self.tx_num_rays,
+                                                self.ray_offset, self.ray_count, ctypes.byref(g), self.rx_radius,
+                                                self.shard_index, self.shard_count, ctypes.byref(self._h)),
+                  "rt_coverage_create_rays")
+        else:
+            self.ray_offset, self.ray_count = 0, self.tx_num_rays
+            check(lib().rt_coverage_create(self.device, self.env.handle, self.max_bounces, self.tx_num_rays, 0,
+                                           ctypes.byref(g), self.rx_radius, self.shard_index, self.shard_count,
+                                           ctypes.byref(self._h)), "rt_coverage_create")
         self.power = torch.empty(grid.num_cells, dtype=torch.float64, device=f"cuda:{self.device}")
         self.last_candidates = 0
 
-    def run_device(self, tx_pos, tx_power=1):
-        """Launch; returns the (num_cells,) float64 device tensor (0 for cells of other shards)."""
+    def trace_records(self, tx_pos, tx_power=1):
+        """Ray mode, stage 1: this rank's rays for every cell.  Returns (keys, amps, counts): device
+        int64 keys (cell << 32 | bin) and float64 amplitudes summed per (cell, bin) over this rank's
+        rays, grouped by owner rank, counts[d] records for rank d."""
+        import torch
+
+        if self.shard_mode != "rays":
+            raise _lib.RfrtError("trace_records needs shard_mode='rays'")
+        tx = np.ascontiguousarray(np.asarray(tx_pos, dtype=np.float64).astype(np.float32))
+        counts = np.zeros(self.shard_count, np.int64)
+        stats = np.zeros(2, np.int64)
+        check(lib().rt_coverage_trace_records(self._h, tx.ctypes.data, float(tx_power), float(self.light_speed_mps),
+                                              float(self.sample_rate_hz),
+                                              cir_flags(self.light_speed_mps, self.sample_rate_hz), self.n_bins,
+                                              counts.ctypes.data, stats.ctypes.data, _lib.stream_handle(self.device)),
+              "rt_coverage_trace_records")
+        self.last_candidates = int(stats[0])
+        n = int(counts.sum())
+        dev = f"cuda:{self.device}"
+        keys = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+        amps = torch.empty(max(n, 1), dtype=torch.float64, device=dev)
+        check(lib().rt_coverage_records(self._h, ptr(keys), ptr(amps), n, _lib.stream_handle(self.device)),
+              "rt_coverage_records")
+        return keys[:n], amps[:n], [int(c) for c in counts]
+
+    def power_from_records(self, keys, amps):
+        """Ray mode, last stage: the power of this rank's cells from the records every rank sent it
+        (concatenated in source-rank order); the (num_cells,) float64 device map, 0 elsewhere."""
+        n = int(keys.numel())
+        check(lib().rt_coverage_power_records(self._h, ptr(keys) if n else None, ptr(amps) if n else None, n,
+                                              self.n_bins, phase_step(self.sample_window_s, self.n_bins),
+                                              ptr(self.power), _lib.stream_handle(self.device)),
+              "rt_coverage_power_records")
+        return self.power
+
+    def run_device(self, tx_pos, tx_power=1, process_group=None):
+        """Launch; returns the (num_cells,) float64 device tensor (0 for cells of other shards).
+        Ray mode with more than one shard exchanges records over ``process_group`` here."""
+        if self.shard_mode == "rays":
+            keys, amps, counts = self.trace_records(tx_pos, tx_power)
+            if self.shard_count > 1:
+                keys, amps = rdist.exchange_records(keys, amps, counts, process_group)
+            return self.power_from_records(keys, amps)
         tx = np.ascontiguousarray(np.asarray(tx_pos, dtype=np.float64).astype(np.float32))
         stats = np.zeros(2, np.int64)
         check(lib().rt_coverage_run(self._h, tx.ctypes.data, float(tx_power), float(self.light_speed_mps),
@@ -133,7 +193,7 @@ class Coverage:
 
     def run(self, tx_pos, tx_power=1, process_group=None):
         """Power map (nz, ny, nx) float64 on the host; with a process group, sum-reduced over ranks."""
-        p = self.run_device(tx_pos, tx_power)
+        p = self.run_device(tx_pos, tx_power, process_group)
         if process_group is not None or self.shard_count > 1:
             import torch.distributed as dist
             dist.all_reduce(p, group=process_group)
@@ -186,12 +246,14 @@ def _dist_shard():
 
 def coverage_map(environment_trimesh, tx_pos, grid: CoverageGrid, light_speed_mps=2.998e8, sample_rate_hz=100e9,
                  sample_window_s=100e-9, max_bounces=2, tx_num_rays=1_000_000, tx_power=1, rx_radius=0.1,
-                 device=None):
-    """coverage.py as a function.  Under torch.distributed, cells are sharded over the ranks and the
-    power map is all-reduced; every rank returns the full map."""
+                 device=None, shard_mode="rays"):
+    """coverage.py as a function.  Under torch.distributed the work is sharded over the ranks (by
+    rays with a record all-to-all, or by x columns of cells) and the power map is all-reduced;
+    every rank returns the full map."""
     rank, world = _dist_shard()
     cov = Coverage(environment_trimesh, light_speed_mps, sample_rate_hz, sample_window_s, max_bounces, tx_num_rays,
-                   grid, rx_radius, device=device, shard_index=rank, shard_count=world)
+                   grid, rx_radius, device=device, shard_index=rank, shard_count=world,
+                   shard_mode=shard_mode if world > 1 else "cells")
     try:
         return cov.run(tx_pos, tx_power)
     finally:

@@ -28,6 +28,34 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
                  hipStream_t stream);
 int build_bvh(rt_mesh* m, const std::vector<float>& tri);      // bvh.hip (host, binned SAH)
 int build_bvh_gpu(rt_mesh* m, const std::vector<float>& tri);  // bvh_gpu.hip (device LBVH)
+
+__global__ void k_pack_leaf_refs(float4* nodes, const int2* leaves, int64_t nnodes) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nnodes; i += (int64_t)gridDim.x * blockDim.x) {
+    float4 q3 = nodes[4 * i + 3];
+    const int c0 = __float_as_int(q3.x), c1 = __float_as_int(q3.y);
+    if (c0 < 0) {
+      const int2 l = leaves[-1 - c0];
+      q3.z = __int_as_float(l.x << 3 | l.y);
+    }
+    if (c1 < 0) {
+      const int2 l = leaves[-1 - c1];
+      q3.w = __int_as_float(l.x << 3 | l.y);
+    }
+    nodes[4 * i + 3] = q3;
+  }
+}
+
+int pack_leaf_refs(rt_mesh* m) {
+  if (m->nf >= ((int64_t)1 << 28) || m->bvh_max_leaf > 4) {
+    set_error("rt_mesh_create: BVH leaves must hold <= 4 faces of a mesh below 2^28 faces");
+    return RT_EINVAL;
+  }
+  hipLaunchKernelGGL(k_pack_leaf_refs, dim3((unsigned)std::min<int64_t>((m->nnodes + 255) / 256, 8192)), dim3(256), 0,
+                     0, (float4*)m->nodes, (const int2*)m->leaves, m->nnodes);
+  RT_HIP(hipGetLastError());
+  RT_HIP(hipDeviceSynchronize());
+  return RT_OK;
+}
 }  // namespace rt
 
 extern "C" {
@@ -135,6 +163,7 @@ int rt_mesh_create_ex(int device, const float* vertices, int64_t nv, const int32
     int rc = 1;
     if (flags & RT_MESH_BVH_GPU) rc = rt::build_bvh_gpu(m, tri);  // 1: too deep for the stack
     if (rc == 1) rc = rt::build_bvh(m, tri);
+    if (!rc) rc = rt::pack_leaf_refs(m);
     if (rc) {
       rt_mesh_destroy(m);
       return rc;
@@ -276,7 +305,7 @@ int rt_query(const rt_mesh* m, const float* o, const float* d, int64_t n, float*
   }
   if (n == 0) return RT_OK;
   if (m->nodes) {
-    rt::BvhView bv{(const float4*)m->nodes, (const int2*)m->leaves, (const float4*)m->lcomp};
+    const rt::BvhView bv = rt::bvh_view(m);
     hipLaunchKernelGGL(k_query_bvh, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, bv, o, d, n,
                        t, face);
   } else {

@@ -72,6 +72,9 @@ struct CovParams {
   double c64, fs64;
   int flags;
   int64_t n_bins;
+  // ray-sharded runs: the owning rank of the record's cell ((cell % nx) % own_world) goes above
+  // the (cell, bin) key at bit own_shift, so one sort groups the records by destination
+  int own_world, own_shift;
 };
 __device__ __forceinline__ float4 traj_p(const CovParams& p, int64_t r, int k) { return p.traj[2 * (r * p.B + k)]; }
 __device__ __forceinline__ float4 traj_d(const CovParams& p, int64_t r, int k) { return p.traj[2 * (r * p.B + k) + 1]; }
@@ -639,7 +642,9 @@ __global__ __launch_bounds__(256) void k_replay(CovParams p, const uint64_t* key
     // amplitudes are >= 0; a zero one (NaN angle -> _bounce_amplitude 0, tracer.py:35-37) leaves
     // impulse_response[bin] untouched, so it must not become an active bin of the power sweep
     const bool keep = bin < p.n_bins && rec_amp != 0.0;
-    out_key[li] = keep ? ((uint64_t)cell << 32) | (uint64_t)bin : ~0ull;
+    uint64_t okey = ((uint64_t)cell << 32) | (uint64_t)bin;
+    if (p.own_world > 1) okey |= (uint64_t)((cell % p.g.nx) % p.own_world) << p.own_shift;
+    out_key[li] = keep ? okey : ~0ull;
     out_amp[li] = keep ? rec_amp : 0.0;
   }
 }
@@ -1052,6 +1057,8 @@ struct rt_coverage {
   const rt_mesh* env = nullptr;
   int B = 0;
   int64_t n = 0, ray_offset = 0;
+  int64_t n_total = 0;     // rays per cell of the whole burst (amplitude tx_power / n_total)
+  bool ray_mode = false;   // ray-sharded: candidates for every cell, records grouped by owner
   rt_grid grid{};
   double r_rx = 0.1;
   int shard = 0, nshard = 1;
@@ -1076,6 +1083,8 @@ struct rt_coverage {
   int64_t cap = 0;
   int64_t last_candidates = 0;
   int64_t last_received = 0;  // first-win (cell, ray) records of the last run
+  int64_t* bounds = nullptr;   // ray mode: [world + 1] starts of each owner's run in the reduced records
+  int64_t n_out = 0;           // ray mode: valid reduced records of the last rt_coverage_trace_records
 };
 
 namespace {
@@ -1141,83 +1150,40 @@ int bits_for(uint64_t v) {
   while (b < 64 && (v >> b) != 0) ++b;
   return b;
 }
-}  // namespace
 
-extern "C" {
+int64_t cov_ncell(const rt_coverage* c) { return c->grid.nx * c->grid.ny * c->grid.nz; }
+int own_shift(const rt_coverage* c) { return 32 + bits_for((uint64_t)cov_ncell(c)); }
 
-int rt_coverage_create(int device, const rt_mesh* env, int max_bounces, int64_t n_rays, int64_t ray_offset,
-                       const rt_grid* grid, double rx_radius, int shard_index, int shard_count, rt_coverage** out) {
-  if (!out || !env || !grid || max_bounces < 1 || max_bounces > 15 || n_rays <= 0 || n_rays > (1 << 24) ||
-      shard_count < 1 || shard_index < 0 || shard_index >= shard_count || grid->nx < 1 || grid->ny < 1 || grid->nz < 1 ||
-      rx_radius <= 0) {
-    rt::set_error("rt_coverage_create: invalid arguments (max_bounces 1..15, n_rays 1..2^24 per call)");
-    return RT_EINVAL;
+// reduced ray-mode records are sorted by (owner, cell, bin): bounds[o] = first record of owner o,
+// bounds[world] = the valid records (the dropped ~0 keys sort last)
+__global__ __launch_bounds__(256) void k_owner_bounds(const uint64_t* ukeys, const int64_t* nuniq, int world,
+                                                      int shift, int64_t* bounds) {
+  const int64_t nu = *nuniq;
+  auto owner = [&](int64_t u) -> int64_t {
+    const uint64_t k = ukeys[u];
+    return k == ~0ull ? (int64_t)world : (int64_t)(k >> shift);
+  };
+  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u <= nu; u += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t lo = u == 0 ? -1 : owner(u - 1), hi = u == nu ? (int64_t)world : owner(u);
+    for (int64_t o = lo + 1; o <= hi; ++o) bounds[o] = u;  // owners lo+1 .. hi start at u
   }
-  const int64_t nc = grid->nx * grid->ny * grid->nz;
-  if (bits_for((uint64_t)nc) > 32) {
-    rt::set_error("rt_coverage_create: too many cells");
-    return RT_EINVAL;
-  }
-  RT_HIP(hipSetDevice(device));
-  int rc = RT_OK;
-  rt_coverage* c = new rt_coverage();
-  c->device = device;
-  c->env = env;
-  c->B = max_bounces;
-  c->n = n_rays;
-  c->ray_offset = ray_offset;
-  c->grid = *grid;
-  c->r_rx = rx_radius;
-  c->shard = shard_index;
-  c->nshard = shard_count;
-  hipError_t e = hipMalloc(&c->traj, sizeof(float4) * 2 * max_bounces * n_rays);
-  if (e == hipSuccess) e = hipMalloc(&c->nseg, n_rays);
-  if (e == hipSuccess) e = hipMalloc(&c->counters, 32);
-  if (e == hipSuccess) e = hipMalloc(&c->nuniq, 8);
-  if (e == hipSuccess) e = hipMalloc(&c->cstart, sizeof(int32_t) * nc);
-  if (e == hipSuccess) e = hipMalloc(&c->cend, sizeof(int32_t) * nc);
-  if (e != hipSuccess) {
-    rt_coverage_destroy(c);
-    return rt::hip_fail(e, "rt_coverage_create");
-  }
-  rc = alloc_cands(c, std::max<int64_t>(1 << 20, 8 * n_rays));
-  if (!rc) rc = alloc_items(c, std::max<int64_t>(1 << 20, 8 * n_rays));
-  if (rc) {
-    rt_coverage_destroy(c);
-    return rc;
-  }
-  *out = c;
-  return RT_OK;
 }
 
-int rt_coverage_destroy(rt_coverage* c) {
-  if (!c) return RT_OK;
-  (void)hipSetDevice(c->device);
-  free_cands(c);
-  if (c->traj) (void)hipFree(c->traj);
-  if (c->nseg) (void)hipFree(c->nseg);
-  if (c->counters) (void)hipFree(c->counters);
-  if (c->nuniq) (void)hipFree(c->nuniq);
-  if (c->cstart) (void)hipFree(c->cstart);
-  if (c->cend) (void)hipFree(c->cend);
-  if (c->items) (void)hipFree(c->items);
-  delete c;
-  return RT_OK;
+__global__ __launch_bounds__(256) void k_strip_owner(const uint64_t* ukeys, int64_t n, int shift, uint64_t* out) {
+  const uint64_t mask = (1ull << shift) - 1;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = ukeys[i] & mask;
 }
 
-int rt_coverage_run(rt_coverage* c, const float* tx_pos, double tx_power, double light_speed, double sample_rate,
-                    int flags, int64_t n_bins, double alpha, double* power, int64_t* stats, void* stream) {
-  if (!c || !tx_pos || !power || n_bins < 1 || n_bins >= ((int64_t)1 << 32)) {
-    rt::set_error("rt_coverage_run: invalid arguments");
-    return RT_EINVAL;
-  }
-  hipStream_t s = (hipStream_t)stream;
-  RT_HIP(hipSetDevice(c->device));
+// Stages 1-4 (trajectories, candidates, exact receiver tests, replay): the first-win records of
+// this plan's rays as (key, amplitude) in c->okeys / c->oamps, in (cell, ray, k) order.
+int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double light_speed, double sample_rate,
+                int flags, int64_t n_bins, hipStream_t s, int64_t* ncand_out, int64_t* nlist_out) {
   CovParams p{};
   p.env_perm = c->env->perm;
   p.env_nrm = c->env->nrm;
   p.env_nf = (int)c->env->nf;
-  p.env_bvh = rt::BvhView{(const float4*)c->env->nodes, (const int2*)c->env->leaves, (const float4*)c->env->lcomp};
+  p.env_bvh = rt::bvh_view(c->env);
   const bool bvh = c->env->nodes != nullptr;
   for (int k = 0; k < 3; ++k) p.tx[k] = tx_pos[k];
   p.B = c->B;
@@ -1232,13 +1198,17 @@ int rt_coverage_run(rt_coverage* c, const float* tx_pos, double tx_power, double
                                   fabs(c->grid.z0) + fabs(c->grid.dz) * (double)c->grid.nz));
     p.r_pad = c->r_rx * (1.0 + 1e-3) + 1e-5 * (1.0 + amax);
   }
-  p.shard = c->shard;
-  p.nshard = c->nshard;
+  // cell-sharded plans skip other ranks' columns from the candidate passes on; ray-sharded plans
+  // find candidates in every cell and tag each record with its cell's owner instead
+  p.shard = c->ray_mode ? 0 : c->shard;
+  p.nshard = c->ray_mode ? 1 : c->nshard;
+  p.own_world = c->ray_mode ? c->nshard : 1;
+  p.own_shift = own_shift(c);
   p.traj = c->traj;
   p.nseg = c->nseg;
   p.count = c->counters;
   p.item_count = c->counters + 1;
-  p.amp0 = tx_power / (double)c->n;
+  p.amp0 = tx_power / (double)(c->n_total > 0 ? c->n_total : c->n);
   p.c32 = (float)light_speed;
   p.fs32 = (float)sample_rate;
   p.c64 = light_speed;
@@ -1294,41 +1264,21 @@ int rt_coverage_run(rt_coverage* c, const float* tx_pos, double tx_power, double
     return RT_EINVAL;
   }
   c->last_candidates = ncand;
-  const int64_t ncell = c->grid.nx * c->grid.ny * c->grid.nz;
-  PowerParams P;
-  P.n_bins = n_bins;
-  P.half = (n_bins - 1) / 2;
-  P.alpha = alpha;
-  P.turns = alpha / 6.283185307179586;
-  P.sin_a = sin(alpha);
-  P.cos_a = cos(alpha);
-  // one wave per owned cell, 4 per block
-  const unsigned grid_cells = (unsigned)std::min<int64_t>((ncell / c->nshard + 4) / 4, 4096);
-  const unsigned grid_small = (unsigned)std::min<int64_t>((ncell / c->nshard + 256) / 256, 8192);
-  const TermArrays terms{c->ukeys, c->tcos, c->tsin, c->ev};
-  if (c->nshard > 1) RT_HIP(hipMemsetAsync(power, 0, ncell * sizeof(double), s));  // cells of other ranks
-  RT_HIP(hipMemsetAsync(c->cstart, 0, ncell * sizeof(int32_t), s));
-  RT_HIP(hipMemsetAsync(c->cend, 0, ncell * sizeof(int32_t), s));
-  if (ncand == 0) {
-    RT_HIP(hipMemsetAsync(c->nuniq, 0, 8, s));
-    hipLaunchKernelGGL(k_power_small, dim3(grid_small), dim3(256), 0, s, terms, c->cstart, c->cend, c->grid, c->shard,
-                       c->nshard, P, power);
-    RT_HIP(hipGetLastError());
-    if (stats) stats[0] = stats[1] = 0;
-    return RT_OK;
-  }
-  const int endbit = 28 + bits_for((uint64_t)ncell);
-  size_t tb = c->tmp_bytes;
-  RT_HIP(hipcub::DeviceRadixSort::SortKeys(c->tmp, tb, c->keys, c->keys_sorted, (int)ncand, 0, endbit, s));
-  const unsigned grid_c = (unsigned)std::min<int64_t>((ncand + 255) / 256, 8192);
-  hipLaunchKernelGGL(k_win, dim3(grid_c), dim3(256), 0, s, p, c->keys_sorted, ncand, c->win, c->trx);
-  hipLaunchKernelGGL(k_first, dim3(grid_c), dim3(256), 0, s, c->keys_sorted, ncand, c->win, c->first_flag);
-  tb = c->tmp_bytes;
-  RT_HIP(hipcub::DeviceSelect::Flagged(c->tmp, tb, hipcub::CountingInputIterator<int64_t>(0), c->first_flag, c->list,
-                                       (int64_t*)(c->counters + 2), (int)ncand, s));
+  *ncand_out = ncand;
   int64_t nlist = 0;
-  RT_HIP(hipMemcpyAsync(&nlist, c->counters + 2, 8, hipMemcpyDeviceToHost, s));
-  RT_HIP(hipStreamSynchronize(s));
+  if (ncand > 0) {
+    const int endbit = 28 + bits_for((uint64_t)cov_ncell(c));
+    size_t tb = c->tmp_bytes;
+    RT_HIP(hipcub::DeviceRadixSort::SortKeys(c->tmp, tb, c->keys, c->keys_sorted, (int)ncand, 0, endbit, s));
+    const unsigned grid_c = (unsigned)std::min<int64_t>((ncand + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_win, dim3(grid_c), dim3(256), 0, s, p, c->keys_sorted, ncand, c->win, c->trx);
+    hipLaunchKernelGGL(k_first, dim3(grid_c), dim3(256), 0, s, c->keys_sorted, ncand, c->win, c->first_flag);
+    tb = c->tmp_bytes;
+    RT_HIP(hipcub::DeviceSelect::Flagged(c->tmp, tb, hipcub::CountingInputIterator<int64_t>(0), c->first_flag,
+                                         c->list, (int64_t*)(c->counters + 2), (int)ncand, s));
+    RT_HIP(hipMemcpyAsync(&nlist, c->counters + 2, 8, hipMemcpyDeviceToHost, s));
+    RT_HIP(hipStreamSynchronize(s));
+  }
   if (nlist > 0) {
     const unsigned grid_l = (unsigned)std::min<int64_t>((nlist + 255) / 256, 8192);
     if (bvh) {
@@ -1354,28 +1304,148 @@ int rt_coverage_run(rt_coverage* c, const float* tx_pos, double tx_power, double
                          (const int32_t*)nullptr, c->okeys, c->oamps);
     }
     RT_HIP(hipGetLastError());
-    // records are in (cell, ray, k) order; a stable sort on (cell, bin) keeps that order within a
-    // bin, so every bin's amplitudes are summed in ray order.  Dropped records (~0) sort last.
-    const int kbits = 32 + bits_for((uint64_t)ncell);
-    tb = c->tmp_bytes;
-    RT_HIP(hipcub::DeviceRadixSort::SortPairs(c->tmp, tb, c->okeys, c->okeys_sorted, c->oamps, c->oamps_sorted,
-                                              (int)nlist, 0, kbits < 64 ? kbits : 64, s));
-    tb = c->tmp_bytes;
-    RT_HIP(hipcub::DeviceReduce::ReduceByKey(c->tmp, tb, c->okeys_sorted, c->ukeys, c->oamps_sorted, c->uamps,
-                                             c->nuniq, hipcub::Sum(), (int)nlist, s));
-    const unsigned grid_u = (unsigned)std::min<int64_t>((nlist + 255) / 256, 8192);
+  }
+  c->last_received = nlist;
+  *nlist_out = nlist;
+  return RT_OK;
+}
+
+// Stable radix sort of n records on their low kbits key bits, then the sum of every run of equal
+// keys (records of one bin arrive in ray order, so they are summed in ray order): c->ukeys /
+// c->uamps, count in c->nuniq.  keys/amps may be caller buffers (records from other ranks).
+int cov_reduce(rt_coverage* c, const uint64_t* keys, const double* amps, int64_t n, int kbits, hipStream_t s) {
+  if (n > c->cap) {  // records gathered from several ranks can outgrow this rank's candidate buffers
+    int rc = alloc_cands(c, n + n / 4 + 1024);
+    if (rc) return rc;
+  }
+  size_t tb = c->tmp_bytes;
+  RT_HIP(hipcub::DeviceRadixSort::SortPairs(c->tmp, tb, keys, c->okeys_sorted, amps, c->oamps_sorted, (int)n, 0,
+                                            kbits < 64 ? kbits : 64, s));
+  tb = c->tmp_bytes;
+  RT_HIP(hipcub::DeviceReduce::ReduceByKey(c->tmp, tb, c->okeys_sorted, c->ukeys, c->oamps_sorted, c->uamps, c->nuniq,
+                                           hipcub::Sum(), (int)n, s));
+  return RT_OK;
+}
+
+// Closed-form signal power of this plan's cells from the reduced records in c->ukeys / c->uamps
+// (nrec: host upper bound of their count); other ranks' cells are zero-filled.
+int cov_power(rt_coverage* c, int64_t nrec, int64_t n_bins, double alpha, double* power, hipStream_t s) {
+  const int64_t ncell = cov_ncell(c);
+  PowerParams P;
+  P.n_bins = n_bins;
+  P.half = (n_bins - 1) / 2;
+  P.alpha = alpha;
+  P.turns = alpha / 6.283185307179586;
+  P.sin_a = sin(alpha);
+  P.cos_a = cos(alpha);
+  // one wave per owned cell, 4 per block
+  const unsigned grid_cells = (unsigned)std::min<int64_t>((ncell / c->nshard + 4) / 4, 4096);
+  const unsigned grid_small = (unsigned)std::min<int64_t>((ncell / c->nshard + 256) / 256, 8192);
+  const TermArrays terms{c->ukeys, c->tcos, c->tsin, c->ev};
+  if (c->nshard > 1) RT_HIP(hipMemsetAsync(power, 0, ncell * sizeof(double), s));  // cells of other ranks
+  RT_HIP(hipMemsetAsync(c->cstart, 0, ncell * sizeof(int32_t), s));
+  RT_HIP(hipMemsetAsync(c->cend, 0, ncell * sizeof(int32_t), s));
+  if (nrec > 0) {
+    const unsigned grid_u = (unsigned)std::min<int64_t>((nrec + 255) / 256, 8192);
     hipLaunchKernelGGL(k_terms, dim3(grid_u), dim3(256), 0, s, c->ukeys, c->uamps, c->nuniq, P, c->tcos, c->tsin, c->ev);
+    hipLaunchKernelGGL(k_cell_ranges, dim3(grid_u), dim3(256), 0, s, c->ukeys, c->nuniq, ncell, c->cstart, c->cend);
+  }
+  hipLaunchKernelGGL(k_power_small, dim3(grid_small), dim3(256), 0, s, terms, c->cstart, c->cend, c->grid, c->shard,
+                     c->nshard, P, power);
+  if (nrec > 0)
+    hipLaunchKernelGGL(k_power, dim3(grid_cells), dim3(256), 0, s, terms, c->cstart, c->cend, c->grid, c->shard,
+                       c->nshard, P, power);
+  RT_HIP(hipGetLastError());
+  return RT_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int rt_coverage_create(int device, const rt_mesh* env, int max_bounces, int64_t n_rays, int64_t ray_offset,
+                       const rt_grid* grid, double rx_radius, int shard_index, int shard_count, rt_coverage** out) {
+  if (!out || !env || !grid || max_bounces < 1 || max_bounces > 15 || n_rays <= 0 || n_rays > (1 << 24) ||
+      shard_count < 1 || shard_index < 0 || shard_index >= shard_count || grid->nx < 1 || grid->ny < 1 || grid->nz < 1 ||
+      rx_radius <= 0) {
+    rt::set_error("rt_coverage_create: invalid arguments (max_bounces 1..15, n_rays 1..2^24 per call)");
+    return RT_EINVAL;
+  }
+  const int64_t nc = grid->nx * grid->ny * grid->nz;
+  if (bits_for((uint64_t)nc) > 32) {
+    rt::set_error("rt_coverage_create: too many cells");
+    return RT_EINVAL;
+  }
+  RT_HIP(hipSetDevice(device));
+  int rc = RT_OK;
+  rt_coverage* c = new rt_coverage();
+  c->device = device;
+  c->env = env;
+  c->B = max_bounces;
+  c->n = n_rays;
+  c->ray_offset = ray_offset;
+  c->grid = *grid;
+  c->r_rx = rx_radius;
+  c->shard = shard_index;
+  c->nshard = shard_count;
+  hipError_t e = hipMalloc(&c->traj, sizeof(float4) * 2 * max_bounces * n_rays);
+  if (e == hipSuccess) e = hipMalloc(&c->nseg, n_rays);
+  if (e == hipSuccess) e = hipMalloc(&c->counters, 32);
+  if (e == hipSuccess) e = hipMalloc(&c->nuniq, 8);
+  if (e == hipSuccess) e = hipMemset(c->nuniq, 0, 8);  // rt_coverage_received before any run: nothing
+  if (e == hipSuccess) e = hipMalloc(&c->cstart, sizeof(int32_t) * nc);
+  if (e == hipSuccess) e = hipMalloc(&c->cend, sizeof(int32_t) * nc);
+  if (e != hipSuccess) {
+    rt_coverage_destroy(c);
+    return rt::hip_fail(e, "rt_coverage_create");
+  }
+  rc = alloc_cands(c, std::max<int64_t>(1 << 20, 8 * n_rays));
+  if (!rc) rc = alloc_items(c, std::max<int64_t>(1 << 20, 8 * n_rays));
+  if (rc) {
+    rt_coverage_destroy(c);
+    return rc;
+  }
+  *out = c;
+  return RT_OK;
+}
+
+int rt_coverage_destroy(rt_coverage* c) {
+  if (!c) return RT_OK;
+  (void)hipSetDevice(c->device);
+  free_cands(c);
+  if (c->traj) (void)hipFree(c->traj);
+  if (c->nseg) (void)hipFree(c->nseg);
+  if (c->counters) (void)hipFree(c->counters);
+  if (c->nuniq) (void)hipFree(c->nuniq);
+  if (c->cstart) (void)hipFree(c->cstart);
+  if (c->cend) (void)hipFree(c->cend);
+  if (c->items) (void)hipFree(c->items);
+  if (c->bounds) (void)hipFree(c->bounds);
+  delete c;
+  return RT_OK;
+}
+
+int rt_coverage_run(rt_coverage* c, const float* tx_pos, double tx_power, double light_speed, double sample_rate,
+                    int flags, int64_t n_bins, double alpha, double* power, int64_t* stats, void* stream) {
+  if (!c || !tx_pos || !power || n_bins < 1 || n_bins >= ((int64_t)1 << 32) || c->ray_mode) {
+    rt::set_error(c && c->ray_mode ? "rt_coverage_run: a ray-sharded plan runs through rt_coverage_trace_records"
+                                   : "rt_coverage_run: invalid arguments");
+    return RT_EINVAL;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  RT_HIP(hipSetDevice(c->device));
+  int64_t ncand = 0, nlist = 0;
+  int rc = cov_records(c, tx_pos, tx_power, light_speed, sample_rate, flags, n_bins, s, &ncand, &nlist);
+  if (rc) return rc;
+  // records are in (cell, ray, k) order; a stable sort on (cell, bin) keeps that order within a
+  // bin, so every bin's amplitudes are summed in ray order.  Dropped records (~0) sort last.
+  if (nlist > 0) {
+    rc = cov_reduce(c, c->okeys, c->oamps, nlist, 32 + bits_for((uint64_t)cov_ncell(c)), s);
+    if (rc) return rc;
   } else {
     RT_HIP(hipMemsetAsync(c->nuniq, 0, 8, s));
   }
-  hipLaunchKernelGGL(k_cell_ranges, dim3((unsigned)std::min<int64_t>((nlist + 255) / 256 + 1, 8192)), dim3(256), 0, s,
-                     c->ukeys, c->nuniq, ncell, c->cstart, c->cend);
-  hipLaunchKernelGGL(k_power_small, dim3(grid_small), dim3(256), 0, s, terms, c->cstart, c->cend, c->grid, c->shard,
-                     c->nshard, P, power);
-  hipLaunchKernelGGL(k_power, dim3(grid_cells), dim3(256), 0, s, terms, c->cstart, c->cend, c->grid, c->shard,
-                     c->nshard, P, power);
-  RT_HIP(hipGetLastError());
-  c->last_received = nlist;
+  rc = cov_power(c, nlist, n_bins, alpha, power, s);
+  if (rc) return rc;
   if (stats) {
     stats[0] = ncand;
     stats[1] = nlist;
@@ -1383,9 +1453,103 @@ int rt_coverage_run(rt_coverage* c, const float* tx_pos, double tx_power, double
   return RT_OK;
 }
 
+int rt_coverage_create_rays(int device, const rt_mesh* env, int max_bounces, int64_t n_rays_total, int64_t ray_offset,
+                            int64_t n_rays, const rt_grid* grid, double rx_radius, int rank, int world,
+                            rt_coverage** out) {
+  if (!out || world < 1 || rank < 0 || rank >= world || n_rays_total < 1 || ray_offset < 0 ||
+      ray_offset + n_rays > n_rays_total || !grid || grid->nx < 1 || grid->ny < 1 || grid->nz < 1) {
+    rt::set_error("rt_coverage_create_rays: invalid arguments (0 <= rank < world, ray range inside the burst)");
+    return RT_EINVAL;
+  }
+  const uint64_t nc = (uint64_t)(grid->nx * grid->ny * grid->nz);
+  if (32 + bits_for(nc) + bits_for((uint64_t)(world - 1)) > 63) {
+    rt::set_error("rt_coverage_create_rays: cells x ranks exceed the 63-bit record key");
+    return RT_EINVAL;
+  }
+  rt_coverage* c = nullptr;
+  int rc = rt_coverage_create(device, env, max_bounces, n_rays, ray_offset, grid, rx_radius, rank, world, &c);
+  if (rc) return rc;
+  c->n_total = n_rays_total;
+  c->ray_mode = true;
+  if (hipMalloc(&c->bounds, sizeof(int64_t) * (world + 1)) != hipSuccess) {
+    rt_coverage_destroy(c);
+    return rt::hip_fail(hipErrorOutOfMemory, "rt_coverage_create_rays");
+  }
+  *out = c;
+  return RT_OK;
+}
+
+int rt_coverage_trace_records(rt_coverage* c, const float* tx_pos, double tx_power, double light_speed,
+                              double sample_rate, int flags, int64_t n_bins, int64_t* counts, int64_t* stats,
+                              void* stream) {
+  if (!c || !c->ray_mode || !tx_pos || !counts || n_bins < 1 || n_bins >= ((int64_t)1 << 32)) {
+    rt::set_error("rt_coverage_trace_records: invalid arguments (needs a plan from rt_coverage_create_rays)");
+    return RT_EINVAL;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  RT_HIP(hipSetDevice(c->device));
+  const int world = c->nshard;
+  int64_t ncand = 0, nlist = 0;
+  int rc = cov_records(c, tx_pos, tx_power, light_speed, sample_rate, flags, n_bins, s, &ncand, &nlist);
+  if (rc) return rc;
+  // local sum per (owner, cell, bin), in ray order; runs of each owner are then contiguous
+  std::vector<int64_t> b(world + 1, 0);
+  if (nlist > 0) {
+    rc = cov_reduce(c, c->okeys, c->oamps, nlist, own_shift(c) + bits_for((uint64_t)(world - 1)), s);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_owner_bounds, dim3((unsigned)std::min<int64_t>((nlist + 255) / 256, 4096)), dim3(256), 0, s,
+                       c->ukeys, c->nuniq, world, own_shift(c), c->bounds);
+    RT_HIP(hipGetLastError());
+    RT_HIP(hipMemcpyAsync(b.data(), c->bounds, sizeof(int64_t) * (world + 1), hipMemcpyDeviceToHost, s));
+    RT_HIP(hipStreamSynchronize(s));
+  }
+  for (int o = 0; o < world; ++o) counts[o] = b[o + 1] - b[o];
+  c->n_out = b[world];
+  if (stats) {
+    stats[0] = ncand;
+    stats[1] = nlist;
+  }
+  return RT_OK;
+}
+
+int rt_coverage_records(rt_coverage* c, uint64_t* keys_out, double* amps_out, int64_t max_out, void* stream) {
+  if (!c || !c->ray_mode || (c->n_out > 0 && (!keys_out || !amps_out)) || max_out < c->n_out) {
+    rt::set_error("rt_coverage_records: invalid arguments (max_out must hold the sum of the counts)");
+    return RT_EINVAL;
+  }
+  if (c->n_out == 0) return RT_OK;
+  hipStream_t s = (hipStream_t)stream;
+  RT_HIP(hipSetDevice(c->device));
+  hipLaunchKernelGGL(k_strip_owner, dim3((unsigned)std::min<int64_t>((c->n_out + 255) / 256, 4096)), dim3(256), 0, s,
+                     c->ukeys, c->n_out, own_shift(c), keys_out);
+  RT_HIP(hipGetLastError());
+  RT_HIP(hipMemcpyAsync(amps_out, c->uamps, sizeof(double) * c->n_out, hipMemcpyDeviceToDevice, s));
+  return RT_OK;
+}
+
+int rt_coverage_power_records(rt_coverage* c, const uint64_t* keys, const double* amps, int64_t n, int64_t n_bins,
+                              double alpha, double* power, void* stream) {
+  if (!c || !c->ray_mode || n < 0 || (n > 0 && (!keys || !amps)) || !power || n_bins < 1 ||
+      n_bins >= ((int64_t)1 << 32) || n > ((int64_t)1 << 31) - 1) {
+    rt::set_error("rt_coverage_power_records: invalid arguments");
+    return RT_EINVAL;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  RT_HIP(hipSetDevice(c->device));
+  int rc = RT_OK;
+  if (n > 0) {
+    rc = cov_reduce(c, keys, amps, n, 32 + bits_for((uint64_t)cov_ncell(c)), s);
+  } else {
+    RT_HIP(hipMemsetAsync(c->nuniq, 0, 8, s));
+  }
+  if (!rc) rc = cov_power(c, n, n_bins, alpha, power, s);
+  return rc;
+}
+
 int rt_coverage_received(rt_coverage* c, uint64_t* keys_out, double* amps_out, int64_t max_out, int64_t* n_out,
                          void* stream) {
-  // the per-cell sparse impulse responses of the last run: (cell << 32 | bin, amplitude), ascending
+  // the per-cell sparse impulse responses of the last run (rt_coverage_run, or this rank's cells
+  // after rt_coverage_power_records): (cell << 32 | bin, amplitude), ascending
   if (!c || !n_out) {
     rt::set_error("rt_coverage_received: invalid arguments");
     return RT_EINVAL;
@@ -1394,7 +1558,12 @@ int rt_coverage_received(rt_coverage* c, uint64_t* keys_out, double* amps_out, i
   int64_t nu = 0;
   RT_HIP(hipMemcpyAsync(&nu, c->nuniq, 8, hipMemcpyDeviceToHost, s));
   RT_HIP(hipStreamSynchronize(s));
-  if (c->last_candidates == 0) nu = 0;
+  if (nu > 0) {  // records dropped by the replay (bin past the window, zero amplitude) sort last as ~0
+    uint64_t last = 0;
+    RT_HIP(hipMemcpyAsync(&last, c->ukeys + nu - 1, 8, hipMemcpyDeviceToHost, s));
+    RT_HIP(hipStreamSynchronize(s));
+    if (last == ~0ull) --nu;
+  }
   *n_out = nu;
   const int64_t m = std::min(nu, max_out);
   if (m > 0 && keys_out) RT_HIP(hipMemcpyAsync(keys_out, c->ukeys, m * 8, hipMemcpyDeviceToDevice, s));

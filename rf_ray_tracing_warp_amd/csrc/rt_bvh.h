@@ -4,8 +4,10 @@
 // Layout (built on the host by bvh.hip, HBM-resident):
 //   nodes  float4[nnodes][4]: child boxes c0 = (lo.xyz, hi.xyz), c1 = ..., then child ids:
 //          q0 = (c0lo.x, c0lo.y, c0lo.z, c0hi.x)  q1 = (c0hi.y, c0hi.z, c1lo.x, c1lo.y)
-//          q2 = (c1lo.z, c1hi.x, c1hi.y, c1hi.z)  q3 = (child0, child1, -, -) as int bits
-//          child >= 0: internal node index;  child < 0: leaf -1-child into `leaves`
+//          q2 = (c1lo.z, c1hi.x, c1hi.y, c1hi.z)  q3 = (child0, child1, leaf0, leaf1) as int bits
+//          child >= 0: internal node index;  child < 0: leaf -1-child into `leaves`, whose
+//          (first, count) is also packed into leaf0/leaf1 as first << 3 | count (count <= 4) by
+//          rt::pack_leaf_refs after either builder, so traversal never loads `leaves`
 //   leaves int2[nleaves]: (first, count) into the leaf-ordered face table
 //   lcomp  float4[nf][3]: faces in leaf order, un-permuted: (a.xyz b.x)(b.yz c.xy)(c.z, original
 //          face id bits, -, -).  48 B per face, all of it used by every lane; the corners are
@@ -24,6 +26,7 @@ struct BvhView {
   const float4* nodes;
   const int2* leaves;
   const float4* lcomp;
+  int nf;  // faces in lcomp
 };
 
 #define RT_BVH_STACK 64
@@ -58,25 +61,45 @@ __device__ __forceinline__ float slab(const RayBox& r, float lx, float ly, float
   return tn <= tf * 1.00001f + 1e-6f ? tn : INFINITY;
 }
 
-__device__ __forceinline__ void leaf_faces(const BvhView& b, const Shear& s, int2 lf, Hit& h) {
-  for (int j = lf.x; j < lf.x + lf.y; ++j) {
+// leaf faces [first, first + count), count <= 4: the four 48-B records are fetched together
+// (indices clamped into the table, the results of q >= count ignored), so a leaf costs one
+// memory latency instead of one per face
+__device__ __forceinline__ void leaf4(const BvhView& b, const Shear& s, int first, int count, Hit& h) {
+  float4 A[4], M[4], C[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int j = min(first + q, b.nf - 1);
     const float4* p = b.lcomp + (int64_t)j * 3;
-    const float4 a = p[0], m = p[1], c = p[2];
-    // corners A = (a.x a.y a.z), B = (a.w m.x m.y), C = (m.z m.w c.x) -> (kx, ky, kz) order
-    const float4 q0 = make_float4(pick(a.x, a.y, a.z, s.kx), pick(a.x, a.y, a.z, s.ky), pick(a.x, a.y, a.z, s.kz),
-                                  pick(a.w, m.x, m.y, s.kx));
-    const float4 q1 = make_float4(pick(a.w, m.x, m.y, s.ky), pick(a.w, m.x, m.y, s.kz), pick(m.z, m.w, c.x, s.kx),
-                                  pick(m.z, m.w, c.x, s.ky));
-    const float c2 = pick(m.z, m.w, c.x, s.kz);
-    float T, det;
-    if (tri_test(s, q0, q1, c2, T, det)) hit_consider(h, T, det, __float_as_int(c.y));
+    A[q] = p[0];
+    M[q] = p[1];
+    C[q] = p[2];
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (q < count) {
+      const float4 a = A[q], m = M[q], c = C[q];
+      // corners A = (a.x a.y a.z), B = (a.w m.x m.y), C = (m.z m.w c.x) -> (kx, ky, kz) order
+      const float4 q0 = make_float4(pick(a.x, a.y, a.z, s.kx), pick(a.x, a.y, a.z, s.ky), pick(a.x, a.y, a.z, s.kz),
+                                    pick(a.w, m.x, m.y, s.kx));
+      const float4 q1 = make_float4(pick(a.w, m.x, m.y, s.ky), pick(a.w, m.x, m.y, s.kz), pick(m.z, m.w, c.x, s.kx),
+                                    pick(m.z, m.w, c.x, s.ky));
+      const float c2 = pick(m.z, m.w, c.x, s.kz);
+      float T, det;
+      if (tri_test(s, q0, q1, c2, T, det)) hit_consider(h, T, det, __float_as_int(c.y));
+    }
   }
 }
 
-// closest hit in a BVH mesh (same result as brute force over all faces): near child first,
-// far child on a per-lane (node, entry t) stack, popped entries re-culled against the best t.
+// closest hit in a BVH mesh (same result as brute force over all faces): near child first, far
+// child on a per-lane (node, entry t) stack, popped entries re-culled against the best t.
 // tcull < RT_MAX_T also culls boxes beyond tcull: every hit with t <= tcull is still found
 // exactly, hits beyond it may be missed (callers that only compare against tcull use it).
+//
+// One flat loop, one step per iteration for every lane: pop (re-culled) and visit happen in the
+// same step, leaves are tested on the spot from the (first, count) packed in their parent node,
+// so a wave iterates as often as its longest lane.  (The nested-loop form -- descend, inner
+// pop loop, inner face loop -- made lanes wait for each other at every phase change: the
+// slowest wave of a 125k-ray K5 burst took 2.2x longer.)
 __device__ __forceinline__ Hit bvh_query(const BvhView& b, const Shear& s, float3 o, float3 d,
                                          float tcull = RT_MAX_T) {
   Hit h;
@@ -85,56 +108,56 @@ __device__ __forceinline__ Hit bvh_query(const BvhView& b, const Shear& s, float
   const RayBox r = make_raybox(o, d);
   int stack[RT_BVH_STACK];
   float stackt[RT_BVH_STACK];
-  int sp = 0;
-  int cur = 0;
-  while (true) {
-    const float4 q0 = b.nodes[4 * cur + 0], q1 = b.nodes[4 * cur + 1];
-    const float4 q2 = b.nodes[4 * cur + 2], q3 = b.nodes[4 * cur + 3];
-    const int c0 = __float_as_int(q3.x), c1 = __float_as_int(q3.y);
-    float t0 = slab(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y);
-    float t1 = slab(r, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w);
-    // leaves are tested on the spot
+  int sp = 0, cur = 0;
+  bool active = true;
+  while (active) {
+    bool visit = true;
+    if (cur < 0) {  // pop
+      if (sp == 0) {
+        active = false;
+        visit = false;
+      } else {
+        --sp;
+        if (stackt[sp] <= fminf(h.t, tc) * 1.00001f + 1e-6f) cur = stack[sp];
+        else visit = false;
+      }
+    }
+    if (visit) {
+      const float4 q0 = b.nodes[4 * cur + 0], q1 = b.nodes[4 * cur + 1];
+      const float4 q2 = b.nodes[4 * cur + 2], q3 = b.nodes[4 * cur + 3];
+      const int c0 = __float_as_int(q3.x), c1 = __float_as_int(q3.y);
+      float t0 = slab(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y);
+      float t1 = slab(r, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w);
 #pragma unroll
-    for (int side = 0; side < 2; ++side) {
-      const int c = side ? c1 : c0;
-      float& tt = side ? t1 : t0;
-      if (c < 0 && tt <= fminf(h.t, tc) * 1.00001f + 1e-6f) {
-        leaf_faces(b, s, b.leaves[-1 - c], h);
-        tt = INFINITY;
-      } else if (c < 0) {
-        tt = INFINITY;
+      for (int side = 0; side < 2; ++side) {
+        const int c = side ? c1 : c0;
+        float& tt = side ? t1 : t0;
+        if (c < 0) {  // leaf child: test its faces now
+          if (tt <= fminf(h.t, tc) * 1.00001f + 1e-6f) {
+            const int pk = __float_as_int(side ? q3.w : q3.z);
+            leaf4(b, s, pk >> 3, pk & 7, h);
+          }
+          tt = INFINITY;
+        }
+      }
+      const float lim = fminf(h.t, tc) * 1.00001f + 1e-6f;
+      const bool h0 = t0 <= lim, h1 = t1 <= lim;
+      if (h0 && h1) {
+        const bool first0 = t0 <= t1;
+        if (sp < RT_BVH_STACK) {  // cannot overflow: tree depth <= RT_BVH_STACK - 4 (bvh.hip)
+          stack[sp] = first0 ? c1 : c0;
+          stackt[sp] = first0 ? t1 : t0;
+          ++sp;
+        }
+        cur = first0 ? c0 : c1;
+      } else if (h0) {
+        cur = c0;
+      } else if (h1) {
+        cur = c1;
+      } else {
+        cur = -1;
       }
     }
-    const float lim = fminf(h.t, tc) * 1.00001f + 1e-6f;
-    const bool h0 = t0 <= lim, h1 = t1 <= lim;
-    if (h0 && h1) {
-      const bool first0 = t0 <= t1;
-      if (sp < RT_BVH_STACK) {  // cannot overflow: tree depth <= RT_BVH_STACK - 4 (bvh.hip)
-        stack[sp] = first0 ? c1 : c0;
-        stackt[sp] = first0 ? t1 : t0;
-        ++sp;
-      }
-      cur = first0 ? c0 : c1;
-      continue;
-    }
-    if (h0) {
-      cur = c0;
-      continue;
-    }
-    if (h1) {
-      cur = c1;
-      continue;
-    }
-    bool found = false;
-    while (sp > 0) {
-      --sp;
-      if (stackt[sp] <= fminf(h.t, tc) * 1.00001f + 1e-6f) {
-        cur = stack[sp];
-        found = true;
-        break;
-      }
-    }
-    if (!found) break;
   }
   return h;
 }

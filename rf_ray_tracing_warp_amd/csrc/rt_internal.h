@@ -5,6 +5,8 @@
 
 #include <string>
 
+#include "rt_bvh.h"
+
 // Device-resident triangle mesh (the object wp.Mesh is in the reference, tracer.py:24,30).
 //
 // HBM layout (all float4, 16-byte aligned):
@@ -36,6 +38,13 @@ int hip_fail(hipError_t e, const char* what);
 // Row order for tracing rays [ray_offset, ray_offset+n) of one burst sorted by initial direction
 // (trace.hip).  Stream-ordered workspace returned in *ws (hipFreeAsync it after the consumer).
 const int32_t* dir_order(int64_t ray_offset, int64_t n, hipStream_t stream, void** ws);
+// Device view of a mesh's BVH for rt::bvh_query
+inline BvhView bvh_view(const rt_mesh* m) {
+  return BvhView{(const float4*)m->nodes, (const int2*)m->leaves, (const float4*)m->lcomp, (int)m->nf};
+}
+// After either builder: copy each leaf child's (first, count) into its parent node (q3.z/q3.w,
+// first << 3 | count), the form bvh_query reads (api.hip)
+int pack_leaf_refs(rt_mesh* m);
 }  // namespace rt
 
 #define RT_HIP(call)                                                   \

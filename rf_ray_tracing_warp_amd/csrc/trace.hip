@@ -335,7 +335,7 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
   a.env_perm = env->perm;
   a.env_nrm = env->nrm;
   a.env_nf = (int)env->nf;
-  a.env_bvh = rt::BvhView{(const float4*)env->nodes, (const int2*)env->leaves, (const float4*)env->lcomp};
+  a.env_bvh = rt::bvh_view(env);
   const bool bvh = env->nodes != nullptr;
   a.rx_perm = rx ? rx->perm : nullptr;
   a.rx_nf = rx ? (int)rx->nf : 0;

@@ -1,6 +1,6 @@
 """Multi-GPU plumbing: one process per GPU, torch.distributed ("nccl" = RCCL over xGMI on ROCm).
 
-Two decompositions:
+Decompositions:
 * rays  -- rank r traces global ray ids [r*n, (r+1)*n) (Warp tid = global id, kernel.py:48-51, so
   every ray's path is independent of the shard); the impulse response is the sum over shards,
   amplitude tx_power / (n * world) per ray (tracer.py:103): ``reduce_sum``.
@@ -8,6 +8,10 @@ Two decompositions:
   rank (x-column cyclic: a strip of constant ix is wholly one rank's, so the candidate passes
   shrink with the rank count); every other rank leaves 0 in its power map and the maps are
   sum-reduced: ``reduce_sum`` again (NaN of an owner survives).
+* coverage rays -- rank r traces its share of every cell's rays (``ray_range``), sums its
+  first-win records per (cell, bin) and sends each record to the owner of its cell (the x-column
+  rule above): ``exchange_records``, one sparse all-to-all.  Owners sum what they receive, in
+  source-rank (= ray) order, compute their cells' power, and the maps are sum-reduced.
 """
 from __future__ import annotations
 
@@ -22,6 +26,12 @@ def rank_world(group=None):
 def ray_shard(rank: int, world: int, rays_per_rank: int):
     """(ray_offset, count) of this rank's global ray ids."""
     return rank * rays_per_rank, rays_per_rank
+
+
+def ray_range(rank: int, world: int, n_total: int):
+    """(ray_offset, count) of rank's share of one burst of n_total rays (contiguous, balanced)."""
+    lo = rank * n_total // world
+    return lo, (rank + 1) * n_total // world - lo
 
 
 def owns_cell(cell: int, rank: int, world: int, nx: int) -> bool:
@@ -46,3 +56,27 @@ def reduce_max(value: float, device, group=None) -> float:
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
         return float(t[0])
     return value
+
+
+def exchange_records(keys, amps, send_counts, group=None):
+    """Sparse all-to-all of coverage records: this rank's (key, amplitude) pairs, grouped by
+    destination rank with send_counts[d] for rank d, go to their owners.  Returns the received
+    (keys int64, amps float64), concatenated in source-rank order (= ray order, since rank r holds
+    ray ids below rank r+1's).  Keys and amplitudes travel as one (n, 2) int64 buffer: one
+    collective for the counts, one for the records.  (gloo, used by the CPU tests, moves device
+    tensors through host memory; "nccl" = RCCL sends them device to device over xGMI.)"""
+    import torch
+    import torch.distributed as dist
+    home = keys.device
+    wire = torch.device("cpu") if (home.type != "cpu" and dist.get_backend(group) == "gloo") else home
+    send_counts = [int(c) for c in send_counts]
+    n = sum(send_counts)
+    sc = torch.tensor(send_counts, dtype=torch.int64, device=wire)
+    rc = torch.empty_like(sc)
+    dist.all_to_all_single(rc, sc, group=group)
+    recv_counts = [int(c) for c in rc.tolist()]
+    packed = torch.stack([keys[:n].view(torch.int64), amps[:n].contiguous().view(torch.int64)], dim=1).to(wire)
+    out = torch.empty((sum(recv_counts), 2), dtype=torch.int64, device=wire)
+    dist.all_to_all_single(out, packed, recv_counts, send_counts, group=group)
+    out = out.to(home)
+    return out[:, 0].contiguous(), out[:, 1].contiguous().view(torch.float64)

@@ -99,3 +99,39 @@ def test_shard_helpers():
     assert owners == [1] * 100
     # a whole x column belongs to one rank
     assert all(rdist.owns_cell(c, (c % 10) % 8, 8, 10) for c in range(100))
+
+
+def _a2a_worker(rank, world, port, out):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # rank r sends (r + d + 1) records to rank d: key = r*1000 + d*100 + i, amp = key / 7
+    counts = [rank + d + 1 for d in range(world)]
+    keys = torch.tensor([rank * 1000 + d * 100 + i for d in range(world) for i in range(counts[d])], dtype=torch.int64)
+    amps = keys.to(torch.float64) / 7.0
+    k, a = rdist.exchange_records(keys, amps, counts)
+    out.put((rank, k.tolist(), a.tolist()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_exchange_records_routes_in_source_rank_order(world):
+    """dist.exchange_records (ray-sharded coverage): every owner receives its records from rank 0,
+    then rank 1, ... -- the ray order the per-(cell, bin) sums rely on -- with amplitudes bit-exact."""
+    q = mp.get_context("spawn").SimpleQueue()
+    pc = mp.spawn(_a2a_worker, args=(world, _port(), q), nprocs=world, join=False)
+    got = dict((r, (k, a)) for r, k, a in (q.get() for _ in range(world)))
+    pc.join()
+    for d in range(world):
+        want = [r * 1000 + d * 100 + i for r in range(world) for i in range(r + d + 1)]
+        assert got[d][0] == want
+        assert got[d][1] == [float(np.float64(x) / 7.0) for x in want]
+
+
+def test_ray_range_partitions_the_burst():
+    for n, w in [(1_000_000, 8), (7, 3), (16_777_216, 8), (5, 5)]:
+        parts = [rdist.ray_range(r, w, n) for r in range(w)]
+        assert parts[0][0] == 0 and sum(c for _, c in parts) == n
+        for (o1, c1), (o2, _) in zip(parts, parts[1:]):
+            assert o1 + c1 == o2

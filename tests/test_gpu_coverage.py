@@ -137,3 +137,77 @@ def test_coverage_on_bvh_terrain():
     power, ref = _compare(cov, grid, t, tx, B, N, win=200e-9)
     assert np.isfinite(ref).sum() >= 3
     cov.close()
+
+
+def _ray_sharded(env, grid, tx, B, N, S, win=100e-9, env_mesh=None):
+    """S ray-mode plans in one process: each traces its share of the rays for every cell, the
+    records are routed to their owners as the all-to-all would (source-rank order), every owner
+    computes its cells, and the maps are summed (what run() does across S GPUs)."""
+    plans = [Coverage(env, 2.998e8, 100e9, win, B, N, grid, shard_index=r, shard_count=S, shard_mode="rays",
+                      env_mesh=env_mesh) for r in range(S)]
+    sent = [p.trace_records(tx, 1) for p in plans]
+    total = torch.zeros(grid.num_cells, dtype=torch.float64, device="cuda")
+    irs = []
+    for d, p in enumerate(plans):
+        ks, as_ = [], []
+        for keys, amps, counts in sent:  # source ranks in order
+            off = sum(counts[:d])
+            ks.append(keys[off:off + counts[d]])
+            as_.append(amps[off:off + counts[d]])
+        total += p.power_from_records(torch.cat(ks), torch.cat(as_))
+        irs.append(p.impulse_responses())
+    for p in plans:
+        p.close()
+    return total.cpu().numpy(), irs
+
+
+@pytest.mark.parametrize("S", [1, 2, 3, 8])
+def test_coverage_ray_sharded_equals_whole(room, S):
+    """Ray shards + record exchange give the single-GPU map: identical NaN pattern and nonzero bins,
+    powers to f64 summation order (each (cell, bin) is summed per shard, then over shards)."""
+    grid, tx, B, N = CoverageGrid(8.0, -2.5, 4.6, 0.37, 0.41, 0.4, 13, 12, 2), (10, 0, 5), 3, 60_000
+    cov = Coverage(room, 2.998e8, 100e9, 100e-9, B, N, grid)
+    whole = cov.run_device(tx).cpu().numpy()
+    wc, wb, wa = cov.impulse_responses()
+    cov.close()
+    total, irs = _ray_sharded(room, grid, tx, B, N, S)
+    np.testing.assert_array_equal(np.isnan(total), np.isnan(whole))
+    ok = ~np.isnan(whole)
+    assert ok.sum() >= 20
+    np.testing.assert_allclose(total[ok], whole[ok], rtol=1e-12)
+    # owners' sparse impulse responses partition the whole run's, with the same bins
+    c = np.concatenate([x[0] for x in irs])
+    b = np.concatenate([x[1] for x in irs])
+    a = np.concatenate([x[2] for x in irs])
+    o = np.lexsort((b, c))
+    np.testing.assert_array_equal(c[o], wc)
+    np.testing.assert_array_equal(b[o], wb)
+    np.testing.assert_allclose(a[o], wa, rtol=1e-12)
+
+
+def test_coverage_ray_sharded_vs_oracle(room):
+    """Ray-sharded (4 shards) against the per-cell reference loop, through the same bar as above."""
+    grid, tx, B, N = CoverageGrid.square(10, 15, 5), (10, 0, 5), 3, 24_000
+    total, irs = _ray_sharded(room, grid, tx, B, N, 4)
+    E = orc.Mesh(room.vertices, room.faces)
+    ref_p, ref_irs, ref_cr = orc.coverage_loop(E, tx, grid.centers().reshape(-1, 3), B, N, win=100e-9, with_cr=True)
+    np.testing.assert_array_equal(np.isnan(total), np.isnan(ref_p))
+    ok = ~np.isnan(ref_p)
+    assert ok.sum() >= 3
+    np.testing.assert_allclose(total[ok], ref_cr[ok], rtol=1e-9)
+
+
+def test_coverage_ray_sharded_bvh_terrain():
+    from rf_ray_tracing_warp_amd._lib import DeviceMesh
+    from rf_ray_tracing_warp_amd.mesh import synthetic_terrain
+    t = synthetic_terrain(256, 50.0)
+    env = DeviceMesh(t.vertices, t.faces, 0)
+    grid, tx, B, N = CoverageGrid(4.0, -6.0, 2.0, 0.9, 0.8, 1.0, 16, 16, 1), (10.0, 0.0, 4.5), 3, 40_000
+    cov = Coverage(t, 2.998e8, 100e9, 200e-9, B, N, grid, env_mesh=env)
+    whole = cov.run_device(tx).cpu().numpy()
+    cov.close()
+    total, _ = _ray_sharded(t, grid, tx, B, N, 8, win=200e-9, env_mesh=env)
+    np.testing.assert_array_equal(np.isnan(total), np.isnan(whole))
+    ok = ~np.isnan(whole)
+    assert ok.sum() >= 10
+    np.testing.assert_allclose(total[ok], whole[ok], rtol=1e-12)

@@ -1,6 +1,9 @@
 """Coverage timing per configuration, for rocprofv3 --kernel-trace and for strong-scaling
-estimates: K3 (room, 256^2) and K5 (terrain stand-in, 1024^2), each as the whole map and as
-rank 0 of an S-way cell shard (the per-rank work of an S-GPU run).  Prints one JSON line per case."""
+estimates: K3 (room, 256^2) and K5 (terrain stand-in, 1024^2), each as the whole map and as the
+per-rank work of an S-GPU run.  MODE=cells: rank 0 of an S-way x-column cell shard.  MODE=rays
+(default): all S ray-shard plans run one after another on this GPU; per rank, the time of its
+trace + local reduce (stage 1) plus its owner stage on the records routed to it, and the slowest
+rank is reported (the all-to-all itself is not included).  Prints one JSON line per case."""
 import json
 import os
 import sys
@@ -18,6 +21,7 @@ def main():
     cases = os.environ.get("CASES", "k3,k5").split(",")
     shards = [int(s) for s in os.environ.get("SHARDS", "1,8").split(",")]
     reps = int(os.environ.get("REPS", "3"))
+    mode = os.environ.get("MODE", "rays")
     for case in cases:
         if case == "k3":
             m = load_stl(os.path.join(ROOT, "models/room.stl"))
@@ -27,6 +31,9 @@ def main():
             grid, tx, win, B = CoverageGrid.square(1024, 50.0, 2.0), (10.0, 0.0, 4.5), 200e-9, 3
         env = DeviceMesh(m.vertices, m.faces, 0)
         for S in shards:
+            if mode == "rays" and S > 1:
+                rays_case(case, m, grid, tx, win, B, env, S, reps)
+                continue
             cov = Coverage(m, 2.998e8, 100e9, win, B, 1_000_000, grid, 0.1, device=0, shard_index=0, shard_count=S,
                            env_mesh=env)
             cov.run_device(tx)
@@ -40,6 +47,49 @@ def main():
                               "candidates_rank0": cov.last_candidates}), flush=True)
             cov.close()
         env.close()
+
+
+def rays_case(case, m, grid, tx, win, B, env, S, reps):
+    import torch
+    from rf_ray_tracing_warp_amd.coverage import Coverage
+    plans = [Coverage(m, 2.998e8, 100e9, win, B, 1_000_000, grid, 0.1, device=0, shard_index=r, shard_count=S,
+                      env_mesh=env, shard_mode="rays") for r in range(S)]
+
+    def timed(fn):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out = fn()
+        torch.cuda.synchronize()
+        return out, time.perf_counter() - t0
+
+    best = None
+    for _ in range(reps + 1):  # first pass warms up
+        sent, t_trace = [], []
+        for p in plans:
+            out, dt = timed(lambda: p.trace_records(tx, 1))
+            sent.append(out)
+            t_trace.append(dt)
+        t_own, nrec = [], []
+        for d, p in enumerate(plans):
+            ks, as_ = [], []
+            for keys, amps, counts in sent:
+                off = sum(counts[:d])
+                ks.append(keys[off:off + counts[d]])
+                as_.append(amps[off:off + counts[d]])
+            k, a = torch.cat(ks), torch.cat(as_)
+            nrec.append(int(k.numel()))
+            _, dt = timed(lambda: p.power_from_records(k, a))
+            t_own.append(dt)
+        per_rank = [a + b for a, b in zip(t_trace, t_own)]
+        if best is None or max(per_rank) < max(best[0]):
+            best = (per_rank, t_trace, t_own, nrec, [sum(c) for _, _, c in sent])
+    per_rank, t_trace, t_own, nrec, nsent = best
+    print(json.dumps({"case": case, "mode": "rays", "shards": S, "ms_per_map_max_rank": max(per_rank) * 1e3,
+                      "ms_trace_stage": [round(x * 1e3, 3) for x in t_trace],
+                      "ms_owner_stage": [round(x * 1e3, 3) for x in t_own],
+                      "records_sent": nsent, "records_received": nrec}), flush=True)
+    for p in plans:
+        p.close()
 
 
 if __name__ == "__main__":
