@@ -261,7 +261,10 @@ def main():
     index = torch.empty(N, dtype=torch.int64, device=dev)
     count = torch.empty(1, dtype=torch.int64, device=dev)
     ws = torch.empty(int(lib().rt_compact_workspace_bytes(N)), dtype=torch.uint8, device=dev)
-    ir = torch.zeros(n_bins, dtype=torch.float64, device=dev)
+    # two impulse-response buffers: step i's RCCL all-reduce (on RCCL's own stream) overlaps step
+    # i+1's trace; a buffer is reused only once the all-reduce issued on it two steps earlier is done
+    irs = [torch.zeros(n_bins, dtype=torch.float64, device=dev) for _ in range(2)]
+    pending = [None, None]
     amp0 = tx_power / (N * world)
     ray_offset = rank * N
     flags = cir_flags(c, fs)
@@ -270,7 +273,17 @@ def main():
     sh = stream.cuda_stream
     ev = []
 
-    def step(timed):
+    def drain():
+        for j in range(2):
+            if pending[j] is not None:
+                pending[j].wait()  # the current stream waits for that all-reduce
+                pending[j] = None
+
+    def step(i, timed):
+        ir = irs[i % 2]
+        if pending[i % 2] is not None:
+            pending[i % 2].wait()
+            pending[i % 2] = None
         ir.zero_()
         if timed:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -284,17 +297,19 @@ def main():
         check(L.rt_cir(ptr(received), ptr(index), ptr(count), N, B, amp0, c, fs, flags, n_bins, ptr(ir), None, None,
                        sh), "rt_cir")
         if world > 1:
-            dist.all_reduce(ir)
+            pending[i % 2] = dist.all_reduce(ir, async_op=True)
 
-    for _ in range(args.warmup):
-        step(False)
+    for i in range(args.warmup):
+        step(i, False)
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
+    for i in range(args.steps):
+        step(i, True)
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

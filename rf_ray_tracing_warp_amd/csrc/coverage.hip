@@ -12,13 +12,15 @@
 //             columns its padded capsule crosses -> column items                      [capsule raster]
 //   k_cells   one column item per lane (balanced: a grazing ray's hundreds of cells spread over
 //             many lanes): ball test of the few cells of the column -> keys (cell, ray, k)
-//   sort      radix sort of the keys: candidates grouped by (cell, ray), k ascending
-//   k_win     exact receiver test of each candidate (the cell's icosphere, 80 faces, unrolled)
-//   k_first   the first winning k of each (cell, ray) -> compact replay list
+//   k_win     exact receiver test of each candidate (the cell's icosphere, 80 faces, unrolled) and
+//             the first-win check (earlier bounces of the same (cell, ray) re-tested where their
+//             segment reaches the cell's ball) -> flags, compacted in order (DeviceSelect)
 //   k_replay  replay from (p_k, d_k) with the full per-cell semantics of kernel.py:57-98, then the
-//             CIR body of tracer.py:101-117 -> (cell, bin, amp)
+//             CIR body of tracer.py:101-117 -> record (owner | cell | bin | ray key, amp), in a
+//             coherent order (direction x coarse position keys)
 // Appends use one atomic per wave (prefix sum of the lanes' counts).
-//   sort + reduce-by-key: per-cell sparse impulse response, bins ascending
+//   sort + reduce-by-key: per-cell sparse impulse response, bins ascending, each bin summed in
+//             ray order (the ray is the key's lowest field)
 //   k_power   closed-form mean square of the nonzero samples of ir (*) sin(2 pi 2.4e9 t)
 //             ('same' mode, np.nonzero) over the piecewise-constant active-bin intervals
 //
@@ -72,9 +74,10 @@ struct CovParams {
   double c64, fs64;
   int flags;
   int64_t n_bins;
-  // ray-sharded runs: the owning rank of the record's cell ((cell % nx) % own_world) goes above
-  // the (cell, bin) key at bit own_shift, so one sort groups the records by destination
+  // record keys (record_key): ray-sharded runs put the owning rank of the record's cell
+  // ((cell % nx) % own_world) above the cell, so one sort groups the records by destination
   int own_world, own_shift;
+  int ray_bits, bin_bits, cell_bits;
 };
 __device__ __forceinline__ float4 traj_p(const CovParams& p, int64_t r, int k) { return p.traj[2 * (r * p.B + k)]; }
 __device__ __forceinline__ float4 traj_d(const CovParams& p, int64_t r, int k) { return p.traj[2 * (r * p.B + k) + 1]; }
@@ -453,24 +456,6 @@ __global__ __launch_bounds__(256) void k_cells(CovParams p) {
   }
 }
 
-// ------------------------------------------------------------------ 3. exact receiver test per candidate
-__global__ __launch_bounds__(256) void k_win(CovParams p, const uint64_t* keys, int64_t nkeys, uint8_t* win,
-                                             float* trx) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nkeys; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint64_t key = keys[i];
-    const int64_t cell = (int64_t)(key >> 28), r = (int64_t)((key >> 4) & 0xFFFFFF);
-    const int k = (int)(key & 15);
-    const float4 tp = traj_p(p, r, k), td = traj_d(p, r, k);
-    const float3 o = make_float3(tp.x, tp.y, tp.z);
-    const float3 d = make_float3(td.x, td.y, td.z);
-    const float te = tp.w;
-    const rt::Hit hr = rx_query(p.g, cell, p.r_rx, o, d);  // (lean variant measured no faster here)
-    // kernel.py:85 -- receiver wins if hit and (env missed or env strictly farther)
-    win[i] = (hr.face >= 0 && (isinf(te) || te > hr.t)) ? 1 : 0;
-    trx[i] = hr.t;
-  }
-}
-
 // np.dot / norm on float32 3-vectors and _bounce_amplitude (tracer.py:106-113), as cir.hip
 __device__ __forceinline__ float npdot(const float* a, const float* b) {
   const float p0 = a[0] * b[0], p1 = a[1] * b[1], p2 = a[2] * b[2];
@@ -521,22 +506,126 @@ struct PathAcc {
   }
 };
 
-// ------------------------------------------------------------------ 4. replay + CIR body
-// first winning bounce of each (cell, ray) group -> replay list (key indices)
-// flag the first winning bounce of every (cell, ray): the list of flagged candidates is then
-// compacted in order (hipcub DeviceSelect::Flagged), so records keep the (cell, ray, k) order
-__global__ __launch_bounds__(256) void k_first(const uint64_t* keys, int64_t nkeys, const uint8_t* win, uint8_t* first_flag) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nkeys; i += (int64_t)gridDim.x * blockDim.x) {
-    bool first = win[i] != 0;
-    if (first) {
-      const uint64_t g = keys[i] >> 4;
-      for (int64_t j = i - 1; j >= 0 && (keys[j] >> 4) == g; --j)
-        if (win[j]) {
-          first = false;
-          break;
-        }
+// ------------------------------------------------------------------ 3-4. receiver test, first win, replay
+// Record key (compact): [owner | cell | bin | ray] with the field widths of CovParams.  Sorting it
+// groups the records by destination rank, then (cell, bin), and within a bin puts them in ray
+// order -- the order of tracer.py:116's accumulation -- whatever order the candidates came in.
+__device__ __forceinline__ uint64_t record_key(const CovParams& p, int64_t cell, int64_t bin, int64_t r) {
+  const uint64_t own = p.own_world > 1 ? (uint64_t)((cell % p.g.nx) % p.own_world) : 0ull;
+  return (((own << p.cell_bits | (uint64_t)cell) << p.bin_bits | (uint64_t)bin) << p.ray_bits) | (uint64_t)r;
+}
+
+// Does the receiver of `cell` win bounce k of ray r (kernel.py:85: hit, and the environment missed
+// or is strictly farther)?  tr: the receiver's t.
+__device__ __forceinline__ bool rx_wins(const CovParams& p, int64_t cell, int64_t r, int k, float& tr) {
+  const float4 tp = traj_p(p, r, k), td = traj_d(p, r, k);
+  const rt::Hit hr = rx_query(p.g, cell, p.r_rx, make_float3(tp.x, tp.y, tp.z), make_float3(td.x, td.y, td.z));
+  tr = hr.t;
+  return hr.face >= 0 && (isinf(tp.w) || tp.w > hr.t);
+}
+
+// The first bounce at which the receiver of `cell` wins is the one replayed.  A candidate
+// (cell, r, k) exists for exactly the segments whose padded capsule reaches the cell's ball
+// (column_cells' final seg_ball test on the same doubles), so an earlier winning bounce k' < k can
+// only be a segment passing seg_ball: re-test those (rare; k < B).
+__device__ __forceinline__ bool first_win(const CovParams& p, int64_t cell, int64_t r, int k) {
+  double cc[3];
+  cell_center(p.g, cell, cc);
+  const double rp2 = p.r_pad * p.r_pad;
+  for (int q = 0; q < k; ++q) {
+    const Seg sq = load_seg(p, r, q);
+    float t;
+    if (seg_ball(sq.o, sq.d, sq.tmax, cc, rp2) && rx_wins(p, cell, r, q, t)) return false;
+  }
+  return true;
+}
+
+// Replay of (cell, r) from its first winning bounce k0 (receiver t = tr) with the full per-cell
+// semantics of kernel.py:57-98, then the CIR body of tracer.py:101-117: the record's key (~0 when
+// the path adds nothing: delay past the window, or amplitude 0) and amplitude.
+template <bool USE_BVH>
+__device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab, int64_t cell, int64_t r, int k0,
+                                       float tr, uint64_t& okey, double& oamp) {
+  PathAcc acc;
+  const float4 t0 = traj_p(p, r, 0);
+  acc.start(t0.x, t0.y, t0.z, p.amp0);  // p_0 = tx
+  for (int q = 1; q <= k0; ++q) {       // environment prefix p_1 .. p_k0
+    const float4 tq = traj_p(p, r, q);
+    acc.add(tq.x, tq.y, tq.z);
+  }
+  const float4 tk = traj_p(p, r, k0), tdk = traj_d(p, r, k0);
+  float3 pos = make_float3(tk.x, tk.y, tk.z);
+  const float3 dir = make_float3(tdk.x, tdk.y, tdk.z);
+  // bounce k0: the receiver wins at t = tr
+  pos.x = fmaf(dir.x, tr, pos.x);
+  pos.y = fmaf(dir.y, tr, pos.y);
+  pos.z = fmaf(dir.z, tr, pos.z);
+  acc.add(pos.x, pos.y, pos.z);
+  float rec_dist = acc.dist;
+  double rec_amp = acc.amp;
+  float3 d = dir;
+  for (int b = k0 + 1; b < p.B; ++b) {  // kernel.py:57-98 with this cell's receiver
+    const rt::Shear s = rt::make_shear(pos, d);
+    // environment first, then the receiver.  (A receiver-first order with the environment query
+    // culled at the receiver hit is equivalent, but its build gave run-to-run different
+    // amplitudes on the terrain BVH on some boxes: DESIGN.md §6.)
+    const rt::Hit he = env_query<USE_BVH>(p, lds_tab, s, pos, d);
+    // BVH scenes: the replay waits on node fetches, so occupancy (lean receiver) pays; on the
+    // LDS brute-force path it is VALU-bound and the register-held receiver is faster
+    const rt::Hit hr = USE_BVH ? rx_query_lean(p.g, cell, p.r_rx, pos, d) : rx_query(p.g, cell, p.r_rx, pos, d);
+    const bool env_hit = he.face >= 0, rx_hit = hr.face >= 0;
+    if (rx_hit && (!env_hit || he.t > hr.t)) {
+      pos.x = fmaf(d.x, hr.t, pos.x);
+      pos.y = fmaf(d.y, hr.t, pos.y);
+      pos.z = fmaf(d.z, hr.t, pos.z);
+      acc.add(pos.x, pos.y, pos.z);
+      rec_dist = acc.dist;  // received_paths = traced prefix through this point (kernel.py:89-90)
+      rec_amp = acc.amp;
+    } else if (env_hit) {
+      pos.x = fmaf(d.x, he.t, pos.x);
+      pos.y = fmaf(d.y, he.t, pos.y);
+      pos.z = fmaf(d.z, he.t, pos.z);
+      acc.add(pos.x, pos.y, pos.z);
+      const float4 n4 = p.env_nrm[he.face];
+      const float3 n = make_float3(n4.x, n4.y, n4.z);
+      const float sc = 2.0f * rt::dot3(d, n);
+      d.x = fmaf(-sc, n.x, d.x);
+      d.y = fmaf(-sc, n.y, d.y);
+      d.z = fmaf(-sc, n.z, d.z);
+    } else {
+      break;
     }
+  }
+  double dl;
+  if (p.flags & RT_CIR_C_F64) {
+    dl = ((double)rec_dist / p.c64) * p.fs64;
+  } else {
+    const float q = rec_dist / p.c32;
+    dl = (p.flags & RT_CIR_FS_F64) ? (double)q * p.fs64 : (double)(q * p.fs32);
+  }
+  const int64_t bin = (int64_t)dl;
+  // amplitudes are >= 0; a zero one (NaN angle -> _bounce_amplitude 0, tracer.py:35-37) leaves
+  // impulse_response[bin] untouched, so it must not become an active bin of the power sweep
+  const bool keep = bin < p.n_bins && rec_amp != 0.0;
+  okey = keep ? record_key(p, cell, bin, r) : ~0ull;
+  oamp = keep ? rec_amp : 0.0;
+}
+
+// Per candidate (cell, ray, k), in whatever order k_cells appended them: the exact receiver test
+// and the first-win check; first wins are flagged with their receiver t, to be compacted and
+// replayed in a coherent order by k_replay.  (Replaying inside this kernel on brute-force scenes
+// measured 37% slower on K3, 10.1 vs 7.4 ms per map: the replay's divergent tail and registers
+// held every candidate's wave.)
+__global__ __launch_bounds__(256) void k_win(CovParams p, const uint64_t* keys, int64_t nkeys, uint8_t* first_flag,
+                                             float* trx) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nkeys; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t key = keys[i];
+    const int64_t cell = (int64_t)(key >> 28), r = (int64_t)((key >> 4) & 0xFFFFFF);
+    const int k = (int)(key & 15);
+    float tr;
+    const bool first = rx_wins(p, cell, r, k, tr) && (k == 0 || first_win(p, cell, r, k));
     first_flag[i] = first ? 1 : 0;
+    trx[i] = tr;
   }
 }
 
@@ -580,72 +669,27 @@ __global__ __launch_bounds__(256) void k_replay(CovParams p, const uint64_t* key
     const int64_t i = list[li];
     const uint64_t key = keys[i];
     const int64_t cell = (int64_t)(key >> 28), r = (int64_t)((key >> 4) & 0xFFFFFF);
-    const int k0 = (int)(key & 15);
-    PathAcc acc;
-    const float4 t0 = traj_p(p, r, 0);
-    acc.start(t0.x, t0.y, t0.z, p.amp0);  // p_0 = tx
-    for (int q = 1; q <= k0; ++q) {                 // environment prefix p_1 .. p_k0
-      const float4 tq = traj_p(p, r, q);
-      acc.add(tq.x, tq.y, tq.z);
-    }
-    const float4 tk = traj_p(p, r, k0), tdk = traj_d(p, r, k0);
-    float3 pos = make_float3(tk.x, tk.y, tk.z);
-    const float3 dir = make_float3(tdk.x, tdk.y, tdk.z);
-    // bounce k0: the receiver wins (k_win) at t = trx[i]
-    pos.x = fmaf(dir.x, trx[i], pos.x);
-    pos.y = fmaf(dir.y, trx[i], pos.y);
-    pos.z = fmaf(dir.z, trx[i], pos.z);
-    acc.add(pos.x, pos.y, pos.z);
-    float rec_dist = acc.dist;
-    double rec_amp = acc.amp;
-    float3 d = dir;
-    for (int b = k0 + 1; b < p.B; ++b) {  // kernel.py:57-98 with this cell's receiver
-      const rt::Shear s = rt::make_shear(pos, d);
-      // environment first, then the receiver.  (A receiver-first order with the environment query
-      // culled at the receiver hit is equivalent, but its build gave run-to-run different
-      // amplitudes on the terrain BVH on some boxes: DESIGN.md §6.)
-      const rt::Hit he = env_query<USE_BVH>(p, lds_tab, s, pos, d);
-      // BVH scenes: the replay waits on node fetches, so occupancy (lean receiver) pays; on the
-      // LDS brute-force path it is VALU-bound and the register-held receiver is faster
-      const rt::Hit hr = USE_BVH ? rx_query_lean(p.g, cell, p.r_rx, pos, d) : rx_query(p.g, cell, p.r_rx, pos, d);
-      const bool env_hit = he.face >= 0, rx_hit = hr.face >= 0;
-      if (rx_hit && (!env_hit || he.t > hr.t)) {
-        pos.x = fmaf(d.x, hr.t, pos.x);
-        pos.y = fmaf(d.y, hr.t, pos.y);
-        pos.z = fmaf(d.z, hr.t, pos.z);
-        acc.add(pos.x, pos.y, pos.z);
-        rec_dist = acc.dist;  // received_paths = traced prefix through this point (kernel.py:89-90)
-        rec_amp = acc.amp;
-      } else if (env_hit) {
-        pos.x = fmaf(d.x, he.t, pos.x);
-        pos.y = fmaf(d.y, he.t, pos.y);
-        pos.z = fmaf(d.z, he.t, pos.z);
-        acc.add(pos.x, pos.y, pos.z);
-        const float4 n4 = p.env_nrm[he.face];
-        const float3 n = make_float3(n4.x, n4.y, n4.z);
-        const float sc = 2.0f * rt::dot3(d, n);
-        d.x = fmaf(-sc, n.x, d.x);
-        d.y = fmaf(-sc, n.y, d.y);
-        d.z = fmaf(-sc, n.z, d.z);
-      } else {
-        break;
-      }
-    }
-    double dl;
-    if (p.flags & RT_CIR_C_F64) {
-      dl = ((double)rec_dist / p.c64) * p.fs64;
-    } else {
-      const float q = rec_dist / p.c32;
-      dl = (p.flags & RT_CIR_FS_F64) ? (double)q * p.fs64 : (double)(q * p.fs32);
-    }
-    const int64_t bin = (int64_t)dl;
-    // amplitudes are >= 0; a zero one (NaN angle -> _bounce_amplitude 0, tracer.py:35-37) leaves
-    // impulse_response[bin] untouched, so it must not become an active bin of the power sweep
-    const bool keep = bin < p.n_bins && rec_amp != 0.0;
-    uint64_t okey = ((uint64_t)cell << 32) | (uint64_t)bin;
-    if (p.own_world > 1) okey |= (uint64_t)((cell % p.g.nx) % p.own_world) << p.own_shift;
-    out_key[li] = keep ? okey : ~0ull;
-    out_amp[li] = keep ? rec_amp : 0.0;
+    replay<USE_BVH>(p, lds_tab, cell, r, (int)(key & 15), trx[i], out_key[li], out_amp[li]);
+  }
+}
+
+// compact record key -> the (owner << own_shift | cell << 32 | bin) key of the reduced records
+struct WideKey {
+  int ray_bits, bin_bits, cell_bits, own_shift;
+  __host__ __device__ __forceinline__ uint64_t operator()(uint64_t k) const {
+    if (k == ~0ull) return ~0ull;
+    const uint64_t bin = (k >> ray_bits) & ((1ull << bin_bits) - 1);
+    const uint64_t cell = (k >> (ray_bits + bin_bits)) & ((1ull << cell_bits) - 1);
+    const uint64_t own = k >> (ray_bits + bin_bits + cell_bits);
+    return own << own_shift | cell << 32 | bin;
+  }
+};
+
+// wide (cell << 32 | bin) keys received from other ranks -> compact [cell | bin] for the sort
+__global__ __launch_bounds__(256) void k_compact_keys(const uint64_t* in, int64_t n, int bin_bits, uint64_t* out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = in[i];
+    out[i] = k == ~0ull ? ~0ull : ((k >> 32) << bin_bits | (k & 0xFFFFFFFFull));
   }
 }
 
@@ -1106,6 +1150,8 @@ void free_cands(rt_coverage* c) {
   c->cap = 0;
 }
 
+using WideIter = hipcub::TransformInputIterator<uint64_t, WideKey, const uint64_t*>;
+
 int alloc_cands(rt_coverage* c, int64_t cap) {
   free_cands(c);
   RT_HIP(hipMalloc(&c->keys, cap * 8));
@@ -1119,7 +1165,6 @@ int alloc_cands(rt_coverage* c, int64_t cap) {
   RT_HIP(hipMalloc(&c->tcos, cap * 8));
   RT_HIP(hipMalloc(&c->tsin, cap * 8));
   RT_HIP(hipMalloc(&c->ev, cap * 32));
-  RT_HIP(hipMalloc(&c->win, cap));
   RT_HIP(hipMalloc(&c->first_flag, cap));
   RT_HIP(hipMalloc(&c->trx, cap * 4));
   RT_HIP(hipMalloc(&c->list, cap * 8));
@@ -1127,8 +1172,8 @@ int alloc_cands(rt_coverage* c, int64_t cap) {
   RT_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, b1, c->keys, c->keys_sorted, (int)cap, 0, 64));
   RT_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, b2, c->okeys, c->okeys_sorted, c->oamps, c->oamps_sorted,
                                             (int)cap, 0, 64));
-  RT_HIP(hipcub::DeviceReduce::ReduceByKey(nullptr, b3, c->okeys_sorted, c->ukeys, c->oamps_sorted, c->uamps,
-                                           c->nuniq, hipcub::Sum(), (int)cap));
+  RT_HIP(hipcub::DeviceReduce::ReduceByKey(nullptr, b3, WideIter(c->okeys_sorted, WideKey{0, 0, 0, 0}), c->ukeys,
+                                           c->oamps_sorted, c->uamps, c->nuniq, hipcub::Sum(), (int)cap));
   RT_HIP(hipcub::DeviceSelect::Flagged(nullptr, b4, hipcub::CountingInputIterator<int64_t>(0), c->first_flag, c->list,
                                        (int64_t*)(c->counters + 2), (int)cap));
   c->tmp_bytes = std::max(std::max(b1, b2), std::max(b3, b4));
@@ -1175,8 +1220,23 @@ __global__ __launch_bounds__(256) void k_strip_owner(const uint64_t* ukeys, int6
     out[i] = ukeys[i] & mask;
 }
 
+// field widths of the compact record key [owner | cell | bin | ray]
+struct KeyBits {
+  int ray, bin, cell, own;
+  int total() const { return own + cell + bin + ray; }
+};
+KeyBits key_bits(const rt_coverage* c, int64_t n_bins) {
+  KeyBits k;
+  k.ray = std::max(1, bits_for((uint64_t)(c->n - 1)));
+  k.bin = std::max(1, bits_for((uint64_t)(n_bins - 1)));
+  k.cell = std::max(1, bits_for((uint64_t)(cov_ncell(c) - 1)));
+  k.own = c->ray_mode ? bits_for((uint64_t)(c->nshard - 1)) : 0;
+  return k;
+}
+WideKey wide_key(const rt_coverage* c, const KeyBits& k) { return WideKey{k.ray, k.bin, k.cell, own_shift(c)}; }
+
 // Stages 1-4 (trajectories, candidates, exact receiver tests, replay): the first-win records of
-// this plan's rays as (key, amplitude) in c->okeys / c->oamps, in (cell, ray, k) order.
+// this plan's rays as (compact record key, amplitude) in c->okeys / c->oamps, in candidate order.
 int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double light_speed, double sample_rate,
                 int flags, int64_t n_bins, hipStream_t s, int64_t* ncand_out, int64_t* nlist_out) {
   CovParams p{};
@@ -1265,65 +1325,72 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
   }
   c->last_candidates = ncand;
   *ncand_out = ncand;
-  int64_t nlist = 0;
+  const KeyBits kb = key_bits(c, n_bins);
+  if (kb.total() > 62) {
+    rt::set_error("rt_coverage_run: rays x cells x bins x ranks exceed the 63-bit record key");
+    return RT_EINVAL;
+  }
+  p.ray_bits = kb.ray;
+  p.bin_bits = kb.bin;
+  p.cell_bits = kb.cell;
+  int64_t nrec = 0, nlist = 0;
   if (ncand > 0) {
-    const int endbit = 28 + bits_for((uint64_t)cov_ncell(c));
-    size_t tb = c->tmp_bytes;
-    RT_HIP(hipcub::DeviceRadixSort::SortKeys(c->tmp, tb, c->keys, c->keys_sorted, (int)ncand, 0, endbit, s));
     const unsigned grid_c = (unsigned)std::min<int64_t>((ncand + 255) / 256, 8192);
-    hipLaunchKernelGGL(k_win, dim3(grid_c), dim3(256), 0, s, p, c->keys_sorted, ncand, c->win, c->trx);
-    hipLaunchKernelGGL(k_first, dim3(grid_c), dim3(256), 0, s, c->keys_sorted, ncand, c->win, c->first_flag);
-    tb = c->tmp_bytes;
+    hipLaunchKernelGGL(k_win, dim3(grid_c), dim3(256), 0, s, p, c->keys, ncand, c->first_flag, c->trx);
+    size_t tb = c->tmp_bytes;
     RT_HIP(hipcub::DeviceSelect::Flagged(c->tmp, tb, hipcub::CountingInputIterator<int64_t>(0), c->first_flag,
                                          c->list, (int64_t*)(c->counters + 2), (int)ncand, s));
     RT_HIP(hipMemcpyAsync(&nlist, c->counters + 2, 8, hipMemcpyDeviceToHost, s));
     RT_HIP(hipStreamSynchronize(s));
-  }
-  if (nlist > 0) {
-    const unsigned grid_l = (unsigned)std::min<int64_t>((nlist + 255) / 256, 8192);
-    if (bvh) {
+    if (nlist > 0) {
       // coherent processing order (16-bit keys through hipCUB, workspace stream-ordered)
+      const unsigned grid_l = (unsigned)std::min<int64_t>((nlist + 255) / 256, 8192);
       size_t cub_bytes = 0;
       RT_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (uint16_t*)nullptr, (uint16_t*)nullptr,
                                                 (int32_t*)nullptr, (int32_t*)nullptr, (int)nlist, 0, 16, s));
-      const size_t kb = ((size_t)nlist * 2 + 255) / 256 * 256, rb = ((size_t)nlist * 4 + 255) / 256 * 256;
+      const size_t kbs = ((size_t)nlist * 2 + 255) / 256 * 256, rbs = ((size_t)nlist * 4 + 255) / 256 * 256;
       void* ws = nullptr;
-      RT_HIP(hipMallocAsync(&ws, 2 * kb + 2 * rb + cub_bytes, s));
+      RT_HIP(hipMallocAsync(&ws, 2 * kbs + 2 * rbs + cub_bytes, s));
       uint16_t* k_in = (uint16_t*)ws;
-      uint16_t* k_out = (uint16_t*)((char*)ws + kb);
-      int32_t* v_in = (int32_t*)((char*)ws + 2 * kb);
-      int32_t* v_out = (int32_t*)((char*)ws + 2 * kb + rb);
-      hipLaunchKernelGGL(k_replay_keys, dim3(grid_l), dim3(256), 0, s, p, c->keys_sorted, c->list, nlist, k_in, v_in);
-      RT_HIP(hipcub::DeviceRadixSort::SortPairs((char*)ws + 2 * kb + 2 * rb, cub_bytes, k_in, k_out, v_in, v_out,
+      uint16_t* k_out = (uint16_t*)((char*)ws + kbs);
+      int32_t* v_in = (int32_t*)((char*)ws + 2 * kbs);
+      int32_t* v_out = (int32_t*)((char*)ws + 2 * kbs + rbs);
+      hipLaunchKernelGGL(k_replay_keys, dim3(grid_l), dim3(256), 0, s, p, c->keys, c->list, nlist, k_in, v_in);
+      RT_HIP(hipcub::DeviceRadixSort::SortPairs((char*)ws + 2 * kbs + 2 * rbs, cub_bytes, k_in, k_out, v_in, v_out,
                                                 (int)nlist, 0, 16, s));
-      hipLaunchKernelGGL(k_replay<true>, dim3(grid_l), dim3(256), lds, s, p, c->keys_sorted, c->trx, c->list, nlist,
-                         v_out, c->okeys, c->oamps);
+      if (bvh)
+        hipLaunchKernelGGL(k_replay<true>, dim3(grid_l), dim3(256), 0, s, p, c->keys, c->trx, c->list, nlist, v_out,
+                           c->okeys, c->oamps);
+      else
+        hipLaunchKernelGGL(k_replay<false>, dim3(grid_l), dim3(256), lds, s, p, c->keys, c->trx, c->list, nlist, v_out,
+                           c->okeys, c->oamps);
       RT_HIP(hipFreeAsync(ws, s));
-    } else {
-      hipLaunchKernelGGL(k_replay<false>, dim3(grid_l), dim3(256), lds, s, p, c->keys_sorted, c->trx, c->list, nlist,
-                         (const int32_t*)nullptr, c->okeys, c->oamps);
+      RT_HIP(hipGetLastError());
     }
-    RT_HIP(hipGetLastError());
+    nrec = nlist;
   }
-  c->last_received = nlist;
-  *nlist_out = nlist;
+  c->last_received = nrec;
+  *nlist_out = nrec;
   return RT_OK;
 }
 
-// Stable radix sort of n records on their low kbits key bits, then the sum of every run of equal
-// keys (records of one bin arrive in ray order, so they are summed in ray order): c->ukeys /
-// c->uamps, count in c->nuniq.  keys/amps may be caller buffers (records from other ranks).
-int cov_reduce(rt_coverage* c, const uint64_t* keys, const double* amps, int64_t n, int kbits, hipStream_t s) {
+// Stable radix sort of n records on their low sort_bits key bits (compact record keys, ~0 =
+// dropped, sorting last thanks to one extra key bit), then the sum of every run of equal
+// (owner, cell, bin) -- runs of one bin arrive in ray order, the ray being the lowest key field,
+// so they are summed in ray order -- into c->ukeys (wide keys, wk) / c->uamps, count in c->nuniq.
+// keys/amps may be caller buffers (records from other ranks).
+int cov_reduce(rt_coverage* c, const uint64_t* keys, const double* amps, int64_t n, int sort_bits, WideKey wk,
+               hipStream_t s) {
   if (n > c->cap) {  // records gathered from several ranks can outgrow this rank's candidate buffers
     int rc = alloc_cands(c, n + n / 4 + 1024);
     if (rc) return rc;
   }
   size_t tb = c->tmp_bytes;
   RT_HIP(hipcub::DeviceRadixSort::SortPairs(c->tmp, tb, keys, c->okeys_sorted, amps, c->oamps_sorted, (int)n, 0,
-                                            kbits < 64 ? kbits : 64, s));
+                                            sort_bits < 64 ? sort_bits : 64, s));
   tb = c->tmp_bytes;
-  RT_HIP(hipcub::DeviceReduce::ReduceByKey(c->tmp, tb, c->okeys_sorted, c->ukeys, c->oamps_sorted, c->uamps, c->nuniq,
-                                           hipcub::Sum(), (int)n, s));
+  RT_HIP(hipcub::DeviceReduce::ReduceByKey(c->tmp, tb, WideIter(c->okeys_sorted, wk), c->ukeys, c->oamps_sorted,
+                                           c->uamps, c->nuniq, hipcub::Sum(), (int)n, s));
   return RT_OK;
 }
 
@@ -1439,7 +1506,8 @@ int rt_coverage_run(rt_coverage* c, const float* tx_pos, double tx_power, double
   // records are in (cell, ray, k) order; a stable sort on (cell, bin) keeps that order within a
   // bin, so every bin's amplitudes are summed in ray order.  Dropped records (~0) sort last.
   if (nlist > 0) {
-    rc = cov_reduce(c, c->okeys, c->oamps, nlist, 32 + bits_for((uint64_t)cov_ncell(c)), s);
+    const KeyBits kb = key_bits(c, n_bins);
+    rc = cov_reduce(c, c->okeys, c->oamps, nlist, kb.total() + 1, wide_key(c, kb), s);
     if (rc) return rc;
   } else {
     RT_HIP(hipMemsetAsync(c->nuniq, 0, 8, s));
@@ -1495,7 +1563,8 @@ int rt_coverage_trace_records(rt_coverage* c, const float* tx_pos, double tx_pow
   // local sum per (owner, cell, bin), in ray order; runs of each owner are then contiguous
   std::vector<int64_t> b(world + 1, 0);
   if (nlist > 0) {
-    rc = cov_reduce(c, c->okeys, c->oamps, nlist, own_shift(c) + bits_for((uint64_t)(world - 1)), s);
+    const KeyBits kb = key_bits(c, n_bins);
+    rc = cov_reduce(c, c->okeys, c->oamps, nlist, kb.total() + 1, wide_key(c, kb), s);
     if (rc) return rc;
     hipLaunchKernelGGL(k_owner_bounds, dim3((unsigned)std::min<int64_t>((nlist + 255) / 256, 4096)), dim3(256), 0, s,
                        c->ukeys, c->nuniq, world, own_shift(c), c->bounds);
@@ -1538,7 +1607,16 @@ int rt_coverage_power_records(rt_coverage* c, const uint64_t* keys, const double
   RT_HIP(hipSetDevice(c->device));
   int rc = RT_OK;
   if (n > 0) {
-    rc = cov_reduce(c, keys, amps, n, 32 + bits_for((uint64_t)cov_ncell(c)), s);
+    // received (cell << 32 | bin) keys -> compact [cell | bin]; runs from ranks r < r' hold lower
+    // ray ids, so the stable sort keeps every bin's partial sums in ray order
+    if (n > c->cap && (rc = alloc_cands(c, n + n / 4 + 1024))) return rc;
+    KeyBits kb = key_bits(c, n_bins);
+    kb.ray = 0;
+    kb.own = 0;
+    hipLaunchKernelGGL(k_compact_keys, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 8192)), dim3(256), 0, s, keys,
+                       n, kb.bin, c->keys_sorted);
+    RT_HIP(hipGetLastError());
+    rc = cov_reduce(c, c->keys_sorted, amps, n, kb.total() + 1, wide_key(c, kb), s);
   } else {
     RT_HIP(hipMemsetAsync(c->nuniq, 0, 8, s));
   }
