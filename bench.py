@@ -57,7 +57,7 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(sample_rays, B, tx, rx, min_s=10.0, max_rays=400_000_000):
+def cpu_baseline(sample_rays, B, tx, rx, min_s=10.0, max_rays=400_000_000, threads=None):
     """The oracle (C restatement of kernel.py + tracer.py host tail) on the host cores."""
     from oracle import oracle as orc
     from rf_ray_tracing_warp_amd.mesh import load_stl, sphere
@@ -65,7 +65,7 @@ def cpu_baseline(sample_rays, B, tx, rx, min_s=10.0, max_rays=400_000_000):
     env = load_stl(os.path.join(REPO, "models", "room.stl"))
     rxm = sphere(rx, 0.1, 1)
     E, R = orc.Mesh(env.vertices, env.faces), orc.Mesh(rxm.vertices, rxm.faces)
-    threads = min(16, os.cpu_count() or 1)
+    threads = threads or min(16, os.cpu_count() or 1)
     orc.trace(E, R, tx, B, 0, 2000, nthreads=threads)  # warm
     # bounded sample: consecutive chunks of the same burst (ray ids 0, 1, 2, ...) until ~min_s of CPU work
     t0 = time.perf_counter()
@@ -389,6 +389,8 @@ def main():
             out["k5_terrain_coverage"] = k5_out
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_sample, B, tx, rx)
+            # Warp's CPU launch is serial: the same restatement on one thread
+            out["cpu_baseline_1thread"] = cpu_baseline(args.cpu_sample // 4, B, tx, rx, min_s=3.0, threads=1)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -84,6 +84,42 @@ __global__ __launch_bounds__(256) void k_scatter(const uint32_t* mask, int64_t n
   }
 }
 
+// Scatter with the scan folded in, for up to kFusedTiles tiles: each block sums the counts of the
+// tiles before it (at most a few KB, L2-resident) instead of waiting for a separate scan kernel; the
+// last block writes the total.  Tiles without a flag return before touching the mask again.
+constexpr int64_t kFusedTiles = 1024;
+__global__ __launch_bounds__(256) void k_scatter_fused(const uint32_t* mask, int64_t n, const int64_t* tile_count,
+                                                       int64_t ntiles, int64_t* out_index, int64_t* out_count) {
+  __shared__ int64_t wpart[4];
+  __shared__ int wbase[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int64_t part = 0;
+  for (int64_t j = threadIdx.x; j < (int64_t)blockIdx.x; j += 256) part += tile_count[j];
+  for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+  if (lane == 0) wpart[w] = part;
+  __syncthreads();
+  int64_t run = wpart[0] + wpart[1] + wpart[2] + wpart[3];
+  const int64_t mine = tile_count[blockIdx.x];
+  if ((int64_t)blockIdx.x == ntiles - 1 && threadIdx.x == 0) *out_count = run + mine;
+  if (mine == 0) return;  // uniform over the block
+  const int64_t base = (int64_t)blockIdx.x * TILE;
+  for (int k = 0; k < 8; ++k) {
+    const int64_t i = base + k * 256 + threadIdx.x;
+    const bool f = i < n && mask[i] != 0u;
+    const unsigned long long bal = __ballot(f);
+    const int wc = __popcll(bal);
+    if (lane == 0) wbase[w] = wc;
+    __syncthreads();
+    int before = 0;
+    for (int j = 0; j < w; ++j) before += wbase[j];
+    const int total = wbase[0] + wbase[1] + wbase[2] + wbase[3];
+    const int rank = __popcll(bal & ((1ull << lane) - 1ull));
+    if (f) out_index[run + before + rank] = i;
+    run += total;
+    __syncthreads();
+  }
+}
+
 // np.dot(float32[3], float32[3]): f32 products, summed in double left to right, rounded once
 __device__ __forceinline__ float npdot(const float* a, const float* b) {
   const float p0 = a[0] * b[0], p1 = a[1] * b[1], p2 = a[2] * b[2];
@@ -184,8 +220,13 @@ int rt_compact(const uint32_t* row_mask, int64_t n, void* workspace, int64_t wor
   }
   int64_t* tiles = (int64_t*)workspace;
   hipLaunchKernelGGL(k_count, dim3((unsigned)ntiles), dim3(256), 0, s, row_mask, n, tiles);
-  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, tiles, ntiles, out_count);
-  hipLaunchKernelGGL(k_scatter, dim3((unsigned)ntiles), dim3(256), 0, s, row_mask, n, tiles, out_index);
+  if (ntiles <= kFusedTiles) {  // up to 2M rows: two launches
+    hipLaunchKernelGGL(k_scatter_fused, dim3((unsigned)ntiles), dim3(256), 0, s, row_mask, n, tiles, ntiles,
+                       out_index, out_count);
+  } else {  // the folded prefix would re-read O(ntiles^2) counts: separate scan
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, tiles, ntiles, out_count);
+    hipLaunchKernelGGL(k_scatter, dim3((unsigned)ntiles), dim3(256), 0, s, row_mask, n, tiles, out_index);
+  }
   RT_HIP(hipGetLastError());
   return RT_OK;
 }
@@ -198,8 +239,10 @@ int rt_cir(const float* received, const int64_t* index, const int64_t* count, in
     return RT_EINVAL;
   }
   if (max_count == 0) return RT_OK;
+  // the count is on the device and usually tiny (K2: ~1 row per 1M rays): one block per CU, a
+  // grid-stride loop covers larger counts; empty blocks cost launch time, not work
   const int64_t want = (max_count + 255) / 256;
-  const unsigned grid = (unsigned)(want < 1024 ? want : 1024);
+  const unsigned grid = (unsigned)(want < 256 ? want : 256);
   hipLaunchKernelGGL(k_cir, dim3(grid), dim3(256), 0, (hipStream_t)stream, received, index, count, max_bounces + 1,
                      amp0, (float)light_speed, (float)sample_rate, light_speed, sample_rate, flags, n_bins,
                      impulse_response, out_bin, out_amp);

@@ -209,6 +209,100 @@ __device__ __forceinline__ rt::Hit rx_query_lean(const rt_grid& g, int64_t cell,
   return h;
 }
 
+// Faces 4g..4g+3 of icosphere(1) subdivide icosahedron face g (trimesh's subdivide order): with
+// the corners c0 c1 c2 (vertex ids < 12) and edge midpoints m01 m12 m20 of face g they are
+// (c0 m01 m20), (m01 c1 m12), (m20 m12 c2), (m01 m12 m20).  kIcoGroup[g] = {c0, c1, c2, m01, m12, m20}.
+struct IcoGroups {
+  int v[RT_ICO1_NF / 4][6];
+};
+constexpr IcoGroups ico_groups() {
+  IcoGroups G{};
+  for (int g = 0; g < RT_ICO1_NF / 4; ++g) {
+    G.v[g][0] = rt_ico1_f[4 * g][0];
+    G.v[g][1] = rt_ico1_f[4 * g + 1][1];
+    G.v[g][2] = rt_ico1_f[4 * g + 2][2];
+    G.v[g][3] = rt_ico1_f[4 * g][1];
+    G.v[g][4] = rt_ico1_f[4 * g + 1][2];
+    G.v[g][5] = rt_ico1_f[4 * g][2];
+  }
+  return G;
+}
+constexpr IcoGroups kIcoGroup = ico_groups();
+constexpr int kGroupFace[4][3] = {{0, 3, 5}, {3, 1, 4}, {5, 4, 2}, {3, 4, 5}};
+constexpr bool ico_groups_ok() {
+  for (int g = 0; g < RT_ICO1_NF / 4; ++g) {
+    for (int j = 0; j < 6; ++j)
+      if ((j < 3) != (kIcoGroup.v[g][j] < 12)) return false;
+    for (int f = 0; f < 4; ++f)
+      for (int k = 0; k < 3; ++k)
+        if (rt_ico1_f[4 * g + f][k] != kIcoGroup.v[g][kGroupFace[f][k]]) return false;
+  }
+  return true;
+}
+static_assert(ico_groups_ok(), "rt_icosphere1.h is not in trimesh's subdivide order");
+
+// receiver vertex vi of the sphere centred at c: (float)(unit * r + centre) per axis in double, as
+// make_rx_perm, permuted to the ray's shear axes
+__device__ __forceinline__ float3 rx_vert(const double c[3], double r, int vi, const rt::Shear& s) {
+  const float w0 = (float)(rt_ico1_v[vi][0] * r + c[0]);
+  const float w1 = (float)(rt_ico1_v[vi][1] * r + c[1]);
+  const float w2 = (float)(rt_ico1_v[vi][2] * r + c[2]);
+  return make_float3(rt::pick(w0, w1, w2, s.kx), rt::pick(w0, w1, w2, s.ky), rt::pick(w0, w1, w2, s.kz));
+}
+
+// rx_query with the 12 icosahedron corners held in registers and each group's 3 edge midpoints
+// generated where the group is tested (a midpoint belongs to two groups and is computed twice,
+// 72 vertex evaluations instead of 42): the same double arithmetic on the same values as
+// make_rx_perm, so every bit agrees with rx_query, with ~45 live vertex floats instead of 126.
+__device__ __forceinline__ rt::Hit rx_query_grouped(const rt_grid& g, int64_t cell, double r, float3 o, float3 d) {
+  const rt::Shear s = rt::make_shear(o, d);
+  double c[3];
+  cell_center(g, cell, c);
+  float3 cn[12];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) cn[i] = rx_vert(c, r, i, s);
+  rt::Hit h;
+  rt::hit_init(h);
+#pragma unroll
+  for (int gi = 0; gi < RT_ICO1_NF / 4; ++gi) {
+    // a fresh copy of r per group: the midpoints shared with another group are recomputed there
+    // instead of being kept live (CSE would hold all 30 midpoints in registers)
+    double rg = r;
+    asm volatile("" : "+v"(rg));
+    float3 v[6];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) v[j] = cn[kIcoGroup.v[gi][j]];
+#pragma unroll
+    for (int j = 3; j < 6; ++j) v[j] = rx_vert(c, rg, kIcoGroup.v[gi][j], s);
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const float3 a = v[kGroupFace[f][0]], b = v[kGroupFace[f][1]], q = v[kGroupFace[f][2]];
+      float T, det;
+      if (rt::tri_test(s, make_float4(a.x, a.y, a.z, b.x), make_float4(b.y, b.z, q.x, q.y), q.z, T, det))
+        rt::hit_consider(h, T, det, 4 * gi + f);
+    }
+  }
+  return h;
+}
+
+// receiver query used by the candidate test and the replay (A/B: RT_COV_RXQ 0 registers,
+// 1 per face, 2 grouped)
+#ifndef RT_COV_RXQ
+#define RT_COV_RXQ 2
+#endif
+#ifndef RT_COV_RXQ_BVH
+#define RT_COV_RXQ_BVH 2
+#endif
+#ifndef RT_COV_RXQ_WIN
+#define RT_COV_RXQ_WIN 2
+#endif
+template <int V>
+__device__ __forceinline__ rt::Hit rx_query_v(const rt_grid& g, int64_t cell, double r, float3 o, float3 d) {
+  if constexpr (V == 0) return rx_query(g, cell, r, o, d);
+  else if constexpr (V == 1) return rx_query_lean(g, cell, r, o, d);
+  else return rx_query_grouped(g, cell, r, o, d);
+}
+
 // ------------------------------------------------------------------ 1. environment trajectories
 template <bool USE_BVH>
 __global__ __launch_bounds__(256) void k_traj(CovParams p) {
@@ -519,7 +613,7 @@ __device__ __forceinline__ uint64_t record_key(const CovParams& p, int64_t cell,
 // or is strictly farther)?  tr: the receiver's t.
 __device__ __forceinline__ bool rx_wins(const CovParams& p, int64_t cell, int64_t r, int k, float& tr) {
   const float4 tp = traj_p(p, r, k), td = traj_d(p, r, k);
-  const rt::Hit hr = rx_query(p.g, cell, p.r_rx, make_float3(tp.x, tp.y, tp.z), make_float3(td.x, td.y, td.z));
+  const rt::Hit hr = rx_query_v<RT_COV_RXQ_WIN>(p.g, cell, p.r_rx, make_float3(tp.x, tp.y, tp.z), make_float3(td.x, td.y, td.z));
   tr = hr.t;
   return hr.face >= 0 && (isinf(tp.w) || tp.w > hr.t);
 }
@@ -527,18 +621,7 @@ __device__ __forceinline__ bool rx_wins(const CovParams& p, int64_t cell, int64_
 // The first bounce at which the receiver of `cell` wins is the one replayed.  A candidate
 // (cell, r, k) exists for exactly the segments whose padded capsule reaches the cell's ball
 // (column_cells' final seg_ball test on the same doubles), so an earlier winning bounce k' < k can
-// only be a segment passing seg_ball: re-test those (rare; k < B).
-__device__ __forceinline__ bool first_win(const CovParams& p, int64_t cell, int64_t r, int k) {
-  double cc[3];
-  cell_center(p.g, cell, cc);
-  const double rp2 = p.r_pad * p.r_pad;
-  for (int q = 0; q < k; ++q) {
-    const Seg sq = load_seg(p, r, q);
-    float t;
-    if (seg_ball(sq.o, sq.d, sq.tmax, cc, rp2) && rx_wins(p, cell, r, q, t)) return false;
-  }
-  return true;
-}
+// only be a segment passing seg_ball: k_win re-tests those (rare; k < B).
 
 // Replay of (cell, r) from its first winning bounce k0 (receiver t = tr) with the full per-cell
 // semantics of kernel.py:57-98, then the CIR body of tracer.py:101-117: the record's key (~0 when
@@ -572,7 +655,8 @@ __device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab
     const rt::Hit he = env_query<USE_BVH>(p, lds_tab, s, pos, d);
     // BVH scenes: the replay waits on node fetches, so occupancy (lean receiver) pays; on the
     // LDS brute-force path it is VALU-bound and the register-held receiver is faster
-    const rt::Hit hr = USE_BVH ? rx_query_lean(p.g, cell, p.r_rx, pos, d) : rx_query(p.g, cell, p.r_rx, pos, d);
+    const rt::Hit hr = USE_BVH ? rx_query_v<RT_COV_RXQ_BVH>(p.g, cell, p.r_rx, pos, d)
+                               : rx_query_v<RT_COV_RXQ>(p.g, cell, p.r_rx, pos, d);
     const bool env_hit = he.face >= 0, rx_hit = hr.face >= 0;
     if (rx_hit && (!env_hit || he.t > hr.t)) {
       pos.x = fmaf(d.x, hr.t, pos.x);
@@ -622,8 +706,29 @@ __global__ __launch_bounds__(256) void k_win(CovParams p, const uint64_t* keys, 
     const uint64_t key = keys[i];
     const int64_t cell = (int64_t)(key >> 28), r = (int64_t)((key >> 4) & 0xFFFFFF);
     const int k = (int)(key & 15);
-    float tr;
-    const bool first = rx_wins(p, cell, r, k, tr) && (k == 0 || first_win(p, cell, r, k));
+    // bounce k, and before it (rarely) the earlier bounces whose segment reaches the cell's ball
+    // (first_win): one receiver query site, so the unrolled query is inlined once
+    double cc[3];
+    cell_center(p.g, cell, cc);
+    const double rp2 = p.r_pad * p.r_pad;
+    bool first = true;
+    float tr = 0.0f;
+#pragma unroll 1
+    for (int q = 0; q <= k; ++q) {
+      if (q < k) {
+        const Seg sq = load_seg(p, r, q);
+        if (!seg_ball(sq.o, sq.d, sq.tmax, cc, rp2)) continue;
+      }
+      float t;
+      const bool w = rx_wins(p, cell, r, q, t);
+      if (q == k) {
+        first = w;
+        tr = t;
+      } else if (w) {
+        first = false;
+        break;
+      }
+    }
     first_flag[i] = first ? 1 : 0;
     trx[i] = tr;
   }
@@ -1407,7 +1512,9 @@ int cov_power(rt_coverage* c, int64_t nrec, int64_t n_bins, double alpha, double
   P.cos_a = cos(alpha);
   // one wave per owned cell, 4 per block
   const unsigned grid_cells = (unsigned)std::min<int64_t>((ncell / c->nshard + 4) / 4, 4096);
-  const unsigned grid_small = (unsigned)std::min<int64_t>((ncell / c->nshard + 256) / 256, 8192);
+  // one thread per small cell, 64 per block: each thread's sweep is a chain of dependent loads,
+  // so a sharded map's few thousand cells must still spread over every CU
+  const unsigned grid_small = (unsigned)std::min<int64_t>((ncell / c->nshard + 64) / 64, 16384);
   const TermArrays terms{c->ukeys, c->tcos, c->tsin, c->ev};
   if (c->nshard > 1) RT_HIP(hipMemsetAsync(power, 0, ncell * sizeof(double), s));  // cells of other ranks
   RT_HIP(hipMemsetAsync(c->cstart, 0, ncell * sizeof(int32_t), s));
@@ -1417,7 +1524,7 @@ int cov_power(rt_coverage* c, int64_t nrec, int64_t n_bins, double alpha, double
     hipLaunchKernelGGL(k_terms, dim3(grid_u), dim3(256), 0, s, c->ukeys, c->uamps, c->nuniq, P, c->tcos, c->tsin, c->ev);
     hipLaunchKernelGGL(k_cell_ranges, dim3(grid_u), dim3(256), 0, s, c->ukeys, c->nuniq, ncell, c->cstart, c->cend);
   }
-  hipLaunchKernelGGL(k_power_small, dim3(grid_small), dim3(256), 0, s, terms, c->cstart, c->cend, c->grid, c->shard,
+  hipLaunchKernelGGL(k_power_small, dim3(grid_small), dim3(64), 0, s, terms, c->cstart, c->cend, c->grid, c->shard,
                      c->nshard, P, power);
   if (nrec > 0)
     hipLaunchKernelGGL(k_power, dim3(grid_cells), dim3(256), 0, s, terms, c->cstart, c->cend, c->grid, c->shard,

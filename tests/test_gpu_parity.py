@@ -220,6 +220,26 @@ def _device_cir(received, mask, B, c, fs, win, txp, N):
     return ir.cpu().numpy(), idx[:k].cpu().numpy(), bins[:k].cpu().numpy(), amps[:k].cpu().numpy()
 
 
+@pytest.mark.parametrize("n", [0, 1, 2047, 2048, 2049, 1_000_000, 2048 * 1024, 2048 * 1024 + 1, 5_000_000])
+@pytest.mark.parametrize("density", [0.0, 1e-6, 0.01, 0.5, 1.0])
+def test_compact_ordered(n, density):
+    """rt_compact == np.nonzero(row_mask) (tracer.py:87), through both launch paths (the scan folded
+    into the scatter up to 1024 tiles, a separate scan above), from no row set to every row set."""
+    rng = np.random.default_rng(n + int(density * 1000))
+    mask = (rng.random(n) < density).astype(np.int32)
+    if n and density == 1e-6:
+        mask[n - 1] = 1  # last row of the last tile
+    m = torch.from_numpy(mask).to(DEV)
+    ws = torch.empty(int(lib().rt_compact_workspace_bytes(n)), dtype=torch.uint8, device=DEV)
+    idx = torch.full((max(n, 1),), -1, dtype=torch.int64, device=DEV)
+    cnt = torch.full((1,), -1, dtype=torch.int64, device=DEV)
+    check(lib().rt_compact(ptr(m), n, ptr(ws), ws.numel(), ptr(idx), ptr(cnt), _stream()))
+    k = int(cnt.item())
+    ref = np.nonzero(mask)[0]
+    assert k == len(ref)
+    np.testing.assert_array_equal(idx[:k].cpu().numpy(), ref)
+
+
 @pytest.mark.parametrize("case", ["edge", "room0", "room1", "room2"])
 def test_cir_matches_reference_golden(case):
     h = np.load(os.path.join(HERE, "golden", "host_cir.npz"))
