@@ -1232,6 +1232,8 @@ struct rt_coverage {
   int64_t cap = 0;
   int64_t last_candidates = 0;
   int64_t last_received = 0;  // first-win (cell, ray) records of the last run
+  void* rord = nullptr;        // replay-order sort workspace (16-bit keys + int32 rows, x2, + hipCUB)
+  size_t rord_bytes = 0;
   int64_t* bounds = nullptr;   // ray mode: [world + 1] starts of each owner's run in the reduced records
   int64_t n_out = 0;           // ray mode: valid reduced records of the last rt_coverage_trace_records
 };
@@ -1242,7 +1244,7 @@ void free_cands(rt_coverage* c) {
   for (void* q : {(void*)c->keys, (void*)c->keys_sorted, (void*)c->okeys, (void*)c->okeys_sorted, (void*)c->ukeys,
                   (void*)c->oamps, (void*)c->oamps_sorted, (void*)c->uamps, (void*)c->tcos, (void*)c->tsin, (void*)c->ev,
                   (void*)c->win, (void*)c->trx,
-                  (void*)c->list, (void*)c->first_flag, c->tmp})
+                  (void*)c->list, (void*)c->first_flag, c->tmp, c->rord})
     if (q) (void)hipFree(q);
   c->keys = c->keys_sorted = c->okeys = c->okeys_sorted = c->ukeys = nullptr;
   c->oamps = c->oamps_sorted = c->uamps = c->tcos = c->tsin = c->ev = nullptr;
@@ -1252,10 +1254,32 @@ void free_cands(rt_coverage* c) {
   c->list = nullptr;
   c->tmp = nullptr;
   c->tmp_bytes = 0;
+  c->rord = nullptr;
+  c->rord_bytes = 0;
   c->cap = 0;
 }
 
 using WideIter = hipcub::TransformInputIterator<uint64_t, WideKey, const uint64_t*>;
+
+size_t rord_key_bytes(int64_t n) { return ((size_t)n * 2 + 255) / 256 * 256; }
+size_t rord_row_bytes(int64_t n) { return ((size_t)n * 4 + 255) / 256 * 256; }
+
+// Record sorts (stable, on the low end_bit key bits).  rocprim sends 8-byte-key radix sorts of up
+// to 1M items to a block merge sort (~15 launches), otherwise to Onesweep (ceil(bits / 8) passes,
+// each a fill + a sort launch).  rocprofv3, one K3 rank of 8 (tools/cov_profile.py): the trace
+// stage's ~0.7M records on 51 bits take 238 us merged vs ~205 us by Onesweep; the owner stage's
+// ~0.2M (31 bits) are faster merged (owner stage 0.23 vs 0.29 ms) and K5's ~0.47M (36 bits) by
+// Onesweep (0.46 vs 0.50 ms).  So: Onesweep from 300k items, rocprim's default below.
+using OnesweepOnly =
+    rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, rocprim::default_config, 0>;
+constexpr int64_t kOnesweepMinItems = 300000;
+hipError_t sort_records(void* tmp, size_t& bytes, const uint64_t* kin, uint64_t* kout, const double* vin, double* vout,
+                        int64_t n, int end_bit, hipStream_t s) {
+  if (n >= kOnesweepMinItems)
+    return rocprim::radix_sort_pairs<OnesweepOnly>(tmp, bytes, kin, kout, vin, vout, (unsigned)n, 0u,
+                                                   (unsigned)end_bit, s);
+  return rocprim::radix_sort_pairs(tmp, bytes, kin, kout, vin, vout, (unsigned)n, 0u, (unsigned)end_bit, s);
+}
 
 int alloc_cands(rt_coverage* c, int64_t cap) {
   free_cands(c);
@@ -1275,14 +1299,23 @@ int alloc_cands(rt_coverage* c, int64_t cap) {
   RT_HIP(hipMalloc(&c->list, cap * 8));
   size_t b1 = 0, b2 = 0, b3 = 0, b4 = 0;
   RT_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, b1, c->keys, c->keys_sorted, (int)cap, 0, 64));
-  RT_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, b2, c->okeys, c->okeys_sorted, c->oamps, c->oamps_sorted,
-                                            (int)cap, 0, 64));
+  size_t b2m = 0;  // both sort_records paths: Onesweep at cap, the merge sort below its threshold
+  RT_HIP(sort_records(nullptr, b2, c->okeys, c->okeys_sorted, c->oamps, c->oamps_sorted, cap, 64, 0));
+  RT_HIP(sort_records(nullptr, b2m, c->okeys, c->okeys_sorted, c->oamps, c->oamps_sorted,
+                      std::min<int64_t>(cap, kOnesweepMinItems - 1), 64, 0));
+  b2 = std::max(b2, b2m);
   RT_HIP(hipcub::DeviceReduce::ReduceByKey(nullptr, b3, WideIter(c->okeys_sorted, WideKey{0, 0, 0, 0}), c->ukeys,
                                            c->oamps_sorted, c->uamps, c->nuniq, hipcub::Sum(), (int)cap));
   RT_HIP(hipcub::DeviceSelect::Flagged(nullptr, b4, hipcub::CountingInputIterator<int64_t>(0), c->first_flag, c->list,
                                        (int64_t*)(c->counters + 2), (int)cap));
   c->tmp_bytes = std::max(std::max(b1, b2), std::max(b3, b4));
   RT_HIP(hipMalloc(&c->tmp, c->tmp_bytes));
+  // replay-order sort workspace for up to cap records (one allocation per growth, not per run)
+  size_t b5 = 0;
+  RT_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, b5, (uint16_t*)nullptr, (uint16_t*)nullptr, (int32_t*)nullptr,
+                                            (int32_t*)nullptr, (int)cap, 0, 16));
+  c->rord_bytes = 2 * rord_key_bytes(cap) + 2 * rord_row_bytes(cap) + b5;
+  RT_HIP(hipMalloc(&c->rord, c->rord_bytes));
   c->cap = cap;
   return RT_OK;
 }
@@ -1450,12 +1483,9 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
     if (nlist > 0) {
       // coherent processing order (16-bit keys through hipCUB, workspace stream-ordered)
       const unsigned grid_l = (unsigned)std::min<int64_t>((nlist + 255) / 256, 8192);
-      size_t cub_bytes = 0;
-      RT_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (uint16_t*)nullptr, (uint16_t*)nullptr,
-                                                (int32_t*)nullptr, (int32_t*)nullptr, (int)nlist, 0, 16, s));
-      const size_t kbs = ((size_t)nlist * 2 + 255) / 256 * 256, rbs = ((size_t)nlist * 4 + 255) / 256 * 256;
-      void* ws = nullptr;
-      RT_HIP(hipMallocAsync(&ws, 2 * kbs + 2 * rbs + cub_bytes, s));
+      const size_t kbs = rord_key_bytes(nlist), rbs = rord_row_bytes(nlist);
+      size_t cub_bytes = c->rord_bytes - 2 * kbs - 2 * rbs;  // the workspace was sized for cap >= nlist
+      void* ws = c->rord;
       uint16_t* k_in = (uint16_t*)ws;
       uint16_t* k_out = (uint16_t*)((char*)ws + kbs);
       int32_t* v_in = (int32_t*)((char*)ws + 2 * kbs);
@@ -1469,7 +1499,6 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
       else
         hipLaunchKernelGGL(k_replay<false>, dim3(grid_l), dim3(256), lds, s, p, c->keys, c->trx, c->list, nlist, v_out,
                            c->okeys, c->oamps);
-      RT_HIP(hipFreeAsync(ws, s));
       RT_HIP(hipGetLastError());
     }
     nrec = nlist;
@@ -1491,8 +1520,7 @@ int cov_reduce(rt_coverage* c, const uint64_t* keys, const double* amps, int64_t
     if (rc) return rc;
   }
   size_t tb = c->tmp_bytes;
-  RT_HIP(hipcub::DeviceRadixSort::SortPairs(c->tmp, tb, keys, c->okeys_sorted, amps, c->oamps_sorted, (int)n, 0,
-                                            sort_bits < 64 ? sort_bits : 64, s));
+  RT_HIP(sort_records(c->tmp, tb, keys, c->okeys_sorted, amps, c->oamps_sorted, n, sort_bits < 64 ? sort_bits : 64, s));
   tb = c->tmp_bytes;
   RT_HIP(hipcub::DeviceReduce::ReduceByKey(c->tmp, tb, WideIter(c->okeys_sorted, wk), c->ukeys, c->oamps_sorted,
                                            c->uamps, c->nuniq, hipcub::Sum(), (int)n, s));
