@@ -233,11 +233,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the N>1 path on a one-GPU box: every rank on cuda:0, gloo instead of RCCL
+    # (RFRT_BENCH_ONE_GPU=1; never used for reported numbers)
+    one_gpu = os.environ.get("RFRT_BENCH_ONE_GPU") == "1"
+    if one_gpu:
+        local = 0
     torch.cuda.set_device(local)
     dev = f"cuda:{local}"
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        dist.init_process_group("nccl", device_id=torch.device(dev))
+        if one_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device(dev))
 
     from rf_ray_tracing_warp_amd import _lib
     from rf_ray_tracing_warp_amd._lib import DeviceMesh, check, lib, ptr
