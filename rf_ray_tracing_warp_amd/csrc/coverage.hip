@@ -736,7 +736,11 @@ __global__ __launch_bounds__(256) void k_win(CovParams p, const uint64_t* keys, 
 
 // BVH scenes: replay order key of list entry li -- the ray's direction at its first win (8x8
 // octahedral cell) over the cell's coarse position (32x32 Morton), so the lanes of a wave walk
-// nearby BVH paths.  Only the processing order changes: records are written at li.
+// nearby BVH paths.  Brute-force scenes are VALU-bound and a wave runs as long as its lane with
+// the most bounces left after the first win, so there the remaining bounce count (2 bits) leads
+// the key and the cell position drops to 16x16.  Only the processing order changes: records are
+// written at li.
+template <bool USE_BVH>
 __global__ __launch_bounds__(256) void k_replay_keys(CovParams p, const uint64_t* keys, const int64_t* list, int64_t nl,
                                                      uint16_t* okey, int32_t* oval) {
   for (int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; li < nl; li += (int64_t)gridDim.x * blockDim.x) {
@@ -758,7 +762,12 @@ __global__ __launch_bounds__(256) void k_replay_keys(CovParams p, const uint64_t
     uint32_t mz = 0;
 #pragma unroll
     for (int b = 0; b < 5; ++b) mz |= ((cx >> b) & 1u) << (2 * b) | ((cy >> b) & 1u) << (2 * b + 1);
-    okey[li] = (uint16_t)((dy * 8 + dx) << 10 | mz);
+    if (USE_BVH) {
+      okey[li] = (uint16_t)((dy * 8 + dx) << 10 | mz);
+    } else {
+      const uint32_t rem = (uint32_t)min(max(p.B - 1 - k0, 0), 3);
+      okey[li] = (uint16_t)(rem << 14 | (dy * 8 + dx) << 8 | mz >> 2);
+    }
     oval[li] = (int32_t)li;
   }
 }
@@ -1490,7 +1499,10 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
       uint16_t* k_out = (uint16_t*)((char*)ws + kbs);
       int32_t* v_in = (int32_t*)((char*)ws + 2 * kbs);
       int32_t* v_out = (int32_t*)((char*)ws + 2 * kbs + rbs);
-      hipLaunchKernelGGL(k_replay_keys, dim3(grid_l), dim3(256), 0, s, p, c->keys, c->list, nlist, k_in, v_in);
+      if (bvh)
+        hipLaunchKernelGGL(k_replay_keys<true>, dim3(grid_l), dim3(256), 0, s, p, c->keys, c->list, nlist, k_in, v_in);
+      else
+        hipLaunchKernelGGL(k_replay_keys<false>, dim3(grid_l), dim3(256), 0, s, p, c->keys, c->list, nlist, k_in, v_in);
       RT_HIP(hipcub::DeviceRadixSort::SortPairs((char*)ws + 2 * kbs + 2 * rbs, cub_bytes, k_in, k_out, v_in, v_out,
                                                 (int)nlist, 0, 16, s));
       if (bvh)
