@@ -734,12 +734,15 @@ __global__ __launch_bounds__(256) void k_win(CovParams p, const uint64_t* keys, 
   }
 }
 
-// BVH scenes: replay order key of list entry li -- the ray's direction at its first win (8x8
-// octahedral cell) over the cell's coarse position (32x32 Morton), so the lanes of a wave walk
-// nearby BVH paths.  Brute-force scenes are VALU-bound and a wave runs as long as its lane with
-// the most bounces left after the first win, so there the remaining bounce count (2 bits) leads
-// the key and the cell position drops to 16x16.  Only the processing order changes: records are
-// written at li.
+// Replay order key of list entry li.  A wave runs as long as its lane with the most bounces left
+// after the first win, so the remaining bounce count (2 bits) leads; then the ray's direction at
+// its first win (8x8 octahedral cell) and the cell's coarse position (16x16 Morton), so the lanes
+// of a wave walk nearby BVH paths.  (RT_COV_BVH_DIRKEY=1 restores direction over a 32x32 Morton
+// cell for BVH scenes: k_replay<true> 3564 vs 3468 us on K5.)  Only the processing order changes:
+// records are written at li.
+#ifndef RT_COV_BVH_DIRKEY
+#define RT_COV_BVH_DIRKEY 0
+#endif
 template <bool USE_BVH>
 __global__ __launch_bounds__(256) void k_replay_keys(CovParams p, const uint64_t* keys, const int64_t* list, int64_t nl,
                                                      uint16_t* okey, int32_t* oval) {
@@ -762,7 +765,7 @@ __global__ __launch_bounds__(256) void k_replay_keys(CovParams p, const uint64_t
     uint32_t mz = 0;
 #pragma unroll
     for (int b = 0; b < 5; ++b) mz |= ((cx >> b) & 1u) << (2 * b) | ((cy >> b) & 1u) << (2 * b + 1);
-    if (USE_BVH) {
+    if (USE_BVH && RT_COV_BVH_DIRKEY) {
       okey[li] = (uint16_t)((dy * 8 + dx) << 10 | mz);
     } else {
       const uint32_t rem = (uint32_t)min(max(p.B - 1 - k0, 0), 3);
