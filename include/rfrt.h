@@ -142,7 +142,22 @@ int rt_coverage_received(rt_coverage* cov, uint64_t* keys_out, double* amps_out,
 int rt_power_dense(const double* impulse_responses, int64_t rows, int64_t n_bins, double alpha, void* scratch,
                    int64_t scratch_bytes, double* power, void* stream);
 
+/* Stage timing of coverage runs (no reference counterpart: the reference prints one wall time per
+ * cell, tracer.py:119).  rt_coverage_profile(cov, 1) records HIP events around the plan's kernels
+ * and counts its work on every later run; rt_coverage_last_profile fills out[0..9] with the last
+ * run's k_traj ms, candidate passes ms (k_cols + k_cells and the host read of their counts),
+ * k_win ms, k_replay ms, reduce + power ms (sort, reduce-by-key, k_terms, k_power), whole-run ms,
+ * traced ray-bounces (trajectory segments), replayed ray-bounces (sum over first-win records of
+ * B - k0), candidates and first-win records.  Unrecorded entries are NaN; synchronises. */
+int rt_coverage_profile(rt_coverage* cov, int enable);
+int rt_coverage_last_profile(rt_coverage* cov, double* out, int n);
+
 /* Self-test entry points used by the parity tests (not part of the reference surface). */
+/* Debug poison: byte in 0..255 fills every coverage plan buffer and a 256 MB block of the default
+ * memory pool (the stream-ordered sort workspaces come from it) with that byte before each run;
+ * < 0 turns it off (default).  A result that changes with the byte reads memory the run never
+ * wrote (tests/test_gpu_poison.py). */
+int rt_debug_poison(int byte);
 int rt_selftest_math(const float* x, int64_t n, float* out, int op, void* stream);
 int rt_ray_dirs(int64_t ray_offset, int64_t n, float* out, void* stream);
 int rt_query(const rt_mesh* mesh, const float* origins, const float* dirs, int64_t n, float* t, int32_t* face,

@@ -268,3 +268,86 @@ def coverage_loop(env: Mesh, tx, centers, B, n_rays, c=2.998e8, fs=100e9, win=10
     if with_cr:
         return np.array(powers), irs, np.array(powers_cr)
     return np.array(powers), irs
+
+
+# --------------------------------------------------------------------------------------------
+# the same host tail, vectorised over paths (cells whose receiver contains the transmitter receive
+# every ray: a million paths, too many for the literal per-path loop above)
+# --------------------------------------------------------------------------------------------
+def _dot32(a, b):
+    """np.dot of float32 3-vectors, row-wise: f32 products summed left to right in f64, rounded once
+    (equal to np.dot on 200k random vectors)."""
+    p = (a * b).astype(np.float64)
+    return ((p[:, 0] + p[:, 1]) + p[:, 2]).astype(np.float32)
+
+
+def _bounce_amplitude_vec(angle):
+    """tracer.py:34-61 element-wise: theta in float32 (NEP 50: math.pi / 2 - float32), the rest in
+    float64 with NumPy's sin/cos/arcsin instead of math's (equal up to libm ulps)."""
+    with np.errstate(all="ignore"):
+        theta = np.float32(math.pi / 2) - angle / np.float32(2)
+        th = theta.astype(np.float64)
+        ti = np.arcsin((1.0 * np.sin(th)) / 5.0)
+        num = 1.0 * np.cos(ti) - 5.0 * np.cos(th)
+        den = 1.0 * np.cos(ti) + 5.0 * np.cos(th)
+        amp = -(num / den) ** 2
+        amp = np.where(amp < -1, -1.0, amp)
+        out = -amp
+        out = np.where(np.isnan(angle) | np.isnan(amp), 0.0, out)
+    return out
+
+
+def cir_from_rows(received, mask, tx_power, tx_num_rays, light_speed_mps, sample_rate_hz, sample_window_s,
+                  arccos=np.arccos):
+    """clean_paths + cir_from_paths (tracer.py:87-117) vectorised over the received rows: the same
+    float32/float64 operations in the same order per path, accumulated with np.add.at in ray order
+    (sequential, like the loop).  ``arccos`` acts on float32 arrays; pass ``arccos_cr_vec`` for the
+    rounded-once variant.  Returns (impulse_response, per-path delay bins, per-path amplitudes)."""
+    rows = received[mask != 0]
+    n, P = rows.shape[0], rows.shape[1]
+    bad = np.isnan(rows).any(axis=2)
+    length = np.where(bad.any(axis=1), np.argmax(bad, axis=1), P)
+    amp = np.full(n, tx_power / tx_num_rays, dtype=np.float64)
+    dist = np.zeros(n, dtype=np.float32)
+    with np.errstate(all="ignore"):
+        for i in range(P - 2):  # vertex i+1 is interior where i + 2 < length
+            act = i + 2 < length
+            if not act.any():
+                break
+            p1, p2, p3 = rows[act, i], rows[act, i + 1], rows[act, i + 2]
+            s1, s2 = p2 - p1, p3 - p2
+            l1 = np.sqrt(_dot32(s1, s1))
+            cosv = _dot32(s1, s2) / (l1 * np.sqrt(_dot32(s2, s2)))
+            amp[act] = amp[act] * _bounce_amplitude_vec(arccos(cosv).astype(np.float32))
+            dist[act] = dist[act] + l1
+        idx = np.arange(n)
+        last = rows[idx, length - 2] - rows[idx, length - 1]
+        dist = dist + np.sqrt(_dot32(last, last))
+        delay = ((dist / light_speed_mps) * sample_rate_hz).astype(np.int64)
+    ir = np.zeros(int(sample_window_s * sample_rate_hz))
+    keep = delay < ir.shape[0]
+    np.add.at(ir, delay[keep], amp[keep])
+    return ir, delay, amp
+
+
+def arccos_cr_vec(x):
+    """float32 arccos rounded once from float64 (the device's choice), element-wise."""
+    with np.errstate(all="ignore"):
+        return np.arccos(np.asarray(x, np.float64)).astype(np.float32)
+
+
+def coverage_cell(env: Mesh, tx, center, B, n_rays, c=2.998e8, fs=100e9, win=100e-9, tx_power=1, rx_radius=0.1,
+                  nthreads=None):
+    """One iteration of coverage.py:38-57 for one receiver centre, at full burst size: the trace
+    restatement, the vectorised host CIR (NumPy arccos and the rounded-once arccos) and the power.
+    Returns dict(ir, ir_cr, power, power_cr, paths)."""
+    import sys as _sys
+    _sys.path.insert(0, os.path.dirname(_HERE))
+    from rf_ray_tracing_warp_amd.mesh import sphere
+
+    rxm = sphere(np.asarray(center, np.float64), rx_radius, 1)
+    o = trace(env, Mesh(rxm.vertices, rxm.faces), tx, B, 0, n_rays, want_traced=False, nthreads=nthreads)
+    ir, _, _ = cir_from_rows(o["received"], o["mask"], tx_power, n_rays, c, fs, win)
+    ir_cr, _, _ = cir_from_rows(o["received"], o["mask"], tx_power, n_rays, c, fs, win, arccos=arccos_cr_vec)
+    return {"ir": ir, "ir_cr": ir_cr, "power": signal_power(ir, win), "power_cr": signal_power(ir_cr, win),
+            "paths": int(np.count_nonzero(o["mask"]))}

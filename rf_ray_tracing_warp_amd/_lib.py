@@ -34,6 +34,10 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise RfrtError(f"{LIB_PATH} is not built: run `python -m rf_ray_tracing_warp_amd.build` "
                         "(the HIP path has no CPU fallback)")
+    # PyTorch ships its own HIP/HSA runtime libraries under the same sonames as /opt/rocm's.  Load
+    # torch first so librfrt binds to the runtime torch uses: loaded the other way round, the
+    # process ends up with two HSA runtimes and librfrt's sees no device (GPU box, r2a).
+    import torch  # noqa: F401
     L = ctypes.CDLL(LIB_PATH)
     L.rt_last_error.restype = ctypes.c_char_p
     L.rt_version.restype = _int
@@ -61,13 +65,16 @@ def lib():
     L.rt_coverage_power_records.argtypes = [_vp, _vp, _vp, _i64, _i64, ctypes.c_double, _vp, _vp]
     L.rt_coverage_received.argtypes = [_vp, _vp, _vp, _i64, ctypes.POINTER(_i64), _vp]
     L.rt_power_dense.argtypes = [_vp, _i64, _i64, ctypes.c_double, _vp, _i64, _vp, _vp]
+    L.rt_coverage_profile.argtypes = [_vp, _int]
+    L.rt_coverage_last_profile.argtypes = [_vp, _vp, _int]
+    L.rt_debug_poison.argtypes = [_int]
     L.rt_selftest_math.argtypes = [_vp, _i64, _vp, _int, _vp]
     L.rt_ray_dirs.argtypes = [_i64, _i64, _vp, _vp]
     L.rt_query.argtypes = [_vp, _vp, _vp, _i64, _vp, _vp, _vp]
     for name in ("rt_mesh_create", "rt_mesh_create_ex", "rt_mesh_destroy", "rt_mesh_info", "rt_bvh_info", "rt_trace", "rt_compact", "rt_cir",
                  "rt_coverage_create", "rt_coverage_destroy", "rt_coverage_run", "rt_coverage_received",
                  "rt_coverage_create_rays", "rt_coverage_trace_records", "rt_coverage_records",
-                 "rt_coverage_power_records",
+                 "rt_coverage_power_records", "rt_coverage_profile", "rt_coverage_last_profile", "rt_debug_poison",
                  "rt_power_dense", "rt_selftest_math", "rt_ray_dirs", "rt_query"):
         getattr(L, name).restype = _int
     _lib = L

@@ -109,7 +109,8 @@ class Coverage:
 
         if not torch.cuda.is_available():
             raise _lib.RfrtError("Coverage needs a ROCm GPU (librfrt has no CPU path)")
-        self.device = torch.cuda.current_device() if device is None else int(device)
+        # one process per GPU: LOCAL_RANK under torchrun, else the current device
+        self.device = rdist.default_device() if device is None else int(device)
         self.light_speed_mps = light_speed_mps
         self.sample_rate_hz = sample_rate_hz
         self.sample_window_s = sample_window_s
@@ -183,6 +184,11 @@ class Coverage:
     def run_device(self, tx_pos, tx_power=1, process_group=None):
         """Launch; returns the (num_cells,) float64 device tensor (0 for cells of other shards).
         Ray mode with more than one shard exchanges records over ``process_group`` here."""
+        import torch
+        with torch.cuda.device(self.device):  # collectives (RCCL) use the current device
+            return self._run_device(tx_pos, tx_power, process_group)
+
+    def _run_device(self, tx_pos, tx_power, process_group):
         if self.shard_mode == "rays":
             keys, amps, counts = self.trace_records(tx_pos, tx_power)
             if self.shard_count > 1:
@@ -199,10 +205,14 @@ class Coverage:
 
     def run(self, tx_pos, tx_power=1, process_group=None):
         """Power map (nz, ny, nx) float64 on the host; with a process group, sum-reduced over ranks."""
+        import torch
         p = self.run_device(tx_pos, tx_power, process_group)
         if process_group is not None or self.shard_count > 1:
             import torch.distributed as dist
-            dist.all_reduce(p, group=process_group)
+            with torch.cuda.device(self.device):
+                wire = p.to(rdist.wire_device(process_group, self.device))
+                dist.all_reduce(wire, group=process_group)
+                p = wire
         g = self.grid
         return p.cpu().numpy().reshape(g.nz, g.ny, g.nx)
 
@@ -222,6 +232,19 @@ class Coverage:
         k = keys[:m].cpu().numpy().view(np.uint64)
         return (k >> np.uint64(32)).astype(np.int64), (k & np.uint64(0xFFFFFFFF)).astype(np.int64), \
             amps[:m].cpu().numpy()
+
+    PROFILE_KEYS = ("traj_ms", "candidates_ms", "win_ms", "replay_ms", "reduce_power_ms", "total_ms",
+                    "traced_ray_bounces", "replayed_ray_bounces", "candidates", "records")
+
+    def profile(self, enable=True):
+        """Record HIP events around this plan's kernels on every later run (rt_coverage_profile)."""
+        check(lib().rt_coverage_profile(self._h, 1 if enable else 0), "rt_coverage_profile")
+
+    def last_profile(self):
+        """Stage times (ms, GPU events) and work counts of the last run: PROFILE_KEYS -> value."""
+        out = np.zeros(10, np.float64)
+        check(lib().rt_coverage_last_profile(self._h, out.ctypes.data, 10), "rt_coverage_last_profile")
+        return dict(zip(self.PROFILE_KEYS, (float(x) for x in out)))
 
     def close(self):
         if getattr(self, "_h", None) and self._h.value and _lib._lib is not None:

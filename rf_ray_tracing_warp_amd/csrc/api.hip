@@ -45,6 +45,18 @@ __global__ void k_pack_leaf_refs(float4* nodes, const int2* leaves, int64_t nnod
   }
 }
 
+int g_poison = -1;
+void keep_pool_memory();  // trace.hip
+
+int poison_pool(size_t bytes, hipStream_t s) {
+  keep_pool_memory();  // freed blocks stay in the pool, so the next allocations see the poison
+  void* p = nullptr;
+  RT_HIP(hipMallocAsync(&p, bytes, s));
+  RT_HIP(hipMemsetAsync(p, g_poison & 0xFF, bytes, s));
+  RT_HIP(hipFreeAsync(p, s));
+  return RT_OK;
+}
+
 int pack_leaf_refs(rt_mesh* m) {
   if (m->nf >= ((int64_t)1 << 28) || m->bvh_max_leaf > 4) {
     set_error("rt_mesh_create: BVH leaves must hold <= 4 faces of a mesh below 2^28 faces");
@@ -63,6 +75,15 @@ extern "C" {
 const char* rt_last_error(void) { return rt::g_err.c_str(); }
 
 int rt_version(void) { return RFRT_VERSION; }
+
+int rt_debug_poison(int byte) {
+  if (byte > 255) {
+    rt::set_error("rt_debug_poison: byte must be 0..255 (or < 0 to disable)");
+    return RT_EINVAL;
+  }
+  rt::g_poison = byte < 0 ? -1 : byte;
+  return RT_OK;
+}
 
 // same contraction as the device / oracle: a.x*b.x + a.y*b.y + a.z*b.z
 static inline float h_dot(const float* a, const float* b) {
@@ -86,7 +107,8 @@ int rt_mesh_create_ex(int device, const float* vertices, int64_t nv, const int32
       return RT_EINVAL;
     }
   }
-  RT_HIP(hipSetDevice(device));
+  rt::DeviceGuard dg(device);
+  RT_HIP(dg.err);
   // the permuted-corner table feeds the brute-force queries: environments of <= 192 faces
   // (staged in LDS) and receivers (read from HBM, rt_trace).  BVH environments read lcomp, so the
   // table (288 B/face) is skipped for meshes too large to serve as a brute-force receiver.
@@ -175,7 +197,7 @@ int rt_mesh_create_ex(int device, const float* vertices, int64_t nv, const int32
 
 int rt_mesh_destroy(rt_mesh* m) {
   if (!m) return RT_OK;
-  (void)hipSetDevice(m->device);
+  rt::DeviceGuard dg(m->device);
   if (m->perm) (void)hipFree(m->perm);
   if (m->nrm) (void)hipFree(m->nrm);
   if (m->nodes) (void)hipFree(m->nodes);
@@ -225,7 +247,13 @@ int rt_trace(const rt_mesh* env, const float* tx_pos, const rt_mesh* rx, int max
     rt::set_error("rt_trace: receiver mesh too large (max 65536 faces, queried by brute force)");
     return RT_EINVAL;
   }
+  if (rx && rx->device != env->device) {
+    rt::set_error("rt_trace: environment and receiver meshes live on different devices");
+    return RT_EINVAL;
+  }
   if (max_bounces == 0) return RT_OK;
+  rt::DeviceGuard dg(env->device);
+  RT_HIP(dg.err);
   return rt::launch_trace(env, tx_pos, rx, max_bounces, ray_offset, n, traced, received, row_mask, hit_kind, hit_face,
                           (hipStream_t)stream);
 }
@@ -304,6 +332,8 @@ int rt_query(const rt_mesh* m, const float* o, const float* d, int64_t n, float*
     return RT_EINVAL;
   }
   if (n == 0) return RT_OK;
+  rt::DeviceGuard dg(m->device);
+  RT_HIP(dg.err);
   if (m->nodes) {
     const rt::BvhView bv = rt::bvh_view(m);
     hipLaunchKernelGGL(k_query_bvh, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, bv, o, d, n,

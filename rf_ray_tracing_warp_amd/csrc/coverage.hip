@@ -626,7 +626,7 @@ __device__ __forceinline__ bool rx_wins(const CovParams& p, int64_t cell, int64_
 // Replay of (cell, r) from its first winning bounce k0 (receiver t = tr) with the full per-cell
 // semantics of kernel.py:57-98, then the CIR body of tracer.py:101-117: the record's key (~0 when
 // the path adds nothing: delay past the window, or amplitude 0) and amplitude.
-template <bool USE_BVH>
+template <bool USE_BVH, bool RX_FIRST>
 __device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab, int64_t cell, int64_t r, int k0,
                                        float tr, uint64_t& okey, double& oamp) {
   PathAcc acc;
@@ -649,14 +649,20 @@ __device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab
   float3 d = dir;
   for (int b = k0 + 1; b < p.B; ++b) {  // kernel.py:57-98 with this cell's receiver
     const rt::Shear s = rt::make_shear(pos, d);
-    // environment first, then the receiver.  (A receiver-first order with the environment query
-    // culled at the receiver hit is equivalent, but its build gave run-to-run different
-    // amplitudes on the terrain BVH on some boxes: DESIGN.md §6.)
-    const rt::Hit he = env_query<USE_BVH>(p, lds_tab, s, pos, d);
-    // BVH scenes: the replay waits on node fetches, so occupancy (lean receiver) pays; on the
-    // LDS brute-force path it is VALU-bound and the register-held receiver is faster
-    const rt::Hit hr = USE_BVH ? rx_query_v<RT_COV_RXQ_BVH>(p.g, cell, p.r_rx, pos, d)
-                               : rx_query_v<RT_COV_RXQ>(p.g, cell, p.r_rx, pos, d);
+    rt::Hit he, hr;
+    if constexpr (RX_FIRST) {
+      // receiver first, then the environment culled at the receiver's t: every environment hit
+      // with t <= hr.t is still found exactly (rt_bvh.h), and one beyond it loses to the receiver
+      // whatever it is (kernel.py:85), so the decision and the chosen hit are unchanged
+      hr = rx_query_v<RT_COV_RXQ_BVH>(p.g, cell, p.r_rx, pos, d);
+      he = env_query<USE_BVH>(p, lds_tab, s, pos, d, hr.face >= 0 ? hr.t : RT_MAX_T);
+    } else {
+      he = env_query<USE_BVH>(p, lds_tab, s, pos, d);
+      // BVH scenes: the replay waits on node fetches, so occupancy (lean receiver) pays; on the
+      // LDS brute-force path it is VALU-bound and the register-held receiver is faster
+      hr = USE_BVH ? rx_query_v<RT_COV_RXQ_BVH>(p.g, cell, p.r_rx, pos, d)
+                   : rx_query_v<RT_COV_RXQ>(p.g, cell, p.r_rx, pos, d);
+    }
     const bool env_hit = he.face >= 0, rx_hit = hr.face >= 0;
     if (rx_hit && (!env_hit || he.t > hr.t)) {
       pos.x = fmaf(d.x, hr.t, pos.x);
@@ -775,7 +781,7 @@ __global__ __launch_bounds__(256) void k_replay_keys(CovParams p, const uint64_t
   }
 }
 
-template <bool USE_BVH>
+template <bool USE_BVH, bool RX_FIRST>
 __global__ __launch_bounds__(256) void k_replay(CovParams p, const uint64_t* keys, const float* trx,
                                                 const int64_t* list, int64_t nl, const int32_t* order,
                                                 uint64_t* out_key, double* out_amp) {
@@ -786,7 +792,7 @@ __global__ __launch_bounds__(256) void k_replay(CovParams p, const uint64_t* key
     const int64_t i = list[li];
     const uint64_t key = keys[i];
     const int64_t cell = (int64_t)(key >> 28), r = (int64_t)((key >> 4) & 0xFFFFFF);
-    replay<USE_BVH>(p, lds_tab, cell, r, (int)(key & 15), trx[i], out_key[li], out_amp[li]);
+    replay<USE_BVH, RX_FIRST>(p, lds_tab, cell, r, (int)(key & 15), trx[i], out_key[li], out_amp[li]);
   }
 }
 
@@ -1248,6 +1254,12 @@ struct rt_coverage {
   size_t rord_bytes = 0;
   int64_t* bounds = nullptr;   // ray mode: [world + 1] starts of each owner's run in the reduced records
   int64_t n_out = 0;           // ray mode: valid reduced records of the last rt_coverage_trace_records
+  // rt_coverage_profile: stage events of the last run and its work counts (device, [0] traced
+  // ray-bounces = sum of the trajectories' segments, [1] replayed ray-bounces)
+  bool profile = false;
+  hipEvent_t pev[8] = {};
+  bool ev_rec[8] = {};
+  unsigned long long* work = nullptr;
 };
 
 namespace {
@@ -1340,6 +1352,61 @@ int alloc_items(rt_coverage* c, int64_t cap) {
   return RT_OK;
 }
 
+// rt_debug_poison: every buffer of the plan (and a block of the default pool, for the
+// stream-ordered workspaces) is filled with the poison byte before a run
+int poison_plan(rt_coverage* c, hipStream_t s) {
+  const int b = rt::g_poison & 0xFF;
+  const int64_t nc = c->grid.nx * c->grid.ny * c->grid.nz;
+  struct {
+    void* p;
+    size_t n;
+  } bufs[] = {{c->traj, sizeof(float4) * 2 * (size_t)c->B * c->n}, {c->nseg, (size_t)c->n},
+              {c->keys, (size_t)c->cap * 8}, {c->keys_sorted, (size_t)c->cap * 8}, {c->okeys, (size_t)c->cap * 8},
+              {c->okeys_sorted, (size_t)c->cap * 8}, {c->ukeys, (size_t)c->cap * 8}, {c->oamps, (size_t)c->cap * 8},
+              {c->oamps_sorted, (size_t)c->cap * 8}, {c->uamps, (size_t)c->cap * 8}, {c->tcos, (size_t)c->cap * 8},
+              {c->tsin, (size_t)c->cap * 8}, {c->ev, (size_t)c->cap * 32}, {c->first_flag, (size_t)c->cap},
+              {c->trx, (size_t)c->cap * 4}, {c->list, (size_t)c->cap * 8}, {c->items, (size_t)c->item_cap * 8},
+              {c->tmp, c->tmp_bytes}, {c->rord, c->rord_bytes}, {c->counters, 32}, {c->nuniq, 8},
+              {c->cstart, sizeof(int32_t) * (size_t)nc}, {c->cend, sizeof(int32_t) * (size_t)nc},
+              {c->bounds, c->bounds ? sizeof(int64_t) * (size_t)(c->nshard + 1) : 0}};
+  for (auto& q : bufs)
+    if (q.p && q.n) RT_HIP(hipMemsetAsync(q.p, b, q.n, s));
+  return rt::poison_pool((size_t)256 << 20, s);
+}
+
+void prof_mark(rt_coverage* c, int i, hipStream_t s) {
+  if (!c->profile) return;
+  if (!c->pev[i] && hipEventCreate(&c->pev[i]) != hipSuccess) return;
+  c->ev_rec[i] = hipEventRecord(c->pev[i], s) == hipSuccess;
+}
+
+// work counts for the rooflines (profiling only): sum of nseg, and sum over replayed records of
+// the bounces the replay runs (its first-win bounce plus the B - 1 - k0 full queries after it)
+__global__ __launch_bounds__(256) void k_count_segments(const uint8_t* nseg, int64_t n, unsigned long long* out) {
+  unsigned long long acc = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    acc += nseg[i];
+  for (int o = 32; o >= 1; o >>= 1) acc += __shfl_down(acc, o, 64);
+  if ((threadIdx.x & 63) == 0 && acc) atomicAdd(out, acc);
+}
+__global__ __launch_bounds__(256) void k_count_replay(const uint64_t* keys, const int64_t* list, int64_t nl, int B,
+                                                      unsigned long long* out) {
+  unsigned long long acc = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nl; i += (int64_t)gridDim.x * blockDim.x)
+    acc += (unsigned long long)(B - (int)(keys[list[i]] & 15));
+  for (int o = 32; o >= 1; o >>= 1) acc += __shfl_down(acc, o, 64);
+  if ((threadIdx.x & 63) == 0 && acc) atomicAdd(out, acc);
+}
+
+// BVH replay query order (A/B, RFRT_COV_RXFIRST=1: receiver first, environment culled at it)
+bool replay_rx_first() {
+  static const bool v = [] {
+    const char* e = getenv("RFRT_COV_RXFIRST");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 int bits_for(uint64_t v) {
   int b = 0;
   while (b < 64 && (v >> b) != 0) ++b;
@@ -1428,17 +1495,26 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
   const size_t lds = bvh ? 0 : (size_t)p.env_nf * 18 * sizeof(float4);
   const unsigned grid_rays = (unsigned)std::min<int64_t>((c->n + 255) / 256, 4096);
   p.order = nullptr;
+  for (bool& r : c->ev_rec) r = false;
   if (bvh) {  // direction-sorted rows: coherent BVH traversal (as rt_trace)
     void* ws = nullptr;
     p.order = rt::dir_order(c->ray_offset, c->n, s, &ws);
     if (!p.order) return RT_EHIP;
+    prof_mark(c, 0, s);
     hipLaunchKernelGGL(k_traj<true>, dim3(grid_rays), dim3(256), lds, s, p);
+    prof_mark(c, 1, s);
     RT_HIP(hipFreeAsync(ws, s));
     p.order = nullptr;
   } else {
+    prof_mark(c, 0, s);
     hipLaunchKernelGGL(k_traj<false>, dim3(grid_rays), dim3(256), lds, s, p);
+    prof_mark(c, 1, s);
   }
   RT_HIP(hipGetLastError());
+  if (c->profile) {
+    RT_HIP(hipMemsetAsync(c->work, 0, 16, s));
+    hipLaunchKernelGGL(k_count_segments, dim3(1024), dim3(256), 0, s, c->nseg, c->n, c->work);
+  }
   // candidates: column items (pass A) then cells (pass B); grow and retry on overflow
   int64_t ncand = 0;
   const unsigned grid_items = 4096;
@@ -1486,7 +1562,9 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
   int64_t nrec = 0, nlist = 0;
   if (ncand > 0) {
     const unsigned grid_c = (unsigned)std::min<int64_t>((ncand + 255) / 256, 8192);
+    prof_mark(c, 2, s);
     hipLaunchKernelGGL(k_win, dim3(grid_c), dim3(256), 0, s, p, c->keys, ncand, c->first_flag, c->trx);
+    prof_mark(c, 3, s);
     size_t tb = c->tmp_bytes;
     RT_HIP(hipcub::DeviceSelect::Flagged(c->tmp, tb, hipcub::CountingInputIterator<int64_t>(0), c->first_flag,
                                          c->list, (int64_t*)(c->counters + 2), (int)ncand, s));
@@ -1508,13 +1586,20 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
         hipLaunchKernelGGL(k_replay_keys<false>, dim3(grid_l), dim3(256), 0, s, p, c->keys, c->list, nlist, k_in, v_in);
       RT_HIP(hipcub::DeviceRadixSort::SortPairs((char*)ws + 2 * kbs + 2 * rbs, cub_bytes, k_in, k_out, v_in, v_out,
                                                 (int)nlist, 0, 16, s));
-      if (bvh)
-        hipLaunchKernelGGL(k_replay<true>, dim3(grid_l), dim3(256), 0, s, p, c->keys, c->trx, c->list, nlist, v_out,
-                           c->okeys, c->oamps);
+      prof_mark(c, 4, s);
+      if (bvh && replay_rx_first())
+        hipLaunchKernelGGL((k_replay<true, true>), dim3(grid_l), dim3(256), 0, s, p, c->keys, c->trx, c->list, nlist,
+                           v_out, c->okeys, c->oamps);
+      else if (bvh)
+        hipLaunchKernelGGL((k_replay<true, false>), dim3(grid_l), dim3(256), 0, s, p, c->keys, c->trx, c->list, nlist,
+                           v_out, c->okeys, c->oamps);
       else
-        hipLaunchKernelGGL(k_replay<false>, dim3(grid_l), dim3(256), lds, s, p, c->keys, c->trx, c->list, nlist, v_out,
-                           c->okeys, c->oamps);
+        hipLaunchKernelGGL((k_replay<false, false>), dim3(grid_l), dim3(256), lds, s, p, c->keys, c->trx, c->list,
+                           nlist, v_out, c->okeys, c->oamps);
+      prof_mark(c, 5, s);
       RT_HIP(hipGetLastError());
+      if (c->profile)
+        hipLaunchKernelGGL(k_count_replay, dim3(1024), dim3(256), 0, s, c->keys, c->list, nlist, p.B, c->work + 1);
     }
     nrec = nlist;
   }
@@ -1592,7 +1677,8 @@ int rt_coverage_create(int device, const rt_mesh* env, int max_bounces, int64_t 
     rt::set_error("rt_coverage_create: too many cells");
     return RT_EINVAL;
   }
-  RT_HIP(hipSetDevice(device));
+  rt::DeviceGuard dg(device);
+  RT_HIP(dg.err);
   int rc = RT_OK;
   rt_coverage* c = new rt_coverage();
   c->device = device;
@@ -1627,7 +1713,7 @@ int rt_coverage_create(int device, const rt_mesh* env, int max_bounces, int64_t 
 
 int rt_coverage_destroy(rt_coverage* c) {
   if (!c) return RT_OK;
-  (void)hipSetDevice(c->device);
+  rt::DeviceGuard dg(c->device);
   free_cands(c);
   if (c->traj) (void)hipFree(c->traj);
   if (c->nseg) (void)hipFree(c->nseg);
@@ -1637,6 +1723,9 @@ int rt_coverage_destroy(rt_coverage* c) {
   if (c->cend) (void)hipFree(c->cend);
   if (c->items) (void)hipFree(c->items);
   if (c->bounds) (void)hipFree(c->bounds);
+  if (c->work) (void)hipFree(c->work);
+  for (hipEvent_t e : c->pev)
+    if (e) (void)hipEventDestroy(e);
   delete c;
   return RT_OK;
 }
@@ -1649,12 +1738,16 @@ int rt_coverage_run(rt_coverage* c, const float* tx_pos, double tx_power, double
     return RT_EINVAL;
   }
   hipStream_t s = (hipStream_t)stream;
-  RT_HIP(hipSetDevice(c->device));
+  rt::DeviceGuard dg(c->device);
+  RT_HIP(dg.err);
   int64_t ncand = 0, nlist = 0;
-  int rc = cov_records(c, tx_pos, tx_power, light_speed, sample_rate, flags, n_bins, s, &ncand, &nlist);
+  int rc = rt::g_poison >= 0 ? poison_plan(c, s) : RT_OK;
+  if (rc) return rc;
+  rc = cov_records(c, tx_pos, tx_power, light_speed, sample_rate, flags, n_bins, s, &ncand, &nlist);
   if (rc) return rc;
   // records are in (cell, ray, k) order; a stable sort on (cell, bin) keeps that order within a
   // bin, so every bin's amplitudes are summed in ray order.  Dropped records (~0) sort last.
+  prof_mark(c, 6, s);
   if (nlist > 0) {
     const KeyBits kb = key_bits(c, n_bins);
     rc = cov_reduce(c, c->okeys, c->oamps, nlist, kb.total() + 1, wide_key(c, kb), s);
@@ -1664,6 +1757,7 @@ int rt_coverage_run(rt_coverage* c, const float* tx_pos, double tx_power, double
   }
   rc = cov_power(c, nlist, n_bins, alpha, power, s);
   if (rc) return rc;
+  prof_mark(c, 7, s);
   if (stats) {
     stats[0] = ncand;
     stats[1] = nlist;
@@ -1705,13 +1799,17 @@ int rt_coverage_trace_records(rt_coverage* c, const float* tx_pos, double tx_pow
     return RT_EINVAL;
   }
   hipStream_t s = (hipStream_t)stream;
-  RT_HIP(hipSetDevice(c->device));
+  rt::DeviceGuard dg(c->device);
+  RT_HIP(dg.err);
   const int world = c->nshard;
   int64_t ncand = 0, nlist = 0;
-  int rc = cov_records(c, tx_pos, tx_power, light_speed, sample_rate, flags, n_bins, s, &ncand, &nlist);
+  int rc = rt::g_poison >= 0 ? poison_plan(c, s) : RT_OK;
+  if (rc) return rc;
+  rc = cov_records(c, tx_pos, tx_power, light_speed, sample_rate, flags, n_bins, s, &ncand, &nlist);
   if (rc) return rc;
   // local sum per (owner, cell, bin), in ray order; runs of each owner are then contiguous
   std::vector<int64_t> b(world + 1, 0);
+  prof_mark(c, 6, s);
   if (nlist > 0) {
     const KeyBits kb = key_bits(c, n_bins);
     rc = cov_reduce(c, c->okeys, c->oamps, nlist, kb.total() + 1, wide_key(c, kb), s);
@@ -1719,6 +1817,7 @@ int rt_coverage_trace_records(rt_coverage* c, const float* tx_pos, double tx_pow
     hipLaunchKernelGGL(k_owner_bounds, dim3((unsigned)std::min<int64_t>((nlist + 255) / 256, 4096)), dim3(256), 0, s,
                        c->ukeys, c->nuniq, world, own_shift(c), c->bounds);
     RT_HIP(hipGetLastError());
+    prof_mark(c, 7, s);
     RT_HIP(hipMemcpyAsync(b.data(), c->bounds, sizeof(int64_t) * (world + 1), hipMemcpyDeviceToHost, s));
     RT_HIP(hipStreamSynchronize(s));
   }
@@ -1738,7 +1837,8 @@ int rt_coverage_records(rt_coverage* c, uint64_t* keys_out, double* amps_out, in
   }
   if (c->n_out == 0) return RT_OK;
   hipStream_t s = (hipStream_t)stream;
-  RT_HIP(hipSetDevice(c->device));
+  rt::DeviceGuard dg(c->device);
+  RT_HIP(dg.err);
   hipLaunchKernelGGL(k_strip_owner, dim3((unsigned)std::min<int64_t>((c->n_out + 255) / 256, 4096)), dim3(256), 0, s,
                      c->ukeys, c->n_out, own_shift(c), keys_out);
   RT_HIP(hipGetLastError());
@@ -1754,8 +1854,12 @@ int rt_coverage_power_records(rt_coverage* c, const uint64_t* keys, const double
     return RT_EINVAL;
   }
   hipStream_t s = (hipStream_t)stream;
-  RT_HIP(hipSetDevice(c->device));
-  int rc = RT_OK;
+  rt::DeviceGuard dg(c->device);
+  RT_HIP(dg.err);
+  int rc = rt::g_poison >= 0 ? poison_plan(c, s) : RT_OK;
+  if (rc) return rc;
+  c->ev_rec[6] = c->ev_rec[7] = false;
+  prof_mark(c, 6, s);
   if (n > 0) {
     // received (cell << 32 | bin) keys -> compact [cell | bin]; runs from ranks r < r' hold lower
     // ray ids, so the stable sort keeps every bin's partial sums in ray order
@@ -1771,7 +1875,52 @@ int rt_coverage_power_records(rt_coverage* c, const uint64_t* keys, const double
     RT_HIP(hipMemsetAsync(c->nuniq, 0, 8, s));
   }
   if (!rc) rc = cov_power(c, n, n_bins, alpha, power, s);
+  if (!rc) prof_mark(c, 7, s);
   return rc;
+}
+
+int rt_coverage_profile(rt_coverage* c, int enable) {
+  if (!c) {
+    rt::set_error("rt_coverage_profile: null plan");
+    return RT_EINVAL;
+  }
+  rt::DeviceGuard dg(c->device);
+  RT_HIP(dg.err);
+  if (enable && !c->work) RT_HIP(hipMalloc(&c->work, 16));
+  c->profile = enable != 0;
+  return RT_OK;
+}
+
+int rt_coverage_last_profile(rt_coverage* c, double* out, int n) {
+  if (!c || !out || n < 10) {
+    rt::set_error("rt_coverage_last_profile: invalid arguments (out needs 10 doubles)");
+    return RT_EINVAL;
+  }
+  rt::DeviceGuard dg(c->device);
+  RT_HIP(dg.err);
+  for (int i = 0; i < n; ++i) out[i] = NAN;
+  auto span = [&](int a, int b) -> double {
+    if (!c->profile || !c->ev_rec[a] || !c->ev_rec[b]) return NAN;
+    float ms = 0.0f;
+    if (hipEventSynchronize(c->pev[b]) != hipSuccess || hipEventElapsedTime(&ms, c->pev[a], c->pev[b]) != hipSuccess)
+      return NAN;
+    return (double)ms;
+  };
+  out[0] = span(0, 1);  // k_traj
+  out[1] = span(1, 2);  // candidates: k_cols + k_cells (+ the host read of their counts)
+  out[2] = span(2, 3);  // k_win
+  out[3] = span(4, 5);  // k_replay
+  out[4] = span(6, 7);  // record sort + reduce-by-key + power (or + owner bounds in ray mode)
+  out[5] = span(0, 7);  // whole run
+  if (c->profile && c->work) {
+    unsigned long long w[2] = {0, 0};
+    RT_HIP(hipMemcpy(w, c->work, 16, hipMemcpyDeviceToHost));
+    out[6] = (double)w[0];
+    out[7] = (double)w[1];
+  }
+  out[8] = (double)c->last_candidates;
+  out[9] = (double)c->last_received;
+  return RT_OK;
 }
 
 int rt_coverage_received(rt_coverage* c, uint64_t* keys_out, double* amps_out, int64_t max_out, int64_t* n_out,
@@ -1783,6 +1932,8 @@ int rt_coverage_received(rt_coverage* c, uint64_t* keys_out, double* amps_out, i
     return RT_EINVAL;
   }
   hipStream_t s = (hipStream_t)stream;
+  rt::DeviceGuard dg(c->device);
+  RT_HIP(dg.err);
   int64_t nu = 0;
   RT_HIP(hipMemcpyAsync(&nu, c->nuniq, 8, hipMemcpyDeviceToHost, s));
   RT_HIP(hipStreamSynchronize(s));

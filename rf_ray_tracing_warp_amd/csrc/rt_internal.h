@@ -35,6 +35,33 @@ struct rt_mesh {
 namespace rt {
 void set_error(const std::string& msg);
 int hip_fail(hipError_t e, const char* what);
+
+// Scoped device switch for the ABI entry points: the calling thread's current device (which
+// PyTorch also uses) is restored on every return path, including error returns and calls made
+// from Python finalisers (DeviceMesh/Coverage __del__).
+struct DeviceGuard {
+  int prev = -1;
+  hipError_t err = hipSuccess;
+  explicit DeviceGuard(int device) {
+    err = hipGetDevice(&prev);
+    if (err == hipSuccess && prev != device) err = hipSetDevice(device);
+    else if (err != hipSuccess) prev = -1;
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+
+// Debug poison (rt_debug_poison): when >= 0, every coverage plan buffer and a large block of the
+// default memory pool are filled with this byte before each run, so a read of memory the run did
+// not write shows up as a changed result instead of depending on what ran before.
+extern int g_poison;
+// fill `bytes` of a fresh stream-ordered allocation with the poison byte and free it back into the
+// pool (whose release threshold keeps it), so the next hipMallocAsync returns poisoned memory
+int poison_pool(size_t bytes, hipStream_t s);
 // Row order for tracing rays [ray_offset, ray_offset+n) of one burst sorted by initial direction
 // (trace.hip).  Stream-ordered workspace returned in *ws (hipFreeAsync it after the consumer).
 const int32_t* dir_order(int64_t ray_offset, int64_t n, hipStream_t stream, void** ws);

@@ -385,6 +385,10 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
   // BVH meshes: trace the rows in direction-sorted order (K4: 2.98 -> 2.06 ms);
   // brute-force meshes gain nothing from it (every face is tested anyway) and keep row order.
   void* sort_ws = nullptr;
+  if (g_poison >= 0) {
+    const int rc = poison_pool((size_t)256 << 20, stream);
+    if (rc) return rc;
+  }
   if (bvh && n >= kSortMinRays && n <= INT32_MAX) {
     a.order = dir_order(ray_offset, n, stream, &sort_ws);
     if (!a.order) return -1;

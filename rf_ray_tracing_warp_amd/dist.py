@@ -15,6 +15,52 @@ Decompositions:
 """
 from __future__ import annotations
 
+import os
+
+
+def default_device():
+    """The GPU of this process: LOCAL_RANK under torchrun (one process per GPU), else the current
+    device.  Never the global rank, which exceeds the local GPU count beyond one node."""
+    import torch
+    lr = os.environ.get("LOCAL_RANK")
+    if lr is not None:
+        return int(lr)
+    return torch.cuda.current_device()
+
+
+def wire_device(group, device):
+    """Where tensors of a collective live: the process's GPU for "nccl" (RCCL), the host for gloo."""
+    import torch
+    import torch.distributed as dist
+    if dist.get_backend(group) == "nccl":
+        return torch.device(f"cuda:{int(device)}")
+    return torch.device("cpu")
+
+
+def gather_rows(rows, group=None, device=0):
+    """All-gather of variable-length row blocks (numpy (k, ...) float32 arrays, one per rank):
+    a counts all-gather, then one padded tensor all-gather.  Returns the list of every rank's rows
+    in rank order.  Replaces dist.all_gather_object (which pickles, and under "nccl" stages the
+    pickles on whatever device is current)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    wire = wire_device(group, device)
+    rows = np.ascontiguousarray(rows, dtype=np.float32)
+    shape = rows.shape[1:]
+    cnt = torch.tensor([rows.shape[0]], dtype=torch.int64, device=wire)
+    counts = [torch.empty_like(cnt) for _ in range(world)]
+    dist.all_gather(counts, cnt, group=group)
+    counts = [int(c.item()) for c in counts]
+    m = max(max(counts), 1)
+    buf = torch.full((m,) + shape, float("nan"), dtype=torch.float32, device=wire)
+    if rows.shape[0]:
+        buf[:rows.shape[0]] = torch.from_numpy(rows).to(wire)
+    parts = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(parts, buf, group=group)
+    return [p[:c].cpu().numpy() for p, c in zip(parts, counts)]
+
 
 def rank_world(group=None):
     import torch.distributed as dist

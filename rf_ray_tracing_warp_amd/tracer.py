@@ -23,18 +23,29 @@ import time
 import numpy as np
 
 from . import _lib
+from . import dist as rdist
 from ._lib import DeviceMesh, check, lib, ptr
 from .mesh import sphere
 
 __all__ = ["Tracer", "cir_flags"]
 
 
+def _promotes_f32(x) -> bool:
+    """Does ``np.float32 <op> x`` compute in float64 under NumPy 2 (NEP 50)?  Python int/float
+    scalars are weak and keep float32; NumPy scalars and arrays are strong and follow
+    np.result_type (float64, int32/int64/uint32/uint64 -> float64; float16, int8/int16 -> float32)."""
+    if isinstance(x, (np.generic, np.ndarray)):
+        return np.result_type(np.float32, np.asarray(x).dtype) != np.float32
+    return False
+
+
 def cir_flags(light_speed_mps, sample_rate_hz) -> int:
-    """NEP 50: tracer.py:115 stays float32 for Python scalars, becomes float64 for NumPy float64."""
+    """tracer.py:115 ``int((distance / light_speed_mps) * sample_rate_hz)`` with ``distance`` a
+    np.float32: each operation is float32 unless NumPy's promotion makes it float64 (NEP 50)."""
     f = 0
-    if isinstance(light_speed_mps, np.floating) and np.dtype(type(light_speed_mps)).itemsize >= 8:
+    if _promotes_f32(light_speed_mps):
         f |= _lib.RT_CIR_C_F64
-    if isinstance(sample_rate_hz, np.floating) and np.dtype(type(sample_rate_hz)).itemsize >= 8:
+    if _promotes_f32(sample_rate_hz):
         f |= _lib.RT_CIR_FS_F64
     return f
 
@@ -48,7 +59,8 @@ class Tracer:
 
         if not torch.cuda.is_available():
             raise _lib.RfrtError("Tracer needs a ROCm GPU (librfrt has no CPU path)")
-        self.device = torch.cuda.current_device() if device is None else int(device)
+        # one process per GPU: LOCAL_RANK under torchrun, else the current device
+        self.device = rdist.default_device() if device is None else int(device)
         self.light_speed_mps = light_speed_mps
         self.sample_rate_hz = sample_rate_hz
         self.sample_window_s = sample_window_s
@@ -165,6 +177,15 @@ class Tracer:
         import torch
         import torch.distributed as dist
 
+        # collectives run with this tracer's GPU current: under "nccl" (RCCL) a collective uses
+        # the current device, which must be the device of the tensors it moves
+        with torch.cuda.device(self.device):
+            return self._compute_cir_distributed(tx_pos, tx_power, rx_pos, rx_radius, group)
+
+    def _compute_cir_distributed(self, tx_pos, tx_power, rx_pos, rx_radius, group):
+        import torch
+        import torch.distributed as dist
+
         rank, world = dist.get_rank(group), dist.get_world_size(group)
         dev = f"cuda:{self.device}"
         N, P = self.tx_num_rays, self.max_bounces + 1
@@ -183,15 +204,10 @@ class Tracer:
             k = int(count.item())
             if k:
                 rows = received.index_select(0, index[:k]).cpu().numpy()
-        if dist.get_backend(group) == "nccl":
-            dist.all_reduce(ir, group=group)
-            impulse_response = ir.cpu().numpy()
-        else:
-            host = ir.cpu()
-            dist.all_reduce(host, group=group)
-            impulse_response = host.numpy()
-        parts = [None] * world
-        dist.all_gather_object(parts, rows, group=group)
+        wire = ir.to(rdist.wire_device(group, self.device))
+        dist.all_reduce(wire, group=group)
+        impulse_response = wire.cpu().numpy()
+        parts = rdist.gather_rows(rows, group, self.device)
         cleaned_paths = []
         for part in parts:
             for row in part:  # tracer.py:90-97

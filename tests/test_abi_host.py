@@ -73,3 +73,22 @@ def test_nep50_cir_flags():
     assert cir_flags(np.float64(2.998e8), 100e9) == _lib.RT_CIR_C_F64
     assert cir_flags(2.998e8, np.float64(100e9)) == _lib.RT_CIR_FS_F64
     assert cir_flags(np.float32(2.998e8), 100e9) == 0
+
+
+@pytest.mark.parametrize("c", [2.998e8, 299800000, np.float64(2.998e8), np.float32(2.998e8), np.int64(299800000),
+                               np.int32(299800000), np.int16(30000), np.uint64(299800000), np.float16(3e4),
+                               np.array(2.998e8), np.array(2.998e8, np.float32)])
+@pytest.mark.parametrize("fs", [100e9, 100_000_000_000, np.float64(100e9), np.float32(100e9), np.int64(10 ** 11),
+                                np.uint32(4_000_000_000)])
+def test_nep50_cir_flags_follow_numpy_promotion(c, fs):
+    """tracer.py:115 with distance a np.float32: the flags select float64 exactly where NumPy 2 does
+    (strong NumPy integer types such as np.int64 promote float32 to float64, Python scalars do not)."""
+    d = np.float32(37.5)
+    q = d / c
+    val = q * fs
+    f = cir_flags(c, fs)
+    assert bool(f & _lib.RT_CIR_C_F64) == (np.asarray(q).dtype == np.float64)
+    if not f & _lib.RT_CIR_C_F64:
+        assert bool(f & _lib.RT_CIR_FS_F64) == (np.asarray(val).dtype == np.float64)
+    else:
+        assert np.asarray(val).dtype == np.float64

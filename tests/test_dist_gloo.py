@@ -135,3 +135,33 @@ def test_ray_range_partitions_the_burst():
         assert parts[0][0] == 0 and sum(c for _, c in parts) == n
         for (o1, c1), (o2, _) in zip(parts, parts[1:]):
             assert o1 + c1 == o2
+
+
+def _gather_worker(rank, world, port, out):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # rank r holds r*2 rows (rank 0: none) of shape (4, 3), values r*100 + row
+    rows = np.stack([np.full((4, 3), rank * 100 + i, np.float32) for i in range(rank * 2)]) if rank else \
+        np.zeros((0, 4, 3), np.float32)
+    parts = rdist.gather_rows(rows, None, 0)
+    out.put((rank, [p.tolist() for p in parts]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_rows_variable_counts(world):
+    """dist.gather_rows (Tracer.compute_cir_distributed's path gather): counts all-gather + one padded
+    tensor all-gather; every rank gets every rank's rows in rank order, empty blocks included."""
+    q = mp.get_context("spawn").SimpleQueue()
+    pc = mp.spawn(_gather_worker, args=(world, _port(), q), nprocs=world, join=False)
+    got = dict(q.get() for _ in range(world))
+    pc.join()
+    for r in range(world):
+        assert len(got[r]) == world
+        for src in range(world):
+            blk = np.asarray(got[r][src], np.float32).reshape(-1, 4, 3)
+            assert blk.shape[0] == src * 2
+            for i in range(src * 2):
+                assert (blk[i] == src * 100 + i).all()

@@ -211,3 +211,29 @@ def test_coverage_ray_sharded_bvh_terrain():
     ok = ~np.isnan(whole)
     assert ok.sum() >= 10
     np.testing.assert_allclose(total[ok], whole[ok], rtol=1e-12)
+
+
+def test_power_from_records_every_sweep_path(room):
+    """The closed-form power of k_power_small (<= 16 bins), k_power's LDS event sweep (17..192) and
+    its range-split sweep (> 192; no full-size map cell has that many) against np.convolve, fed
+    through rt_coverage_power_records with synthetic per-cell impulse responses."""
+    rng = np.random.default_rng(8)
+    sizes = [0, 1, 2, 5, 16, 17, 64, 191, 192, 193, 400, 2500, 9999]
+    grid = CoverageGrid(0.0, 0.0, 5.0, 1.0, 1.0, 1.0, len(sizes), 1, 1)
+    n, win = 10000, 100e-9
+    irs = np.zeros((len(sizes), n))
+    for c, K in enumerate(sizes):
+        if K:
+            irs[c, np.sort(rng.choice(n, K, replace=False))] = rng.uniform(1e-9, 1e-5, K)
+    irs[2, :] = 0
+    irs[2, [4999, 5000]] = [1e-6, 2e-6]  # the isolated sin(0) sample next to an active one
+    cells, bins = np.nonzero(irs)
+    keys = torch.from_numpy(((cells.astype(np.uint64) << np.uint64(32)) | bins.astype(np.uint64)).view(np.int64)).cuda()
+    amps = torch.from_numpy(irs[cells, bins]).cuda()
+    cov = Coverage(room, 2.998e8, 100e9, win, 3, 1000, grid, shard_mode="rays")
+    got = cov.power_from_records(keys, amps).cpu().numpy()
+    cov.close()
+    ref = np.array([orc.signal_power(irs[c], win) for c in range(len(sizes))])
+    np.testing.assert_array_equal(np.isnan(got), np.isnan(ref))
+    ok = ~np.isnan(ref)
+    np.testing.assert_allclose(got[ok], ref[ok], rtol=1e-9)
