@@ -10,7 +10,12 @@ One step = one pass of the hot path over one synthetic isotropic burst of 1M ray
 Rays are sharded by global ray id (rank r traces ids [r*N, (r+1)*N)): per-GPU work is fixed as
 GPUs are added ("weak").  Inputs (mesh tables) are resident in HBM before the timed region.
 
-    python bench.py [--gpus N --steps K --warmup W]
+Side legs (each its own JSON object in the line): K3 coverage (room, 256^2 cells), K4 (terrain
+stand-in, 5 bounces, ray shards) and K5 coverage (terrain, 1024^2 cells), each with the roofline of
+its dominant kernel from HIP events recorded by the library (rt_coverage_profile / rt_profile), and
+CPU baselines (the oracle, -O3 -march=native, built and timed on this host).
+
+    python bench.py [--gpus N --steps K --warmup W] [--legs k2,k3,k4,k5]
     torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL)
 
 Prints ONE JSON line on rank 0.
@@ -20,7 +25,9 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -28,9 +35,14 @@ import numpy as np
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-METRIC = "ray-bounces/sec on room.stl (1 GPU) + coverage cells/sec at 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 VALU_PEAK_GWI = 1024 * 2.4 / 2  # 256 CUs x 4 SIMDs, one wave64 VALU instruction per 2 cycles
+
+
+def d4_bytes(B):
+    """algorithmic bytes per ray-bounce = the reference kernel's per-ray buffer
+    contract (traced + received rows of 12 (B+1) B, row_mask 4 B) over its B bounces."""
+    return (24 * (B + 1) + 4) / B
 
 
 def parse():
@@ -38,11 +50,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--legs", default="k2,k3,k4,k5", help="comma list of k2 (always run), k3, k4, k5")
     ap.add_argument("--rays", type=int, default=1_000_000, help="rays per GPU per step (K2: 1M)")
     ap.add_argument("--bounces", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="rays per CPU-baseline chunk (~10 s total)")
-    ap.add_argument("--no-coverage", action="store_true")
+    ap.add_argument("--cpu-runs", type=int, default=5, help="timed CPU-baseline runs (median), after 1 warm-up")
+    ap.add_argument("--cpu-rays", type=int, default=8_000_000, help="rays per CPU-baseline run (all threads)")
+    ap.add_argument("--cpu-cells", type=int, default=4, help="K3 cells per coverage CPU-baseline run")
+    ap.add_argument("--no-coverage", action="store_true", help="skip K3 (same as leaving it out of --legs)")
     ap.add_argument("--coverage-grid", type=int, default=256, help="K3: n x n receiver cells at z=5 on room.stl")
     ap.add_argument("--coverage-rays", type=int, default=1_000_000)
     ap.add_argument("--coverage-runs", type=int, default=3)
@@ -52,38 +67,116 @@ def parse():
     ap.add_argument("--k4-rays", type=int, default=2_097_152, help="rays per GPU (K4: 16.7M over 8 GPUs)")
     ap.add_argument("--k5-grid", type=int, default=1024)
     ap.add_argument("--k5-rays", type=int, default=1_000_000)
+    ap.add_argument("--k5-runs", type=int, default=2)
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_k2.json"),
                     help="per-launch HBM bytes measured by rocprofv3 PMC (profiles/)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    legs = set(x.strip() for x in a.legs.split(",") if x.strip()) | {"k2"}
+    if a.no_coverage:
+        legs.discard("k3")
+    if a.no_k4:
+        legs -= {"k4", "k5"}
+    a.legs = legs
+    return a
 
 
-def cpu_baseline(sample_rays, B, tx, rx, min_s=10.0, max_rays=400_000_000, threads=None):
-    """The oracle (C restatement of kernel.py + tracer.py host tail) on the host cores."""
+# ------------------------------------------------------------------ CPU baselines (rank 0, N=1)
+def host_info():
+    model = ""
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                model = line.split(":", 1)[1].strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    # the box gives one GPU's job a share of the host (OMP_NUM_THREADS, 16 there); use all of it
+    share = int(os.environ.get("OMP_NUM_THREADS") or aff or 1)
+    return {"lscpu_model": model, "os_cpu_count": os.cpu_count(), "affinity_cpus": aff, "threads_used": share}
+
+
+def native_oracle():
+    """Build the oracle -O3 -march=native on this host (the prebuilt one is -march=x86-64-v3)."""
+    from oracle import oracle as orc
+    path = os.path.join(tempfile.mkdtemp(prefix="rfrt_oracle_"), "librt_oracle_native.so")
+    try:
+        orc.build_native(path)
+        orc.load(path)
+        return "gcc -O3 -march=native -ffp-contract=off -fopenmp (built on this host)"
+    except (OSError, subprocess.CalledProcessError):
+        orc.load(os.path.join(REPO, "oracle", "_build", "librt_oracle.so"))
+        return "gcc -O3 -march=x86-64-v3 -ffp-contract=off -fopenmp (prebuilt; native build failed)"
+
+
+def _median_runs(fn, runs):
+    fn()  # warm-up
+    ts = []
+    for _ in range(runs):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts)), ts
+
+
+def cpu_baseline_k2(args, B, tx, rx, info, build):
+    """The oracle (C restatement of kernel.py + tracer.py host tail) on the host cores: one run =
+    trace of `rays` rays of the K2 burst + clean + CIR (tracer.py:84-117), median of cpu_runs."""
     from oracle import oracle as orc
     from rf_ray_tracing_warp_amd.mesh import load_stl, sphere
 
     env = load_stl(os.path.join(REPO, "models", "room.stl"))
     rxm = sphere(rx, 0.1, 1)
     E, R = orc.Mesh(env.vertices, env.faces), orc.Mesh(rxm.vertices, rxm.faces)
-    threads = threads or min(16, os.cpu_count() or 1)
-    orc.trace(E, R, tx, B, 0, 2000, nthreads=threads)  # warm
-    # bounded sample: consecutive chunks of the same burst (ray ids 0, 1, 2, ...) until ~min_s of CPU work
-    t0 = time.perf_counter()
-    done = 0
-    while True:
-        o = orc.trace(E, R, tx, B, done, sample_rays, want_traced=True, nthreads=threads)
-        paths = orc.clean_paths(o["received"], o["mask"])
-        orc.cir_from_paths(paths, 1, sample_rays, 2.998e8, 100e9, 100e-9)
-        done += sample_rays
-        dt = time.perf_counter() - t0
-        if dt >= min_s or done >= max_rays:
-            break
-    return {"value": done * B / dt, "unit": "ray-bounces/s", "cores": threads, "kind": "port",
-            "sample": f"{done} rays x {B} bounces (ray ids 0..{done - 1}, chunks of {sample_rays}) of the K2 "
-                      f"room.stl burst: trace + host CIR by oracle/rt_oracle.c (OpenMP, {threads} threads), "
-                      f"{dt:.1f} s"}
+    out = {}
+    for label, threads, rays in (("all", info["threads_used"], args.cpu_rays),
+                                 ("1thread", 1, max(args.cpu_rays // 16, 50_000))):
+        def run():
+            o = orc.trace(E, R, tx, B, 0, rays, want_traced=True, nthreads=threads)
+            orc.cir_from_paths(orc.clean_paths(o["received"], o["mask"]), 1, rays, 2.998e8, 100e9, 100e-9)
+        med, ts = _median_runs(run, args.cpu_runs)
+        out[label] = {"value": rays * B / med, "unit": "ray-bounces/s", "cores": threads, "kind": "port",
+                      "sample": f"ray ids 0..{rays - 1} of the K2 room.stl burst ({rays} rays x {B} bounces): "
+                                f"trace (traced + received + row_mask) + host CIR, oracle/rt_oracle.c, "
+                                f"median of {args.cpu_runs} runs after 1 warm-up ({', '.join(f'{t:.2f}' for t in ts)} s)",
+                      "build": build, "host": info}
+    return out
 
 
+def cpu_baseline_k3(args, info):
+    """coverage.py:38-57 literally on the host for a seeded sample of K3 cells (full 1M-ray trace
+    with the cell's icosphere, the per-path host CIR of tracer.py:84-117, np.convolve power):
+    cells/s over the sample, median of cpu_runs.  Also the reference's np.convolve step alone."""
+    from oracle import oracle as orc
+    from rf_ray_tracing_warp_amd.coverage import CoverageGrid
+    from rf_ray_tracing_warp_amd.mesh import load_stl, sphere
+
+    env = load_stl(os.path.join(REPO, "models", "room.stl"))
+    E = orc.Mesh(env.vertices, env.faces)
+    grid = CoverageGrid.square(args.coverage_grid, 15.0, 5.0)
+    cells = np.random.default_rng(2).choice(grid.num_cells, args.cpu_cells, replace=False)
+    cen = grid.centers().reshape(-1, 3)[cells]
+    N, B, tx = args.coverage_rays, args.bounces, (10.0, 0.0, 5.0)
+
+    def run():
+        for c in cen:
+            rxm = sphere(c, 0.1, 1)
+            o = orc.trace(E, orc.Mesh(rxm.vertices, rxm.faces), tx, B, 0, N, want_traced=False,
+                          nthreads=info["threads_used"])
+            ir = orc.cir_from_paths(orc.clean_paths(o["received"], o["mask"]), 1, N, 2.998e8, 100e9, 100e-9)
+            orc.signal_power(ir, 100e-9)
+    med, ts = _median_runs(run, max(1, args.cpu_runs // 2))
+    ir = np.zeros(10000)
+    ir[[3000, 5000, 7000]] = 1e-6
+    conv, _ = _median_runs(lambda: orc.signal_power(ir, 100e-9), 5)
+    return {"value": len(cells) / med, "unit": "cells/s", "cores": info["threads_used"], "kind": "port",
+            "sample": f"{len(cells)} seeded K3 cells ({', '.join(str(int(c)) for c in cells)}), each the reference "
+                      f"loop body: {N}-ray trace with its icosphere + host CIR + np.convolve power; median of "
+                      f"{len(ts)} runs ({', '.join(f'{t:.2f}' for t in ts)} s)",
+            "np_convolve_power_ms_per_cell": conv * 1e3, "host": info}
+
+
+# ------------------------------------------------------------------ coverage legs
 def shard_desc(mode, world):
     if world == 1:
         return "1 GPU"
@@ -93,19 +186,32 @@ def shard_desc(mode, world):
     return f"cells sharded by x column (ix % {world}), every GPU traces all rays, RCCL sum of the power map"
 
 
-def coverage_leg(args, env_m, env, local, rank, world, dist):
-    """K3: coverage.py on room.stl, n x n cells at z = 5, tx (10,0,5), 1M rays per cell, 3 bounces.
-    N > 1: each rank traces 1/N of every cell's rays and sends its (cell, bin, amplitude) records to
-    the cells' owners (x columns, ix % world) in one RCCL all-to-all, or (--coverage-shard cells)
-    each rank computes its x columns from all rays; the power map is sum-reduced (RCCL)."""
-    import torch
-    from rf_ray_tracing_warp_amd.coverage import Coverage, CoverageGrid
+def _leg_traffic(kernel):
+    """HBM bytes per launch of `kernel` at the bench's default leg sizes, from the last PMC passes
+    (profiles/traffic_legs.json, tools/summarize_r2.py): a property of the code and the input."""
+    try:
+        with open(os.path.join(REPO, "profiles", "traffic_legs.json")) as fh:
+            t = json.load(fh).get(kernel)
+        return (t["hbm_bytes_per_launch"], t.get("l2_hit_rate"), t.get("source")) if t else (None, None, None)
+    except (OSError, ValueError, KeyError):
+        return None, None, None
 
-    grid = CoverageGrid.square(args.coverage_grid, 15.0, 5.0)
-    mode = args.coverage_shard if world > 1 else "cells"
-    cov = Coverage(env_m, 2.998e8, 100e9, 100e-9, args.bounces, args.coverage_rays, grid, 0.1, device=local,
-                   shard_index=rank, shard_count=world, env_mesh=env, shard_mode=mode)
-    tx = (10.0, 0.0, 5.0)
+
+def _roofline(kernel, ms, work, B, note, default_size=True):
+    if not (ms and ms > 0 and work):
+        return None
+    bpb = d4_bytes(B)
+    ach = work * bpb / (ms * 1e-3) / 1e9
+    traffic, l2, src = _leg_traffic(kernel) if default_size else (None, None, None)
+    return {"bound": "hbm", "kernel": kernel, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": ach / HBM_PEAK_GBS, "traffic": traffic, "l2_hit_rate": l2, "traffic_source": src,
+            "kernel_ms": ms, "ray_bounces": int(work), "bytes_per_ray_bounce": bpb,
+            "ray_bounces_per_s": work / (ms * 1e-3), "note": note}
+
+
+def run_coverage(cov, tx, runs, world, dist, local):
+    """Time `runs` maps (profiling off), then one profiled map for the stage breakdown."""
+    import torch
 
     def one():
         p = cov.run_device(tx, 1)
@@ -118,27 +224,57 @@ def coverage_leg(args, env_m, env, local, rank, world, dist):
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.coverage_runs):
+    for _ in range(runs):
         p = one()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    dt = (time.perf_counter() - t0) / args.coverage_runs
+    dt = (time.perf_counter() - t0) / runs
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t[0])
     pm = p.cpu().numpy()
-    cand = torch.tensor([float(cov.last_candidates)], dtype=torch.float64, device=f"cuda:{local}")
-    if world > 1:
-        dist.all_reduce(cand)
-    cov.close()
+    cov.profile(True)
+    one()
+    prof = cov.last_profile()
+    cov.profile(False)
+    return dt, pm, prof
+
+
+def coverage_block(name, cov, grid, dt, pm, prof, B, workload, world, mode, bvh, default_size):
+    t = "true" if bvh else "false"
+    traj = _roofline(f"k_traj<{t}>", prof["traj_ms"], prof["traced_ray_bounces"], B,
+                     "trajectory pass, D4 bytes over the actually traced ray-bounces (rays x segments)",
+                     default_size and world == 1)
+    rep = _roofline(f"k_replay<{t}>", prof["replay_ms"], prof["replayed_ray_bounces"], B,
+                    "first-win replay, D4 bytes over its ray-bounces (sum of B - k0 over first-win records)",
+                    default_size and world == 1)
     return {"metric": "coverage cells/sec", "value": grid.num_cells / dt, "unit": "cells/s", "ms_per_map": dt * 1e3,
-            "workload": f"K3: room.stl, {grid.nx}x{grid.ny} receivers at z=5 (centres -15+(i+1/2)*30/{grid.nx}), "
-                        f"tx (10,0,5), {args.coverage_rays} rays per cell, {args.bounces} bounces, 10000 bins, "
-                        f"signal power per cell; {shard_desc(mode, world)}",
-            "scaling": "strong", "cells_receiving": int(np.isfinite(pm).sum()),
-            "candidates": int(cand.item()), "algorithm": "exact shared-trajectory (csrc/coverage.hip)"}
+            "workload": workload + f"; {shard_desc(mode, world)}", "scaling": "strong",
+            "cells_receiving": int(np.isfinite(pm).sum()), "candidates": int(prof["candidates"]),
+            "first_win_records": int(prof["records"]),
+            "stage_ms": {k: prof[k] for k in ("traj_ms", "candidates_ms", "win_ms", "replay_ms", "reduce_power_ms",
+                                                "total_ms")},
+            "roofline": traj, "roofline_replay": rep,
+            "algorithm": "exact shared-trajectory (csrc/coverage.hip)", "name": name}
+
+
+def coverage_leg(args, env_m, env, local, rank, world, dist):
+    """K3: coverage.py on room.stl, n x n cells at z = 5, tx (10,0,5), 1M rays per cell, 3 bounces."""
+    from rf_ray_tracing_warp_amd.coverage import Coverage, CoverageGrid
+
+    grid = CoverageGrid.square(args.coverage_grid, 15.0, 5.0)
+    mode = args.coverage_shard if world > 1 else "cells"
+    cov = Coverage(env_m, 2.998e8, 100e9, 100e-9, args.bounces, args.coverage_rays, grid, 0.1, device=local,
+                   shard_index=rank, shard_count=world, env_mesh=env, shard_mode=mode)
+    dt, pm, prof = run_coverage(cov, (10.0, 0.0, 5.0), args.coverage_runs, world, dist, local)
+    cov.close()
+    return coverage_block("K3", cov, grid, dt, pm, prof, args.bounces,
+                          f"K3: room.stl, {grid.nx}x{grid.ny} receivers at z=5 (centres -15+(i+1/2)*30/{grid.nx}), "
+                          f"tx (10,0,5), {args.coverage_rays} rays per cell, {args.bounces} bounces, 10000 bins, "
+                          f"signal power per cell", world, mode, False,
+                          args.coverage_grid == 256 and args.coverage_rays == 1_000_000 and args.bounces == 3)
 
 
 def terrain_legs(args, local, rank, world, dist):
@@ -155,73 +291,75 @@ def terrain_legs(args, local, rank, world, dist):
     terr = synthetic_terrain(1024, 50.0)
     env = DeviceMesh(terr.vertices, terr.faces, local)
     t_build = time.perf_counter() - t_build
-    B, N = 5, args.k4_rays
-    P = B + 1
-    rxm = sphere((-10.125, 0.0, 4.8), 0.1, 1)
-    rx = DeviceMesh(rxm.vertices, rxm.faces, local)
-    tx = np.asarray((10.0, 0.0, 4.5), np.float32)
-    traced = torch.empty((N, P, 3), dtype=torch.float32, device=dev)
-    received = torch.empty((N, P, 3), dtype=torch.float32, device=dev)
-    mask = torch.empty(N, dtype=torch.int32, device=dev)
-    sh = torch.cuda.current_stream().cuda_stream
+    k4 = k5 = None
     L = lib()
+    if "k4" in args.legs:
+        B, N = 5, args.k4_rays
+        P = B + 1
+        rxm = sphere((-10.125, 0.0, 4.8), 0.1, 1)
+        rx = DeviceMesh(rxm.vertices, rxm.faces, local)
+        tx = np.asarray((10.0, 0.0, 4.5), np.float32)
+        traced = torch.empty((N, P, 3), dtype=torch.float32, device=dev)
+        received = torch.empty((N, P, 3), dtype=torch.float32, device=dev)
+        mask = torch.empty(N, dtype=torch.int32, device=dev)
+        sh = torch.cuda.current_stream().cuda_stream
 
-    def step():
-        check(L.rt_trace(env.handle, tx.ctypes.data, rx.handle, B, rank * N, N, ptr(traced), ptr(received), ptr(mask),
-                         None, None, sh), "rt_trace")
+        def step(kind=None):
+            check(L.rt_trace(env.handle, tx.ctypes.data, rx.handle, B, rank * N, N, ptr(traced), ptr(received),
+                             ptr(mask), ptr(kind), None, sh), "rt_trace")
 
-    step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    reps = 5
-    t0 = time.perf_counter()
-    for _ in range(reps):
         step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = (time.perf_counter() - t0) / reps
-    if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt[0])
-    k4 = {"metric": "ray-bounces/sec", "value": world * N * B / dt, "unit": "ray-bounces/s", "ms_per_step": dt * 1e3,
-          "workload": f"K4 on the declared apollo stand-in (synthetic terrain 1024^2 vertices, {len(terr.faces)} faces, "
-                      f"BVH), {N} rays/GPU x {world}, {B} bounces, traced+received+row_mask",
-          "scaling": "weak", "mesh_build_s": t_build}
-    del traced, received, mask
-    grid = CoverageGrid.square(args.k5_grid, 50.0, 2.0)
-    mode = args.coverage_shard if world > 1 else "cells"
-    cov = Coverage(terr, 2.998e8, 100e9, 200e-9, 3, args.k5_rays, grid, 0.1, device=local, shard_index=rank,
-                   shard_count=world, env_mesh=env, shard_mode=mode)
-
-    def one():
-        p = cov.run_device((10.0, 0.0, 4.5), 1)
+        torch.cuda.synchronize()
         if world > 1:
-            dist.all_reduce(p)
-        return p
-
-    one()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    p = one()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt[0])
-    pm = p.cpu().numpy()
-    k5 = {"metric": "coverage cells/sec", "value": grid.num_cells / dt, "unit": "cells/s", "ms_per_map": dt * 1e3,
-          "workload": f"K5 on the terrain stand-in: {grid.nx}x{grid.ny} receivers at z=2 over +-50 m, tx (10,0,4.5), "
-                      f"{args.k5_rays} rays per cell, 3 bounces, 20000 bins; {shard_desc(mode, world)}",
-          "scaling": "strong", "cells_receiving": int(np.isfinite(pm).sum()), "candidates": int(cov.last_candidates)}
-    cov.close()
+            dist.barrier()
+        reps = 5
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt = (time.perf_counter() - t0) / reps
+        if world > 1:
+            tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            dt = float(tt[0])
+        # one profiled launch (kernel and ray-order sort on HIP events), then the active ray-bounces
+        L.rt_profile(1)
+        step()
+        pr = np.zeros(2, np.float64)
+        check(L.rt_trace_last_profile(pr.ctypes.data, 2), "rt_trace_last_profile")
+        L.rt_profile(0)
+        kind = torch.empty((N, B), dtype=torch.int32, device=dev)
+        step(kind)
+        # iterations that issued a query: every env / RX hit plus each ray's first miss
+        active = int((kind != 0).sum().item()) + int((kind == 0).any(dim=1).sum().item())
+        roof = _roofline("k_trace_bvh<5>", float(pr[0]), N * B, B, "nominal N x B ray-bounces (D4), trace kernel "
+                         "alone (the ray-order sort is sort_ms); traffic: BVH node/leaf gathers (16-B lanes, FETCH_SIZE "
+                         "x2 not calibrated for gathers: the true bytes lie between traffic/2 and traffic)",
+                         N == 2_097_152 and world == 1)
+        if roof:
+            roof["sort_ms"] = float(pr[1])
+            roof["active_ray_bounces"] = active
+        k4 = {"metric": "ray-bounces/sec", "value": world * N * B / dt, "unit": "ray-bounces/s",
+              "ms_per_step": dt * 1e3,
+              "workload": f"K4 on the declared apollo stand-in (synthetic terrain 1024^2 vertices, {len(terr.faces)} "
+                          f"faces, BVH), {N} rays/GPU x {world}, {B} bounces, traced+received+row_mask",
+              "scaling": "weak", "mesh_build_s": t_build, "roofline": roof}
+        del traced, received, mask, kind
+        rx.close()
+    if "k5" in args.legs:
+        grid = CoverageGrid.square(args.k5_grid, 50.0, 2.0)
+        mode = args.coverage_shard if world > 1 else "cells"
+        cov = Coverage(terr, 2.998e8, 100e9, 200e-9, 3, args.k5_rays, grid, 0.1, device=local, shard_index=rank,
+                       shard_count=world, env_mesh=env, shard_mode=mode)
+        dt, pm, prof = run_coverage(cov, (10.0, 0.0, 4.5), args.k5_runs, world, dist, local)
+        cov.close()
+        k5 = coverage_block("K5", cov, grid, dt, pm, prof, 3,
+                            f"K5 on the terrain stand-in: {grid.nx}x{grid.ny} receivers at z=2 over +-50 m, "
+                            f"tx (10,0,4.5), {args.k5_rays} rays per cell, 3 bounces, 20000 bins", world, mode,
+                            True, args.k5_grid == 1024 and args.k5_rays == 1_000_000)
+    env.close()
     return k4, k5
 
 
@@ -247,7 +385,6 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=torch.device(dev))
 
-    from rf_ray_tracing_warp_amd import _lib
     from rf_ray_tracing_warp_amd._lib import DeviceMesh, check, lib, ptr
     from rf_ray_tracing_warp_amd.mesh import load_stl, sphere
     from rf_ray_tracing_warp_amd.tracer import cir_flags
@@ -329,12 +466,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
     received_rows = int(count.item())
+    del traced, received
 
-    cov_out = None
-    if not args.no_coverage:
-        cov_out = coverage_leg(args, env_m, env, local, rank, world, dist)
+    cov_out = coverage_leg(args, env_m, env, local, rank, world, dist) if "k3" in args.legs else None
     k4_out = k5_out = None
-    if not args.no_k4:
+    if args.legs & {"k4", "k5"}:
         k4_out, k5_out = terrain_legs(args, local, rank, world, dist)
 
     if rank == 0:
@@ -351,22 +487,24 @@ def main():
         except (OSError, ValueError):
             pass
         # the binding resource of the brute-force LDS kernel is the VALU issue rate: VALU
-        # instructions per launch come from a PMC pass (profiles/r1_k2_sq_counters.json, a
-        # property of the code and the input), the time from the live HIP events above
+        # instructions per launch come from a PMC pass (profiles/, a property of the code and the
+        # input), the time from the live HIP events above
         valu = None
         try:
-            with open(os.path.join(REPO, "profiles", "r1_k2_sq_counters.json")) as fh:
+            with open(os.path.join(REPO, "profiles", "k2_sq_counters.json")) as fh:
                 sq = json.load(fh)
             if N == 1_000_000 and B == 3:
                 rate = sq["SQ_INSTS_VALU"] / (kern_ms * 1e-3) / 1e9  # wave-instructions / ns
-                peak = VALU_PEAK_GWI
-                valu = {"bound": "valu", "achieved": rate, "peak": peak, "unit": "G wave-instr/s", "frac": rate / peak,
-                        "valu_instr_per_launch": sq["SQ_INSTS_VALU"],
+                valu = {"bound": "valu", "achieved": rate, "peak": VALU_PEAK_GWI, "unit": "G wave-instr/s",
+                        "frac": rate / VALU_PEAK_GWI, "valu_instr_per_launch": sq["SQ_INSTS_VALU"],
+                        "source": sq.get("source"),
                         "note": "peak = 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction"}
         except (OSError, ValueError, KeyError):
             pass
+        gpus = f"{world} GPU" + ("s" if world > 1 else "")
         out = {
-            "metric": METRIC,
+            "metric": f"ray-bounces/sec on room.stl ({gpus}, K2); coverage cells/sec ({gpus}) in 'coverage' (K3) "
+                      f"and 'k5_terrain_coverage' (K5)",
             "value": value,
             "unit": "ray-bounces/s",
             "n_gpus": world,
@@ -384,7 +522,7 @@ def main():
                        "parallelism": f"ray-id shards x{world}, RCCL all-reduce of the CIR"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_trace_bf<3>", "kernel_ms": kern_ms,
+                         "kernel": f"k_trace_bf<{B}>", "kernel_ms": kern_ms,
                          "algorithmic_bytes_per_launch": bytes_per_launch},
             "compute_roofline": valu,
             "received_rows_last_step": received_rows,
@@ -396,9 +534,14 @@ def main():
         if k5_out is not None:
             out["k5_terrain_coverage"] = k5_out
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_sample, B, tx, rx)
+            info = host_info()
+            build = native_oracle()
+            cb = cpu_baseline_k2(args, B, tx, rx, info, build)
+            out["cpu_baseline"] = cb["all"]
             # Warp's CPU launch is serial: the same restatement on one thread
-            out["cpu_baseline_1thread"] = cpu_baseline(args.cpu_sample // 4, B, tx, rx, min_s=3.0, threads=1)
+            out["cpu_baseline_1thread"] = cb["1thread"]
+            if cov_out is not None:
+                out["coverage"]["cpu_baseline"] = cpu_baseline_k3(args, info)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -150,6 +150,11 @@ int rt_power_dense(const double* impulse_responses, int64_t rows, int64_t n_bins
  * traced ray-bounces (trajectory segments), replayed ray-bounces (sum over first-win records of
  * B - k0), candidates and first-win records.  Unrecorded entries are NaN; synchronises. */
 int rt_coverage_profile(rt_coverage* cov, int enable);
+/* Process-wide rt_trace timing: rt_profile(1) records HIP events around every later rt_trace's
+ * trace kernel and (BVH meshes) its ray-order sort; rt_trace_last_profile fills out[0] = trace
+ * kernel ms, out[1] = ray-order sort ms (NaN when not recorded) of the last call; synchronises. */
+int rt_profile(int enable);
+int rt_trace_last_profile(double* out, int n);
 int rt_coverage_last_profile(rt_coverage* cov, double* out, int n);
 
 /* Self-test entry points used by the parity tests (not part of the reference surface). */

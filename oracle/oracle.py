@@ -32,6 +32,19 @@ def build():
     subprocess.run(["make", "-s", "-C", _HERE], check=True)
 
 
+def build_native(out_path):
+    """-O3 -march=native build for the CPU baseline, on the machine that times it."""
+    subprocess.run(["make", "-s", "-C", _HERE, "native", f"OUT={out_path}"], check=True)
+    return out_path
+
+
+def load(path):
+    """Use the oracle library at ``path`` (e.g. build_native's) for every later call."""
+    global _lib, _LIB_PATH
+    _lib, _LIB_PATH = None, path
+    return lib()
+
+
 def lib():
     global _lib
     if _lib is None:

@@ -68,6 +68,8 @@ def lib():
     L.rt_coverage_profile.argtypes = [_vp, _int]
     L.rt_coverage_last_profile.argtypes = [_vp, _vp, _int]
     L.rt_debug_poison.argtypes = [_int]
+    L.rt_profile.argtypes = [_int]
+    L.rt_trace_last_profile.argtypes = [_vp, _int]
     L.rt_selftest_math.argtypes = [_vp, _i64, _vp, _int, _vp]
     L.rt_ray_dirs.argtypes = [_i64, _i64, _vp, _vp]
     L.rt_query.argtypes = [_vp, _vp, _vp, _i64, _vp, _vp, _vp]
@@ -75,6 +77,7 @@ def lib():
                  "rt_coverage_create", "rt_coverage_destroy", "rt_coverage_run", "rt_coverage_received",
                  "rt_coverage_create_rays", "rt_coverage_trace_records", "rt_coverage_records",
                  "rt_coverage_power_records", "rt_coverage_profile", "rt_coverage_last_profile", "rt_debug_poison",
+                 "rt_profile", "rt_trace_last_profile",
                  "rt_power_dense", "rt_selftest_math", "rt_ray_dirs", "rt_query"):
         getattr(L, name).restype = _int
     _lib = L

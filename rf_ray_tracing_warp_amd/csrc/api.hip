@@ -46,6 +46,8 @@ __global__ void k_pack_leaf_refs(float4* nodes, const int2* leaves, int64_t nnod
 }
 
 int g_poison = -1;
+extern bool g_profile;                      // trace.hip
+int trace_last_profile(double* out, int n);  // trace.hip
 void keep_pool_memory();  // trace.hip
 
 int poison_pool(size_t bytes, hipStream_t s) {
@@ -75,6 +77,19 @@ extern "C" {
 const char* rt_last_error(void) { return rt::g_err.c_str(); }
 
 int rt_version(void) { return RFRT_VERSION; }
+
+int rt_profile(int enable) {
+  rt::g_profile = enable != 0;
+  return RT_OK;
+}
+
+int rt_trace_last_profile(double* out, int n) {
+  if (!out || n < 1) {
+    rt::set_error("rt_trace_last_profile: invalid arguments");
+    return RT_EINVAL;
+  }
+  return rt::trace_last_profile(out, n);
+}
 
 int rt_debug_poison(int byte) {
   if (byte > 255) {

@@ -346,6 +346,8 @@ const int32_t* dir_order(int64_t ray_offset, int64_t n, hipStream_t stream, void
   return r_out;
 }
 
+void trace_mark(int i, hipStream_t s);
+
 int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B, int64_t ray_offset, int64_t n,
                  float* traced, float* received, uint32_t* mask, int32_t* hit_kind, int32_t* hit_face,
                  hipStream_t stream) {
@@ -389,10 +391,12 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
     const int rc = poison_pool((size_t)256 << 20, stream);
     if (rc) return rc;
   }
+  trace_mark(0, stream);
   if (bvh && n >= kSortMinRays && n <= INT32_MAX) {
     a.order = dir_order(ray_offset, n, stream, &sort_ws);
     if (!a.order) return -1;
   }
+  trace_mark(1, stream);
   switch (B) {
 #define RT_CASE(BB)                                                                     \
   case BB:                                                                              \
@@ -411,7 +415,32 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
       break;
   }
   RT_HIP(hipGetLastError());
+  trace_mark(2, stream);
   if (sort_ws) RT_HIP(hipFreeAsync(sort_ws, stream));
+  return 0;
+}
+
+// rt_profile / rt_trace_last_profile: HIP events around the last rt_trace's ray-order sort and
+// trace kernel (process-wide, for measurement; not thread-safe)
+bool g_profile = false;
+static hipEvent_t g_tev[3] = {};
+static bool g_trec[3] = {};
+void trace_mark(int i, hipStream_t s) {
+  if (!g_profile) return;
+  if (!g_tev[i] && hipEventCreate(&g_tev[i]) != hipSuccess) return;
+  g_trec[i] = hipEventRecord(g_tev[i], s) == hipSuccess;
+}
+int trace_last_profile(double* out, int n) {
+  for (int i = 0; i < n; ++i) out[i] = NAN;
+  auto span = [](int a, int b) -> double {
+    float ms = 0.0f;
+    if (!g_trec[a] || !g_trec[b] || hipEventSynchronize(g_tev[b]) != hipSuccess ||
+        hipEventElapsedTime(&ms, g_tev[a], g_tev[b]) != hipSuccess)
+      return NAN;
+    return (double)ms;
+  };
+  if (n > 0) out[0] = span(1, 2);
+  if (n > 1) out[1] = span(0, 1);
   return 0;
 }
 
