@@ -17,12 +17,14 @@ import sys
 PKG = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
-OBJ = os.path.join(PKG, "_build")
-LIB = os.path.join(PKG, "librfrt.so")
+OBJ = os.environ.get("RFRT_BUILD_DIR") or os.path.join(PKG, "_build")
+LIB = os.environ.get("RFRT_LIB_OUT") or os.path.join(PKG, "librfrt.so")
 ARCH = os.environ.get("RFRT_ARCH", "gfx950")
 
+# RFRT_EXTRA_CFLAGS (with RFRT_BUILD_DIR / RFRT_LIB_OUT): A/B variant libraries, e.g. tools/cov_variants.py
 CFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-contract=off",
-          "-fno-fast-math", "-fno-slp-vectorize", "-Wall", "-Wno-unused-function", f"-I{os.path.join(REPO, 'include')}"]
+          "-fno-fast-math", "-fno-slp-vectorize", "-Wall", "-Wno-unused-function",
+          f"-I{os.path.join(REPO, 'include')}"] + os.environ.get("RFRT_EXTRA_CFLAGS", "").split()
 
 
 def hipcc() -> str:

@@ -11,7 +11,10 @@
 // (np.dot on float32 = f32-rounded products summed in double, rounded once; norm = sqrtf of
 // it), so bins match bit for bit.  The amplitude uses double acos/sin/asin/cos where the
 // reference uses NumPy's float32 arccos and Python's math: agreement ~1e-7 relative.
-// Accumulation uses a double atomic add (order differs from the host loop at ~1e-16).
+// Accumulation is deterministic and in the reference's order: k_cir writes every path's (bin,
+// amplitude) in ray order, then one workgroup applies impulse_response[bin] += amplitude chunk by
+// chunk, each bin's additions by a single lane in ray order (tracer.py:116-117 exactly; a double
+// atomic add gave run-to-run different last bits for bins with several paths).
 #include <math.h>
 
 #include "../../include/rfrt.h"
@@ -193,7 +196,37 @@ __device__ void cir_one(const float* received, const int64_t* index, int64_t k, 
   const int64_t bin = (int64_t)dl;  // int() truncates toward zero
   if (out_bin) out_bin[k] = (int32_t)(bin < 2147483647 ? bin : 2147483647);
   if (out_amp) out_amp[k] = amp;
-  if (ir && bin < n_bins) atomicAdd(ir + bin, amp);
+}
+
+// impulse_response[bin] += amp for paths k = 0 .. count-1 in order (tracer.py:116-117): chunks of
+// 1024 paths; in a chunk the first lane of each distinct bin adds that bin's amplitudes in path
+// order (bins of different lanes are distinct, so no two lanes touch one bin)
+__global__ __launch_bounds__(1024) void k_cir_accum(const int32_t* bins, const double* amps, const int64_t* count,
+                                                    int64_t n_bins, double* ir) {
+  __shared__ int32_t sb[1024];
+  __shared__ double sa[1024];
+  const int64_t cnt = *count;
+  const int t = threadIdx.x;
+  for (int64_t base = 0; base < cnt; base += 1024) {
+    const int64_t k = base + t;
+    const int32_t b = k < cnt ? bins[k] : -1;
+    sb[t] = (b >= 0 && b < n_bins) ? b : -1;
+    sa[t] = k < cnt ? amps[k] : 0.0;
+    __syncthreads();
+    const int32_t mb = sb[t];
+    if (mb >= 0) {
+      bool leader = true;
+      for (int j = 0; j < t && leader; ++j) leader = sb[j] != mb;
+      if (leader) {
+        const int m = (int)(cnt - base < 1024 ? cnt - base : 1024);
+        double v = ir[mb];
+        for (int j = t; j < m; ++j)
+          if (sb[j] == mb) v += sa[j];
+        ir[mb] = v;
+      }
+    }
+    __syncthreads();
+  }
 }
 
 }  // namespace
@@ -239,14 +272,28 @@ int rt_cir(const float* received, const int64_t* index, const int64_t* count, in
     return RT_EINVAL;
   }
   if (max_count == 0) return RT_OK;
+  hipStream_t s = (hipStream_t)stream;
+  // per-path (bin, amplitude): the caller's diagnostic outputs, or stream-ordered pool scratch
+  void* scratch = nullptr;
+  int32_t* bins = out_bin;
+  double* amps = out_amp;
+  if (impulse_response && (!bins || !amps)) {
+    rt::keep_pool_memory();
+    RT_HIP(hipMallocAsync(&scratch, (size_t)max_count * 12 + 16, s));
+    if (!amps) amps = (double*)scratch;
+    if (!bins) bins = (int32_t*)((char*)scratch + (size_t)max_count * 8);
+  }
   // the count is on the device and usually tiny (K2: ~1 row per 1M rays): one block per CU, a
   // grid-stride loop covers larger counts; empty blocks cost launch time, not work
   const int64_t want = (max_count + 255) / 256;
   const unsigned grid = (unsigned)(want < 256 ? want : 256);
-  hipLaunchKernelGGL(k_cir, dim3(grid), dim3(256), 0, (hipStream_t)stream, received, index, count, max_bounces + 1,
-                     amp0, (float)light_speed, (float)sample_rate, light_speed, sample_rate, flags, n_bins,
-                     impulse_response, out_bin, out_amp);
+  hipLaunchKernelGGL(k_cir, dim3(grid), dim3(256), 0, s, received, index, count, max_bounces + 1, amp0,
+                     (float)light_speed, (float)sample_rate, light_speed, sample_rate, flags, n_bins, nullptr, bins,
+                     amps);
+  if (impulse_response)
+    hipLaunchKernelGGL(k_cir_accum, dim3(1), dim3(1024), 0, s, bins, amps, count, n_bins, impulse_response);
   RT_HIP(hipGetLastError());
+  if (scratch) RT_HIP(hipFreeAsync(scratch, s));
   return RT_OK;
 }
 

@@ -285,22 +285,116 @@ __device__ __forceinline__ rt::Hit rx_query_grouped(const rt_grid& g, int64_t ce
   return h;
 }
 
+// ---- culled receiver query.  The 80 faces come in 20 groups of 4 (one subdivided icosahedron face
+// each, kIcoGroup), every group inside a ball (rt_ico1_gball, unit coordinates).  A face the
+// watertight test can accept has its triangle within rounding of the ray's line, so a group whose
+// ball (radius padded for the f32 vertex and test rounding) the line misses, or which lies wholly
+// behind the origin, holds no face that can be hit.  The passing groups are split at the line's
+// closest approach to the centre: the near side first; then a far group is needed only if its
+// ball's entry t is not beyond the best hit so far (a convex receiver is crossed at most twice, so
+// after a near-side hit the far side is usually skipped).  Each lane walks its own groups (~3 on
+// average, ~5 for the slowest lane of a wave, against 20 for the full test), with the group's
+// vertices computed as make_rx_perm computes them -- (float)(unit * r + centre) in double, the
+// products unit * r staged in LDS -- so every hit is bit-identical to rx_query's.
+struct RxLds {
+  double ur[RT_ICO1_NV][4];      // rt_ico1_v * r, the double product of make_rx_perm (w unused)
+  uint64_t vid[RT_ICO1_NF / 4];  // the group's vertex ids c0 c1 c2 m01 m12 m20, 6 bits each
+};
+__device__ __forceinline__ void stage_rx(RxLds& L, double r) {
+  for (int i = threadIdx.x; i < RT_ICO1_NV * 3; i += blockDim.x) L.ur[i / 3][i % 3] = rt_ico1_v[i / 3][i % 3] * r;
+  for (int g = threadIdx.x; g < RT_ICO1_NF / 4; g += blockDim.x) {
+    uint64_t w = 0;
+    for (int j = 0; j < 6; ++j) w |= (uint64_t)kIcoGroup.v[g][j] << (6 * j);
+    L.vid[g] = w;
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void rx_group(const RxLds& L, const double c[3], const rt::Shear& s, int gi, rt::Hit& h) {
+  const uint64_t w = L.vid[gi];
+  float3 v[6];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    const int vi = (int)((w >> (6 * j)) & 63);
+    const double2 xy = *reinterpret_cast<const double2*>(&L.ur[vi][0]);
+    const float x = (float)(xy.x + c[0]), y = (float)(xy.y + c[1]), z = (float)(L.ur[vi][2] + c[2]);
+    v[j] = make_float3(rt::pick(x, y, z, s.kx), rt::pick(x, y, z, s.ky), rt::pick(x, y, z, s.kz));
+  }
+#pragma unroll
+  for (int f = 0; f < 4; ++f) {
+    const float3 a = v[kGroupFace[f][0]], b = v[kGroupFace[f][1]], q = v[kGroupFace[f][2]];
+    float T, det;
+    if (rt::tri_test(s, make_float4(a.x, a.y, a.z, b.x), make_float4(b.y, b.z, q.x, q.y), q.z, T, det))
+      rt::hit_consider(h, T, det, 4 * gi + f);
+  }
+}
+
+__device__ __forceinline__ rt::Hit rx_query_culled(const RxLds& L, const rt_grid& g, int64_t cell, double r, float3 o,
+                                                   float3 d) {
+  const rt::Shear s = rt::make_shear(o, d);
+  double c[3];
+  cell_center(g, cell, c);
+  // line geometry in double: t0 = closest approach to the centre, u = centre -> that point
+  const double qx = c[0] - o.x, qy = c[1] - o.y, qz = c[2] - o.z;
+  const double dd = (double)d.x * d.x + (double)d.y * d.y + (double)d.z * d.z;
+  const double t0 = (qx * d.x + qy * d.y + qz * d.z) / dd;
+  const float ux = (float)(t0 * d.x - qx), uy = (float)(t0 * d.y - qy), uz = (float)(t0 * d.z - qz);
+  const float ddf = (float)dd, inv_dd = (float)(1.0 / dd), inv_len = (float)(1.0 / sqrt(dd)), t0f = (float)t0;
+  const float rf = (float)r;
+  // pad: f32 vertices (half an ulp of the coordinates) and the watertight test's rounding
+  const double amax = fmax(fmax(fabs(c[0]), fabs(c[1])), fmax(fabs(c[2]), fmax(fmax(fabs(o.x), fabs(o.y)), fabs(o.z))));
+  const float pad = (float)(1e-3 * r + 2e-5 * (1.0 + amax) + 4e-6 * fabs(t0) * sqrt(dd));
+  uint32_t near = 0, far = 0;
+  float far_tmin = INFINITY;
+#pragma unroll
+  for (int gi = 0; gi < RT_ICO1_NF / 4; ++gi) {
+    const float mx = rt_ico1_gball[gi][0] * rf, my = rt_ico1_gball[gi][1] * rf, mz = rt_ico1_gball[gi][2] * rf;
+    const float wx = mx - ux, wy = my - uy, wz = mz - uz;  // ball centre relative to the closest point
+    const float cx = wy * d.z - wz * d.y, cy = wz * d.x - wx * d.z, cz = wx * d.y - wy * d.x;
+    const float R = rt_ico1_gball[gi][3] * rf + pad;
+    const float tb = t0f + (mx * d.x + my * d.y + mz * d.z) * inv_dd;  // the ball centre's line parameter
+    const float half = R * inv_len;
+    const bool ok = (cx * cx + cy * cy + cz * cz <= R * R * ddf) && (tb + half >= 0.0f);
+    if (ok && tb <= t0f) near |= 1u << gi;
+    if (ok && tb > t0f) {
+      far |= 1u << gi;
+      far_tmin = fminf(far_tmin, tb - half);
+    }
+  }
+  rt::Hit h;
+  rt::hit_init(h);
+  while (near) {
+    const int gi = __builtin_ctz(near);
+    near &= near - 1;
+    rx_group(L, c, s, gi, h);
+  }
+  if (far_tmin > h.t) far = 0;  // every far face's t is beyond the near hit (ties kept)
+  while (far) {
+    const int gi = __builtin_ctz(far);
+    far &= far - 1;
+    rx_group(L, c, s, gi, h);
+  }
+  return h;
+}
+
 // receiver query used by the candidate test and the replay (A/B: RT_COV_RXQ 0 registers,
-// 1 per face, 2 grouped)
+// 1 per face, 2 grouped, 3 culled groups)
 #ifndef RT_COV_RXQ
-#define RT_COV_RXQ 2
+#define RT_COV_RXQ 3
 #endif
 #ifndef RT_COV_RXQ_BVH
-#define RT_COV_RXQ_BVH 2
+#define RT_COV_RXQ_BVH 3
 #endif
 #ifndef RT_COV_RXQ_WIN
-#define RT_COV_RXQ_WIN 2
+#define RT_COV_RXQ_WIN 3
 #endif
 template <int V>
-__device__ __forceinline__ rt::Hit rx_query_v(const rt_grid& g, int64_t cell, double r, float3 o, float3 d) {
+__device__ __forceinline__ rt::Hit rx_query_v(const RxLds& L, const rt_grid& g, int64_t cell, double r, float3 o,
+                                              float3 d) {
   if constexpr (V == 0) return rx_query(g, cell, r, o, d);
   else if constexpr (V == 1) return rx_query_lean(g, cell, r, o, d);
-  else return rx_query_grouped(g, cell, r, o, d);
+  else if constexpr (V == 2) return rx_query_grouped(g, cell, r, o, d);
+  else return rx_query_culled(L, g, cell, r, o, d);
 }
 
 // ------------------------------------------------------------------ 1. environment trajectories
@@ -611,9 +705,11 @@ __device__ __forceinline__ uint64_t record_key(const CovParams& p, int64_t cell,
 
 // Does the receiver of `cell` win bounce k of ray r (kernel.py:85: hit, and the environment missed
 // or is strictly farther)?  tr: the receiver's t.
-__device__ __forceinline__ bool rx_wins(const CovParams& p, int64_t cell, int64_t r, int k, float& tr) {
+__device__ __forceinline__ bool rx_wins(const CovParams& p, const RxLds& L, int64_t cell, int64_t r, int k,
+                                        float& tr) {
   const float4 tp = traj_p(p, r, k), td = traj_d(p, r, k);
-  const rt::Hit hr = rx_query_v<RT_COV_RXQ_WIN>(p.g, cell, p.r_rx, make_float3(tp.x, tp.y, tp.z), make_float3(td.x, td.y, td.z));
+  const rt::Hit hr = rx_query_v<RT_COV_RXQ_WIN>(L, p.g, cell, p.r_rx, make_float3(tp.x, tp.y, tp.z),
+                                                make_float3(td.x, td.y, td.z));
   tr = hr.t;
   return hr.face >= 0 && (isinf(tp.w) || tp.w > hr.t);
 }
@@ -627,8 +723,8 @@ __device__ __forceinline__ bool rx_wins(const CovParams& p, int64_t cell, int64_
 // semantics of kernel.py:57-98, then the CIR body of tracer.py:101-117: the record's key (~0 when
 // the path adds nothing: delay past the window, or amplitude 0) and amplitude.
 template <bool USE_BVH, bool RX_FIRST>
-__device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab, int64_t cell, int64_t r, int k0,
-                                       float tr, uint64_t& okey, double& oamp) {
+__device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab, const RxLds& L, int64_t cell,
+                                       int64_t r, int k0, float tr, uint64_t& okey, double& oamp) {
   PathAcc acc;
   const float4 t0 = traj_p(p, r, 0);
   acc.start(t0.x, t0.y, t0.z, p.amp0);  // p_0 = tx
@@ -654,14 +750,13 @@ __device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab
       // receiver first, then the environment culled at the receiver's t: every environment hit
       // with t <= hr.t is still found exactly (rt_bvh.h), and one beyond it loses to the receiver
       // whatever it is (kernel.py:85), so the decision and the chosen hit are unchanged
-      hr = rx_query_v<RT_COV_RXQ_BVH>(p.g, cell, p.r_rx, pos, d);
+      hr = USE_BVH ? rx_query_v<RT_COV_RXQ_BVH>(L, p.g, cell, p.r_rx, pos, d)
+                   : rx_query_v<RT_COV_RXQ>(L, p.g, cell, p.r_rx, pos, d);
       he = env_query<USE_BVH>(p, lds_tab, s, pos, d, hr.face >= 0 ? hr.t : RT_MAX_T);
     } else {
       he = env_query<USE_BVH>(p, lds_tab, s, pos, d);
-      // BVH scenes: the replay waits on node fetches, so occupancy (lean receiver) pays; on the
-      // LDS brute-force path it is VALU-bound and the register-held receiver is faster
-      hr = USE_BVH ? rx_query_v<RT_COV_RXQ_BVH>(p.g, cell, p.r_rx, pos, d)
-                   : rx_query_v<RT_COV_RXQ>(p.g, cell, p.r_rx, pos, d);
+      hr = USE_BVH ? rx_query_v<RT_COV_RXQ_BVH>(L, p.g, cell, p.r_rx, pos, d)
+                   : rx_query_v<RT_COV_RXQ>(L, p.g, cell, p.r_rx, pos, d);
     }
     const bool env_hit = he.face >= 0, rx_hit = hr.face >= 0;
     if (rx_hit && (!env_hit || he.t > hr.t)) {
@@ -708,6 +803,8 @@ __device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab
 // held every candidate's wave.)
 __global__ __launch_bounds__(256) void k_win(CovParams p, const uint64_t* keys, int64_t nkeys, uint8_t* first_flag,
                                              float* trx) {
+  __shared__ RxLds L;
+  stage_rx(L, p.r_rx);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nkeys; i += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t key = keys[i];
     const int64_t cell = (int64_t)(key >> 28), r = (int64_t)((key >> 4) & 0xFFFFFF);
@@ -726,7 +823,7 @@ __global__ __launch_bounds__(256) void k_win(CovParams p, const uint64_t* keys, 
         if (!seg_ball(sq.o, sq.d, sq.tmax, cc, rp2)) continue;
       }
       float t;
-      const bool w = rx_wins(p, cell, r, q, t);
+      const bool w = rx_wins(p, L, cell, r, q, t);
       if (q == k) {
         first = w;
         tr = t;
@@ -786,13 +883,15 @@ __global__ __launch_bounds__(256) void k_replay(CovParams p, const uint64_t* key
                                                 const int64_t* list, int64_t nl, const int32_t* order,
                                                 uint64_t* out_key, double* out_amp) {
   extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
+  __shared__ RxLds L;
+  stage_rx(L, p.r_rx);
   stage_env<USE_BVH>(p, lds_tab);
   for (int64_t jl = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; jl < nl; jl += (int64_t)gridDim.x * blockDim.x) {
     const int64_t li = order ? (int64_t)order[jl] : jl;
     const int64_t i = list[li];
     const uint64_t key = keys[i];
     const int64_t cell = (int64_t)(key >> 28), r = (int64_t)((key >> 4) & 0xFFFFFF);
-    replay<USE_BVH, RX_FIRST>(p, lds_tab, cell, r, (int)(key & 15), trx[i], out_key[li], out_amp[li]);
+    replay<USE_BVH, RX_FIRST>(p, lds_tab, L, cell, r, (int)(key & 15), trx[i], out_key[li], out_amp[li]);
   }
 }
 
@@ -1283,7 +1382,6 @@ void free_cands(rt_coverage* c) {
   c->cap = 0;
 }
 
-using WideIter = hipcub::TransformInputIterator<uint64_t, WideKey, const uint64_t*>;
 
 size_t rord_key_bytes(int64_t n) { return ((size_t)n * 2 + 255) / 256 * 256; }
 size_t rord_row_bytes(int64_t n) { return ((size_t)n * 4 + 255) / 256 * 256; }
@@ -1304,6 +1402,9 @@ hipError_t sort_records(void* tmp, size_t& bytes, const uint64_t* kin, uint64_t*
                                                    (unsigned)end_bit, s);
   return rocprim::radix_sort_pairs(tmp, bytes, kin, kout, vin, vout, (unsigned)n, 0u, (unsigned)end_bit, s);
 }
+
+hipError_t reduce_records(void* tmp, size_t& bytes, const uint64_t* keys, const double* amps, int64_t n, WideKey wk,
+                          uint64_t* ukeys, double* uamps, int64_t* nuniq, hipStream_t s);
 
 int alloc_cands(rt_coverage* c, int64_t cap) {
   free_cands(c);
@@ -1328,8 +1429,8 @@ int alloc_cands(rt_coverage* c, int64_t cap) {
   RT_HIP(sort_records(nullptr, b2m, c->okeys, c->okeys_sorted, c->oamps, c->oamps_sorted,
                       std::min<int64_t>(cap, kOnesweepMinItems - 1), 64, 0));
   b2 = std::max(b2, b2m);
-  RT_HIP(hipcub::DeviceReduce::ReduceByKey(nullptr, b3, WideIter(c->okeys_sorted, WideKey{0, 0, 0, 0}), c->ukeys,
-                                           c->oamps_sorted, c->uamps, c->nuniq, hipcub::Sum(), (int)cap));
+  RT_HIP(reduce_records(nullptr, b3, c->okeys_sorted, c->oamps_sorted, cap, WideKey{0, 0, 0, 0}, c->ukeys, c->uamps,
+                        c->nuniq, 0));
   RT_HIP(hipcub::DeviceSelect::Flagged(nullptr, b4, hipcub::CountingInputIterator<int64_t>(0), c->first_flag, c->list,
                                        (int64_t*)(c->counters + 2), (int)cap));
   c->tmp_bytes = std::max(std::max(b1, b2), std::max(b3, b4));
@@ -1398,11 +1499,12 @@ __global__ __launch_bounds__(256) void k_count_replay(const uint64_t* keys, cons
   if ((threadIdx.x & 63) == 0 && acc) atomicAdd(out, acc);
 }
 
-// BVH replay query order (A/B, RFRT_COV_RXFIRST=1: receiver first, environment culled at it)
+// replay query order: receiver first and the environment query culled at its t (default), or
+// the reference's order, environment then receiver (RFRT_COV_RXFIRST=0, for A/B checks)
 bool replay_rx_first() {
   static const bool v = [] {
     const char* e = getenv("RFRT_COV_RXFIRST");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   return v;
 }
@@ -1587,6 +1689,8 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
       RT_HIP(hipcub::DeviceRadixSort::SortPairs((char*)ws + 2 * kbs + 2 * rbs, cub_bytes, k_in, k_out, v_in, v_out,
                                                 (int)nlist, 0, 16, s));
       prof_mark(c, 4, s);
+      // BVH scenes: receiver first, the traversal culled at its t (K5 replay 3.47 -> 2.7 ms); the
+      // LDS brute force tests every face anyway (a plane-culled variant measured 5% slower on K3)
       if (bvh && replay_rx_first())
         hipLaunchKernelGGL((k_replay<true, true>), dim3(grid_l), dim3(256), 0, s, p, c->keys, c->trx, c->list, nlist,
                            v_out, c->okeys, c->oamps);
@@ -1610,9 +1714,22 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
 
 // Stable radix sort of n records on their low sort_bits key bits (compact record keys, ~0 =
 // dropped, sorting last thanks to one extra key bit), then the sum of every run of equal
-// (owner, cell, bin) -- runs of one bin arrive in ray order, the ray being the lowest key field,
-// so they are summed in ray order -- into c->ukeys (wide keys, wk) / c->uamps, count in c->nuniq.
-// keys/amps may be caller buffers (records from other ranks).
+// (owner, cell, bin) into c->ukeys (wide keys, wk) / c->uamps, count in c->nuniq.  Runs of one bin
+// arrive in ray order (the ray is the lowest key field).  The sums use rocPRIM's deterministic
+// reduce-by-key: its association is fixed by the record layout, so every run gives the same bits
+// run after run.  (hipcub::DeviceReduce::ReduceByKey, used in round 1, combines tile partials
+// through rocPRIM's non-deterministic decoupled look-back: a bin whose records span a tile
+// boundary -- the transmitter's cells put ~1M records in a few bins -- changed in the last bit from
+// run to run.  A one-thread-per-run sequential sum, the reference's exact order, took 11 ms on such
+// a run.  DESIGN.md §6.)  keys/amps may be caller buffers (records from other ranks).
+using WideIter = hipcub::TransformInputIterator<uint64_t, WideKey, const uint64_t*>;
+
+hipError_t reduce_records(void* tmp, size_t& bytes, const uint64_t* keys, const double* amps, int64_t n, WideKey wk,
+                          uint64_t* ukeys, double* uamps, int64_t* nuniq, hipStream_t s) {
+  return rocprim::deterministic_reduce_by_key(tmp, bytes, WideIter(keys, wk), amps, (size_t)n, ukeys, uamps, nuniq,
+                                              rocprim::plus<double>(), rocprim::equal_to<uint64_t>(), s);
+}
+
 int cov_reduce(rt_coverage* c, const uint64_t* keys, const double* amps, int64_t n, int sort_bits, WideKey wk,
                hipStream_t s) {
   if (n > c->cap) {  // records gathered from several ranks can outgrow this rank's candidate buffers
@@ -1622,8 +1739,7 @@ int cov_reduce(rt_coverage* c, const uint64_t* keys, const double* amps, int64_t
   size_t tb = c->tmp_bytes;
   RT_HIP(sort_records(c->tmp, tb, keys, c->okeys_sorted, amps, c->oamps_sorted, n, sort_bits < 64 ? sort_bits : 64, s));
   tb = c->tmp_bytes;
-  RT_HIP(hipcub::DeviceReduce::ReduceByKey(c->tmp, tb, WideIter(c->okeys_sorted, wk), c->ukeys, c->oamps_sorted,
-                                           c->uamps, c->nuniq, hipcub::Sum(), (int)n, s));
+  RT_HIP(reduce_records(c->tmp, tb, c->okeys_sorted, c->oamps_sorted, n, wk, c->ukeys, c->uamps, c->nuniq, s));
   return RT_OK;
 }
 

@@ -62,6 +62,8 @@ extern int g_poison;
 // fill `bytes` of a fresh stream-ordered allocation with the poison byte and free it back into the
 // pool (whose release threshold keeps it), so the next hipMallocAsync returns poisoned memory
 int poison_pool(size_t bytes, hipStream_t s);
+// keep freed blocks of the device's default memory pool across synchronizes (trace.hip)
+void keep_pool_memory();
 // Row order for tracing rays [ray_offset, ray_offset+n) of one burst sorted by initial direction
 // (trace.hip).  Stream-ordered workspace returned in *ws (hipFreeAsync it after the consumer).
 const int32_t* dir_order(int64_t ray_offset, int64_t n, hipStream_t stream, void** ws);

@@ -17,7 +17,8 @@ def child(cases, reps):
     from rf_ray_tracing_warp_amd._lib import DeviceMesh
     from rf_ray_tracing_warp_amd.coverage import Coverage, CoverageGrid
     from rf_ray_tracing_warp_amd.mesh import load_stl, synthetic_terrain
-    out = {"lib": os.path.basename(os.environ.get("RFRT_LIB_PATH", "librfrt.so"))}
+    out = {"lib": os.path.basename(os.environ.get("RFRT_LIB_PATH", "librfrt.so")),
+           "rxfirst": os.environ.get("RFRT_COV_RXFIRST", "1")}
     for case in cases:
         if case == "k3":
             m = load_stl(os.path.join(ROOT, "models/room.stl"))
@@ -50,8 +51,10 @@ if __name__ == "__main__":
     cases = os.environ.get("CASES", "k3,k5")
     reps = os.environ.get("REPS", "3")
     res = []
-    for lib in libs:
+    for spec in libs:  # path[@VAR=value,...]: per-variant environment (e.g. @RFRT_COV_RXFIRST=0)
+        lib, _, extra = spec.partition("@")
         env = dict(os.environ, RFRT_LIB_PATH=os.path.abspath(lib))
+        env.update(kv.split("=", 1) for kv in extra.split(",") if kv)
         r = subprocess.run([sys.executable, __file__, "child", cases, reps], env=env, capture_output=True, text=True,
                            timeout=600)
         if r.returncode != 0:
