@@ -201,6 +201,7 @@ int rt_mesh_create_ex(int device, const float* vertices, int64_t nv, const int32
     if (flags & RT_MESH_BVH_GPU) rc = rt::build_bvh_gpu(m, tri);  // 1: too deep for the stack
     if (rc == 1) rc = rt::build_bvh(m, tri);
     if (!rc) rc = rt::pack_leaf_refs(m);
+    if (!rc) rc = rt::build_wide(m);
     if (rc) {
       rt_mesh_destroy(m);
       return rc;
@@ -218,6 +219,7 @@ int rt_mesh_destroy(rt_mesh* m) {
   if (m->nodes) (void)hipFree(m->nodes);
   if (m->leaves) (void)hipFree(m->leaves);
   if (m->lcomp) (void)hipFree(m->lcomp);
+  if (m->wide) (void)hipFree(m->wide);
   delete m;
   return RT_OK;
 }

@@ -397,9 +397,21 @@ __device__ __forceinline__ rt::Hit rx_query_v(const RxLds& L, const rt_grid& g, 
   else return rx_query_culled(L, g, cell, r, o, d);
 }
 
+// Minimum waves per SIMD the coverage kernels are built for (launch bounds; 1 = register-unbounded).
+// Unbounded, k_traj<true> took 98 VGPRs (4 waves) and k_replay 201 (2 waves); 5 and 3 (96 and 168
+// VGPRs, ~100 B more spills in the replay) measured K5 6.06 -> 5.59 ms and K3 6.01 -> 5.60 ms per
+// map (k_replay<true> 2.50 -> 2.08 ms, k_replay<false> 3.03 -> 2.53 ms); 4 for the replay
+// (128 VGPRs, 200 B more spills) was no better.
+#ifndef RT_COV_TRAJ_WAVES
+#define RT_COV_TRAJ_WAVES 5
+#endif
+#ifndef RT_COV_REPLAY_WAVES
+#define RT_COV_REPLAY_WAVES 3
+#endif
+
 // ------------------------------------------------------------------ 1. environment trajectories
 template <bool USE_BVH>
-__global__ __launch_bounds__(256) void k_traj(CovParams p) {
+__global__ __launch_bounds__(256, RT_COV_TRAJ_WAVES) void k_traj(CovParams p) {
   extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
   stage_env<USE_BVH>(p, lds_tab);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -879,7 +891,7 @@ __global__ __launch_bounds__(256) void k_replay_keys(CovParams p, const uint64_t
 }
 
 template <bool USE_BVH, bool RX_FIRST>
-__global__ __launch_bounds__(256) void k_replay(CovParams p, const uint64_t* keys, const float* trx,
+__global__ __launch_bounds__(256, RT_COV_REPLAY_WAVES) void k_replay(CovParams p, const uint64_t* keys, const float* trx,
                                                 const int64_t* list, int64_t nl, const int32_t* order,
                                                 uint64_t* out_key, double* out_amp) {
   extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];

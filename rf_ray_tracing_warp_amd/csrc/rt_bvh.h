@@ -27,9 +27,14 @@ struct BvhView {
   const int2* leaves;
   const float4* lcomp;
   int nf;  // faces in lcomp
+  const float4* wide;  // 4-wide nodes (8 float4 each, see Walk4), collapsed from `nodes`
 };
 
 #define RT_BVH_STACK 64
+// 0: binary nodes (Walk2), 1: 4-wide nodes (Walk4, default: K4 trace 1438 -> 1277 us)
+#ifndef RT_BVH_WIDE
+#define RT_BVH_WIDE 1
+#endif
 
 struct RayBox {
   float ox, oy, oz, ix, iy, iz;  // origin and per-axis reciprocal direction (never 0/NaN)
@@ -90,76 +95,204 @@ __device__ __forceinline__ void leaf4(const BvhView& b, const Shear& s, int firs
   }
 }
 
-// closest hit in a BVH mesh (same result as brute force over all faces): near child first, far
-// child on a per-lane (node, entry t) stack, popped entries re-culled against the best t.
+__device__ __forceinline__ float cull_limit(const Hit& h, float tc) { return fminf(h.t, tc) * 1.00001f + 1e-6f; }
+
+// Closest hit in a BVH mesh, the same result as brute force over all faces, as a resumable walk:
+// init() for a ray, then step() until it returns false; h is then the (t, face) minimum.  One step
+// = one flat-loop iteration for every lane (pop, re-culled against the best t, and visit in the
+// same step; leaves tested on the spot from the (first, count) packed in their parent), so a wave
+// iterates as often as its longest lane.  (The nested-loop form -- descend, inner pop loop, inner
+// face loop -- made lanes wait for each other at every phase change: the slowest wave of a
+// 125k-ray K5 burst took 2.2x longer.)  Callers either loop step() (bvh_query) or interleave
+// steps of different rays and bounces in one loop (k_trace_pool).
+//
 // tcull < RT_MAX_T also culls boxes beyond tcull: every hit with t <= tcull is still found
 // exactly, hits beyond it may be missed (callers that only compare against tcull use it).
 //
-// One flat loop, one step per iteration for every lane: pop (re-culled) and visit happen in the
-// same step, leaves are tested on the spot from the (first, count) packed in their parent node,
-// so a wave iterates as often as its longest lane.  (The nested-loop form -- descend, inner
-// pop loop, inner face loop -- made lanes wait for each other at every phase change: the
-// slowest wave of a 125k-ray K5 burst took 2.2x longer.)
-__device__ __forceinline__ Hit bvh_query(const BvhView& b, const Shear& s, float3 o, float3 d,
-                                         float tcull = RT_MAX_T) {
+// The (node, entry t) stack is a private array: scratch memory.  Kept in LDS instead (12 entries
+// per lane, deeper ones private) it measured no faster on K4 (1431 vs 1454 us) or K5.
+
+// The (node, entry t) stack, kept apart from the walk's scalar state: inside one aggregate with
+// the dynamically indexed arrays, the scalars went to scratch too (k_traj<true> 92 -> 102 VGPRs
+// and +40 B scratch: cur, sp, the best hit and the ray box reloaded every step).
+struct WalkStack {
+  int node[RT_BVH_STACK];
+  float t[RT_BVH_STACK];
+};
+
+// binary nodes: near child first, far child pushed
+struct Walk2 {
   Hit h;
-  hit_init(h);
-  const float tc = fminf(RT_MAX_T, tcull);
-  const RayBox r = make_raybox(o, d);
-  int stack[RT_BVH_STACK];
-  float stackt[RT_BVH_STACK];
-  int sp = 0, cur = 0;
-  bool active = true;
-  while (active) {
+  RayBox r;
+  float tc;
+  int cur, sp;
+
+  __device__ __forceinline__ void init(float3 o, float3 d, float tcull = RT_MAX_T) {
+    hit_init(h);
+    tc = fminf(RT_MAX_T, tcull);
+    r = make_raybox(o, d);
+    cur = 0;
+    sp = 0;
+  }
+  __device__ __forceinline__ bool step(const BvhView& b, const Shear& s, WalkStack& st) {
     bool visit = true;
     if (cur < 0) {  // pop
-      if (sp == 0) {
-        active = false;
-        visit = false;
-      } else {
-        --sp;
-        if (stackt[sp] <= fminf(h.t, tc) * 1.00001f + 1e-6f) cur = stack[sp];
-        else visit = false;
-      }
+      if (sp == 0) return false;
+      --sp;
+      if (st.t[sp] <= cull_limit(h, tc)) cur = st.node[sp];
+      else visit = false;
     }
     if (visit) {
-      const float4 q0 = b.nodes[4 * cur + 0], q1 = b.nodes[4 * cur + 1];
-      const float4 q2 = b.nodes[4 * cur + 2], q3 = b.nodes[4 * cur + 3];
-      const int c0 = __float_as_int(q3.x), c1 = __float_as_int(q3.y);
-      float t0 = slab(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y);
-      float t1 = slab(r, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w);
+    const float4 q0 = b.nodes[4 * cur + 0], q1 = b.nodes[4 * cur + 1];
+    const float4 q2 = b.nodes[4 * cur + 2], q3 = b.nodes[4 * cur + 3];
+    const int c0 = __float_as_int(q3.x), c1 = __float_as_int(q3.y);
+    float t0 = slab(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y);
+    float t1 = slab(r, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w);
 #pragma unroll
-      for (int side = 0; side < 2; ++side) {
-        const int c = side ? c1 : c0;
-        float& tt = side ? t1 : t0;
-        if (c < 0) {  // leaf child: test its faces now
-          if (tt <= fminf(h.t, tc) * 1.00001f + 1e-6f) {
-            const int pk = __float_as_int(side ? q3.w : q3.z);
-            leaf4(b, s, pk >> 3, pk & 7, h);
-          }
-          tt = INFINITY;
+    for (int side = 0; side < 2; ++side) {
+      const int c = side ? c1 : c0;
+      float& tt = side ? t1 : t0;
+      if (c < 0) {  // leaf child: test its faces now
+        if (tt <= cull_limit(h, tc)) {
+          const int pk = __float_as_int(side ? q3.w : q3.z);
+          leaf4(b, s, pk >> 3, pk & 7, h);
         }
-      }
-      const float lim = fminf(h.t, tc) * 1.00001f + 1e-6f;
-      const bool h0 = t0 <= lim, h1 = t1 <= lim;
-      if (h0 && h1) {
-        const bool first0 = t0 <= t1;
-        if (sp < RT_BVH_STACK) {  // cannot overflow: tree depth <= RT_BVH_STACK - 4 (bvh.hip)
-          stack[sp] = first0 ? c1 : c0;
-          stackt[sp] = first0 ? t1 : t0;
-          ++sp;
-        }
-        cur = first0 ? c0 : c1;
-      } else if (h0) {
-        cur = c0;
-      } else if (h1) {
-        cur = c1;
-      } else {
-        cur = -1;
+        tt = INFINITY;
       }
     }
+    const float lim = cull_limit(h, tc);
+    const bool h0 = t0 <= lim, h1 = t1 <= lim;
+    if (h0 && h1) {
+      const bool first0 = t0 <= t1;
+      if (sp < RT_BVH_STACK) {  // cannot overflow: tree depth <= RT_BVH_STACK - 4 (bvh.hip)
+        st.node[sp] = first0 ? c1 : c0;
+        st.t[sp] = first0 ? t1 : t0;
+        ++sp;
+      }
+      cur = first0 ? c0 : c1;
+    } else {
+      cur = h0 ? c0 : (h1 ? c1 : -1);
+    }
+    }
+    return true;
   }
-  return h;
+};
+
+// 4-wide nodes (bvh_wide.hip collapses the binary tree, breadth first): 8 float4 = 128 B,
+//   w[0] lo.x[4]  w[1] hi.x[4]  w[2] lo.y[4]  w[3] hi.y[4]  w[4] lo.z[4]  w[5] hi.z[4]
+//   w[6] child refs (int bits): >= 0 wide node, -1 empty slot, <= -2 leaf ~(first << 3 | count)
+// The child boxes are the binary tree's own (rounded outward and padded), so culling stays
+// exactly as conservative as Walk2's and the (t, face) minimum cannot depend on the tree.
+// Per visit: four slab tests; the hit leaves tested on the spot, nearest first; the hit inner
+// children sorted by entry t, the nearest visited next and the others pushed far to near.
+// About half the dependent node fetches of the binary walk per query.  (The top 85 or 192 wide
+// nodes staged in LDS per workgroup measured slower, 1575 / 1603 vs 1522 us on K4 with the same
+// row mapping: every wave of a direction-sorted burst reads the same top nodes, which L1/L2 serve.)
+__device__ __forceinline__ void cas(float& ta, int& ra, float& tb, int& rb) {
+  const bool sw = tb < ta;
+  const float t0 = sw ? tb : ta, t1 = sw ? ta : tb;
+  const int r0 = sw ? rb : ra, r1 = sw ? ra : rb;
+  ta = t0;
+  tb = t1;
+  ra = r0;
+  rb = r1;
+}
+
+struct Walk4 {
+  Hit h;
+  RayBox r;
+  float tc;
+  int cur, sp;
+
+  __device__ __forceinline__ void init(float3 o, float3 d, float tcull = RT_MAX_T) {
+    hit_init(h);
+    tc = fminf(RT_MAX_T, tcull);
+    r = make_raybox(o, d);
+    cur = 0;
+    sp = 0;
+  }
+  __device__ __forceinline__ void push(WalkStack& st, int c, float t) {
+    if (sp < RT_BVH_STACK) {  // cannot overflow: bound checked on the host (build_wide)
+      st.node[sp] = c;
+      st.t[sp] = t;
+      ++sp;
+    }
+  }
+  __device__ __forceinline__ bool step(const BvhView& b, const Shear& s, WalkStack& st) {
+    bool visit = true;
+    if (cur < 0) {  // pop
+      if (sp == 0) return false;
+      --sp;
+      if (st.t[sp] <= cull_limit(h, tc)) cur = st.node[sp];
+      else visit = false;
+    }
+    if (visit) {
+    const float4* w = b.wide + 8 * (int64_t)cur;
+    const float4 lx = w[0], hx = w[1], ly = w[2], hy = w[3], lz = w[4], hz = w[5];
+    const float4 rf = w[6];
+    int c0 = __float_as_int(rf.x), c1 = __float_as_int(rf.y), c2 = __float_as_int(rf.z), c3 = __float_as_int(rf.w);
+    float t0 = slab(r, lx.x, ly.x, lz.x, hx.x, hy.x, hz.x);
+    float t1 = slab(r, lx.y, ly.y, lz.y, hx.y, hy.y, hz.y);
+    float t2 = slab(r, lx.z, ly.z, lz.z, hx.z, hy.z, hz.z);
+    float t3 = slab(r, lx.w, ly.w, lz.w, hx.w, hy.w, hz.w);
+    // leaves (and empty slots) leave the ordering; hit leaves are tested now, nearest first
+    float l0 = c0 < -1 ? t0 : INFINITY, l1 = c1 < -1 ? t1 : INFINITY;
+    float l2 = c2 < -1 ? t2 : INFINITY, l3 = c3 < -1 ? t3 : INFINITY;
+    int p0 = ~c0, p1 = ~c1, p2 = ~c2, p3 = ~c3;
+    t0 = c0 >= 0 ? t0 : INFINITY;
+    t1 = c1 >= 0 ? t1 : INFINITY;
+    t2 = c2 >= 0 ? t2 : INFINITY;
+    t3 = c3 >= 0 ? t3 : INFINITY;
+    cas(l0, p0, l1, p1);
+    cas(l2, p2, l3, p3);
+    cas(l0, p0, l2, p2);
+    cas(l1, p1, l3, p3);
+    cas(l1, p1, l2, p2);
+#pragma unroll 1
+    for (int q = 0; q < 4; ++q) {  // one leaf4 body in the code; the sorted list shifts down
+      if (!(l0 <= cull_limit(h, tc))) break;
+      leaf4(b, s, p0 >> 3, p0 & 7, h);
+      l0 = l1;
+      l1 = l2;
+      l2 = l3;
+      l3 = INFINITY;
+      p0 = p1;
+      p1 = p2;
+      p2 = p3;
+    }
+    cas(t0, c0, t1, c1);
+    cas(t2, c2, t3, c3);
+    cas(t0, c0, t2, c2);
+    cas(t1, c1, t3, c3);
+    cas(t1, c1, t2, c2);
+    const float lim = cull_limit(h, tc);
+    if (t0 <= lim) {  // far to near, so the nearest of the rest is popped first
+      if (t3 <= lim) push(st, c3, t3);
+      if (t2 <= lim) push(st, c2, t2);
+      if (t1 <= lim) push(st, c1, t1);
+      cur = c0;
+    } else {
+      cur = -1;
+    }
+    }
+    return true;
+  }
+};
+
+#if RT_BVH_WIDE
+using Walk = Walk4;
+#else
+using Walk = Walk2;
+#endif
+
+__device__ __forceinline__ Hit bvh_query(const BvhView& b, const Shear& s, float3 o, float3 d,
+                                         float tcull = RT_MAX_T) {
+  Walk w;
+  WalkStack st;
+  w.init(o, d, tcull);
+  bool active = true;
+  while (active) active = w.step(b, s, st);
+  return w.h;
 }
 
 }  // namespace rt

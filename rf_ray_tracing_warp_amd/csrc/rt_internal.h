@@ -28,8 +28,9 @@ struct rt_mesh {
   float* nodes = nullptr;  // [nnodes][16]
   int* leaves = nullptr;   // [nleaves][2] (first, count)
   float* lcomp = nullptr;  // leaf-ordered compact faces: 3 float4 (a.xyz b.x)(b.yz c.xy)(c.z, face bits, 0, 0)
-  int64_t nnodes = 0, nleaves = 0;
-  int bvh_depth = 0, bvh_max_leaf = 0;
+  float* wide = nullptr;   // [nwide][32] 4-wide nodes collapsed from `nodes` (bvh_wide.hip)
+  int64_t nnodes = 0, nleaves = 0, nwide = 0;
+  int bvh_depth = 0, bvh_max_leaf = 0, wide_stack = 0;
 };
 
 namespace rt {
@@ -69,11 +70,14 @@ void keep_pool_memory();
 const int32_t* dir_order(int64_t ray_offset, int64_t n, hipStream_t stream, void** ws);
 // Device view of a mesh's BVH for rt::bvh_query
 inline BvhView bvh_view(const rt_mesh* m) {
-  return BvhView{(const float4*)m->nodes, (const int2*)m->leaves, (const float4*)m->lcomp, (int)m->nf};
+  return BvhView{(const float4*)m->nodes, (const int2*)m->leaves, (const float4*)m->lcomp, (int)m->nf,
+                 (const float4*)m->wide};
 }
 // After either builder: copy each leaf child's (first, count) into its parent node (q3.z/q3.w,
 // first << 3 | count), the form bvh_query reads (api.hip)
 int pack_leaf_refs(rt_mesh* m);
+// After pack_leaf_refs: the 4-wide copy of the tree that rt::bvh4_query traverses (bvh_wide.hip)
+int build_wide(rt_mesh* m);
 }  // namespace rt
 
 #define RT_HIP(call)                                                   \

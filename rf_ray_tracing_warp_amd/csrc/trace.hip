@@ -14,6 +14,8 @@
 #include <math.h>
 
 #include <hipcub/hipcub.hpp>
+#include <algorithm>
+#include <cstdlib>
 #include <mutex>
 
 #include "rt_bvh.h"
@@ -189,9 +191,11 @@ __global__ __launch_bounds__(256) void k_trace_bf(TraceArgs a) {
   trace_body<B, USE_BVH>(a);
 }
 // BVH meshes: traversal is latency-bound (dependent node fetches), so the kernel is built for
-// RT_BVH_WAVES waves per SIMD
+// RT_BVH_WAVES waves per SIMD.  4 (128 VGPRs, no spills beyond the walk stack) beat 6 (80 VGPRs,
+// the path and walk state spilled inside the traversal loop): K4 1416 -> 1077 us per rt_trace
+// with the 4-wide walk; 3 (132 VGPRs) measured 1141 us.
 #ifndef RT_BVH_WAVES
-#define RT_BVH_WAVES 6
+#define RT_BVH_WAVES 4
 #endif
 template <int B>
 __global__ __launch_bounds__(256, RT_BVH_WAVES) void k_trace_bvh(TraceArgs a) {
@@ -398,12 +402,12 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
   }
   trace_mark(1, stream);
   switch (B) {
-#define RT_CASE(BB)                                                                     \
-  case BB:                                                                              \
-    if (bvh)                                                                            \
-      hipLaunchKernelGGL((k_trace_bvh<BB>), dim3(grid), blk, lds, stream, a);           \
-    else                                                                                \
-      hipLaunchKernelGGL((k_trace_bf<BB, false>), dim3(grid), blk, lds, stream, a);     \
+#define RT_CASE(BB)                                                                             \
+  case BB:                                                                                      \
+    if (bvh)                                                                                    \
+      hipLaunchKernelGGL((k_trace_bvh<BB>), dim3(grid), blk, lds, stream, a);                   \
+    else                                                                                        \
+      hipLaunchKernelGGL((k_trace_bf<BB, false>), dim3(grid), blk, lds, stream, a);             \
     break;
     RT_CASE(1) RT_CASE(2) RT_CASE(3) RT_CASE(4) RT_CASE(5) RT_CASE(6) RT_CASE(7) RT_CASE(8)
 #undef RT_CASE

@@ -37,7 +37,12 @@ def child(cases, reps):
         dt = (time.perf_counter() - t0) / reps
         c, b, a = cov.impulse_responses()
         h = hashlib.sha256(p.cpu().numpy().tobytes() + c.tobytes() + b.tobytes() + a.tobytes()).hexdigest()[:16]
-        out[case] = {"ms": round(dt * 1e3, 3), "hash": h}
+        cov.profile(True)
+        cov.run_device(tx)
+        pr = cov.last_profile()
+        cov.profile(False)
+        out[case] = {"ms": round(dt * 1e3, 3), "hash": h,
+                     "stages": {k: round(v, 3) for k, v in pr.items() if k.endswith("_ms")}}
         cov.close()
         env.close()
     print(json.dumps(out), flush=True)

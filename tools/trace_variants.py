@@ -48,6 +48,7 @@ def child(n, B, reps, scene="room"):
     e1.record(st)
     torch.cuda.synchronize()
     print(json.dumps({"variant": os.environ.get(os.environ.get("VAR_ENV", "RFRT_TRACE_VARIANT"), "0"),
+                      "lib": os.path.basename(os.environ.get("RFRT_LIB_PATH", "librfrt.so")),
                       "us": e0.elapsed_time(e1) * 1e3 / reps, "hash": h[:16], "bvh": env.bvh_info()}))
 
 
@@ -55,11 +56,18 @@ if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "child":
         child(int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), sys.argv[5])
         sys.exit(0)
-    variants = os.environ.get("VARIANTS", "0 1 3").split()
+    # LIBS="a.so b.so": one child per library (RFRT_LIB_PATH); else VARIANTS of one env switch
+    libs = os.environ.get("LIBS", "").split()
+    variants = libs or os.environ.get("VARIANTS", "0 1 3").split()
     res = []
     for v in variants:
         env = dict(os.environ)
-        env[os.environ.get("VAR_ENV", "RFRT_TRACE_VARIANT")] = v
+        if libs:  # path[@VAR=value,...]: per-variant environment (e.g. @RFRT_COV_RXFIRST=0)
+            lib, _, extra = v.partition("@")
+            env["RFRT_LIB_PATH"] = os.path.abspath(lib)
+            env.update(kv.split("=", 1) for kv in extra.split(",") if kv)
+        else:
+            env[os.environ.get("VAR_ENV", "RFRT_TRACE_VARIANT")] = v
         scene = os.environ.get("SCENE", "room")
         n, B, reps = ("2097152", "5", "5") if scene == "terrain" else ("1000000", "3", "50")
         out = subprocess.run([sys.executable, __file__, "child", n, B, reps, scene], env=env, capture_output=True,
