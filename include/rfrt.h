@@ -112,11 +112,13 @@ int rt_coverage_run(rt_coverage* cov, const float* tx_pos, double tx_power, doub
 /* ---- ray-sharded coverage (multi-GPU, SURVEY §8 E1 with F2): rank r of `world` traces global ray
  * ids [ray_offset, ray_offset + n_rays) of a burst of n_rays_total rays per cell (amplitude
  * tx_power / n_rays_total, tracer.py:103) for EVERY cell, sums its first-win records per
- * (cell, bin) in ray order, and sends each cell's records to the cell's owner, the rank with
- * ix % world == rank (ix = cell % nx).  The owner sums the runs it receives (in rank order, i.e.
- * ray order) and computes the power of its cells.  Replaces the per-cell loop of coverage.py:38-57
- * split over ranks; every rank's trajectory, candidate and replay work shrinks with the rank
- * count, and the exchange is a sparse all-to-all of (cell, bin, amplitude) records.
+ * (cell, bin), and sends each cell's records to the cell's owner, the rank with ix % world == rank
+ * (ix = cell % nx).  The owner sums the records it receives and computes the power of its cells.
+ * Replaces the per-cell loop of coverage.py:38-57 split over ranks; every rank's trajectory,
+ * candidate and replay work shrinks with the rank count, and the exchange is a sparse all-to-all
+ * of (cell, bin, sum) records.  Sums are exact: 192-bit unsigned fixed point, unit 2^-136, three
+ * uint64 per record (least significant first), rounded once to f64 by the owner, so the map does
+ * not depend on the rank count or on the order in which records arrive.
  *   1. rt_coverage_create_rays                         (once)
  *   2. rt_coverage_trace_records -> counts[world]      (records for each destination rank; syncs)
  *   3. rt_coverage_records -> caller device buffers    (grouped by destination, rank 0 first)
@@ -129,10 +131,14 @@ int rt_coverage_create_rays(int device, const rt_mesh* env, int max_bounces, int
 int rt_coverage_trace_records(rt_coverage* cov, const float* tx_pos, double tx_power, double light_speed,
                               double sample_rate, int flags, int64_t n_bins, int64_t* counts, int64_t* stats,
                               void* stream);
-/* keys_out (cell << 32 | bin), amps_out: device, max_out >= sum(counts). */
-int rt_coverage_records(rt_coverage* cov, uint64_t* keys_out, double* amps_out, int64_t max_out, void* stream);
-int rt_coverage_power_records(rt_coverage* cov, const uint64_t* keys, const double* amps, int64_t n, int64_t n_bins,
+/* keys_out (cell << 32 | bin), sums_out (3 uint64 per record): device, max_out >= sum(counts). */
+int rt_coverage_records(rt_coverage* cov, uint64_t* keys_out, uint64_t* sums_out, int64_t max_out, void* stream);
+/* keys (cell << 32 | bin) and sums (3 uint64 per record) received from every rank, in any order. */
+int rt_coverage_power_records(rt_coverage* cov, const uint64_t* keys, const uint64_t* sums, int64_t n, int64_t n_bins,
                               double alpha, double* power, void* stream);
+/* f64 amplitudes (finite, >= 0, below 2^56) -> the exact fixed-point sums of rt_coverage_records
+ * (truncated below 2^-136), on the device. */
+int rt_coverage_amps_to_sums(const double* amps, int64_t n, uint64_t* sums, void* stream);
 /* Sparse per-cell impulse responses of the last rt_coverage_run (or, ray-sharded, of this rank's cells
  * after rt_coverage_power_records): keys (cell << 32 | bin) ascending, amplitudes. */
 int rt_coverage_received(rt_coverage* cov, uint64_t* keys_out, double* amps_out, int64_t max_out, int64_t* n_out,

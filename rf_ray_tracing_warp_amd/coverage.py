@@ -139,13 +139,14 @@ class Coverage:
                                            ctypes.byref(self._h)), "rt_coverage_create")
         self.power = torch.empty(grid.num_cells, dtype=torch.float64, device=f"cuda:{self.device}")
         self.last_candidates = 0
-        self._rec = None  # ray mode: (keys, amps) record buffers of trace_records
+        self._rec = None  # ray mode: (keys, sums) record buffers of trace_records
 
     def trace_records(self, tx_pos, tx_power=1):
-        """Ray mode, stage 1: this rank's rays for every cell.  Returns (keys, amps, counts): device
-        int64 keys (cell << 32 | bin) and float64 amplitudes summed per (cell, bin) over this rank's
-        rays, grouped by owner rank, counts[d] records for rank d.  The tensors are views of this
-        plan's buffers, overwritten by its next trace_records call."""
+        """Ray mode, stage 1: this rank's rays for every cell.  Returns (keys, sums, counts): device
+        int64 keys (cell << 32 | bin) and the amplitudes summed per (cell, bin) over this rank's rays
+        as exact fixed point ((n, 3) int64: 192-bit unsigned, unit 2^-136, least significant word
+        first; include/rfrt.h), grouped by owner rank, counts[d] records for rank d.  The tensors are
+        views of this plan's buffers, overwritten by its next trace_records call."""
         import torch
 
         if self.shard_mode != "rays":
@@ -165,21 +166,29 @@ class Coverage:
         if self._rec is None or self._rec[0].numel() < max(n, 1):
             dev = f"cuda:{self.device}"
             m = max(n + n // 4, 1024)
-            self._rec = (torch.empty(m, dtype=torch.int64, device=dev), torch.empty(m, dtype=torch.float64, device=dev))
-        keys, amps = self._rec
-        check(lib().rt_coverage_records(self._h, ptr(keys), ptr(amps), n, _lib.stream_handle(self.device)),
+            self._rec = (torch.empty(m, dtype=torch.int64, device=dev), torch.empty((m, 3), dtype=torch.int64, device=dev))
+        keys, sums = self._rec
+        check(lib().rt_coverage_records(self._h, ptr(keys), ptr(sums), n, _lib.stream_handle(self.device)),
               "rt_coverage_records")
-        return keys[:n], amps[:n], [int(c) for c in counts]
+        return keys[:n], sums[:n], [int(c) for c in counts]
 
-    def power_from_records(self, keys, amps):
+    def power_from_records(self, keys, sums):
         """Ray mode, last stage: the power of this rank's cells from the records every rank sent it
-        (concatenated in source-rank order); the (num_cells,) float64 device map, 0 elsewhere."""
+        (keys and (n, 3) fixed-point sums, any order); the (num_cells,) float64 device map, 0
+        elsewhere."""
         n = int(keys.numel())
-        check(lib().rt_coverage_power_records(self._h, ptr(keys) if n else None, ptr(amps) if n else None, n,
+        if n and tuple(sums.shape) != (n, 3):
+            raise ValueError(f"sums must be (n, 3) int64 fixed point, got {tuple(sums.shape)}")
+        check(lib().rt_coverage_power_records(self._h, ptr(keys) if n else None, ptr(sums) if n else None, n,
                                               self.n_bins, phase_step(self.sample_window_s, self.n_bins),
                                               ptr(self.power), _lib.stream_handle(self.device)),
               "rt_coverage_power_records")
         return self.power
+
+    def power_from_amplitudes(self, keys, amps):
+        """power_from_records for float64 amplitudes (e.g. per-cell impulse responses computed
+        elsewhere): converted exactly to the fixed-point sums on the device first."""
+        return self.power_from_records(keys, amps_to_sums(amps))
 
     def run_device(self, tx_pos, tx_power=1, process_group=None):
         """Launch; returns the (num_cells,) float64 device tensor (0 for cells of other shards).
@@ -190,10 +199,10 @@ class Coverage:
 
     def _run_device(self, tx_pos, tx_power, process_group):
         if self.shard_mode == "rays":
-            keys, amps, counts = self.trace_records(tx_pos, tx_power)
+            keys, sums, counts = self.trace_records(tx_pos, tx_power)
             if self.shard_count > 1:
-                keys, amps = rdist.exchange_records(keys, amps, counts, process_group)
-            return self.power_from_records(keys, amps)
+                keys, sums = rdist.exchange_records(keys, sums, counts, process_group)
+            return self.power_from_records(keys, sums)
         tx = np.ascontiguousarray(np.asarray(tx_pos, dtype=np.float64).astype(np.float32))
         stats = np.zeros(2, np.int64)
         check(lib().rt_coverage_run(self._h, tx.ctypes.data, float(tx_power), float(self.light_speed_mps),
@@ -253,6 +262,18 @@ class Coverage:
 
     def __del__(self):
         self.close()
+
+
+def amps_to_sums(amps):
+    """float64 device amplitudes (finite, >= 0) -> (n, 3) int64 exact fixed-point sums
+    (rt_coverage_amps_to_sums: 192-bit unsigned, unit 2^-136)."""
+    import torch
+    n = int(amps.numel())
+    sums = torch.empty((max(n, 1), 3), dtype=torch.int64, device=amps.device)
+    a = amps.contiguous().to(torch.float64)
+    check(lib().rt_coverage_amps_to_sums(ptr(a) if n else None, n, ptr(sums) if n else None,
+                                         _lib.stream_handle(amps.device.index)), "rt_coverage_amps_to_sums")
+    return sums[:n]
 
 
 def coverage_points(power_map, grid: CoverageGrid):

@@ -77,7 +77,7 @@ struct CovParams {
   // record keys (record_key): ray-sharded runs put the owning rank of the record's cell
   // ((cell % nx) % own_world) above the cell, so one sort groups the records by destination
   int own_world, own_shift;
-  int ray_bits, bin_bits, cell_bits;
+  int bin_bits, cell_bits;
 };
 __device__ __forceinline__ float4 traj_p(const CovParams& p, int64_t r, int k) { return p.traj[2 * (r * p.B + k)]; }
 __device__ __forceinline__ float4 traj_d(const CovParams& p, int64_t r, int k) { return p.traj[2 * (r * p.B + k) + 1]; }
@@ -707,12 +707,12 @@ struct PathAcc {
 };
 
 // ------------------------------------------------------------------ 3-4. receiver test, first win, replay
-// Record key (compact): [owner | cell | bin | ray] with the field widths of CovParams.  Sorting it
-// groups the records by destination rank, then (cell, bin), and within a bin puts them in ray
-// order -- the order of tracer.py:116's accumulation -- whatever order the candidates came in.
-__device__ __forceinline__ uint64_t record_key(const CovParams& p, int64_t cell, int64_t bin, int64_t r) {
+// Record key (compact): [owner | cell | bin] with the field widths of CovParams.  Sorting it groups
+// the records by destination rank, then (cell, bin); the bins are summed exactly (Fx192), so the
+// order of the records within a bin -- tracer.py:116 adds them in ray order -- cannot matter.
+__device__ __forceinline__ uint64_t record_key(const CovParams& p, int64_t cell, int64_t bin) {
   const uint64_t own = p.own_world > 1 ? (uint64_t)((cell % p.g.nx) % p.own_world) : 0ull;
-  return (((own << p.cell_bits | (uint64_t)cell) << p.bin_bits | (uint64_t)bin) << p.ray_bits) | (uint64_t)r;
+  return (own << p.cell_bits | (uint64_t)cell) << p.bin_bits | (uint64_t)bin;
 }
 
 // Does the receiver of `cell` win bounce k of ray r (kernel.py:85: hit, and the environment missed
@@ -804,7 +804,7 @@ __device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab
   // amplitudes are >= 0; a zero one (NaN angle -> _bounce_amplitude 0, tracer.py:35-37) leaves
   // impulse_response[bin] untouched, so it must not become an active bin of the power sweep
   const bool keep = bin < p.n_bins && rec_amp != 0.0;
-  okey = keep ? record_key(p, cell, bin, r) : ~0ull;
+  okey = keep ? record_key(p, cell, bin) : ~0ull;
   oamp = keep ? rec_amp : 0.0;
 }
 
@@ -1114,15 +1114,37 @@ constexpr int kPowSmall = 16;  // cells with at most this many terms: one thread
 
 // cells of ours with 0..kPowSmall terms: one thread per cell, serial sweep (most cells of a large
 // map receive a handful of bins; a wave per such cell costs more than its whole sweep)
+// Larger cells are listed (big[], count in *nbig; one atomic per wave) for k_power, which then
+// visits only them (it used to stride over every cell of the map to skip the small ones: 1M cell
+// ranges read per K5 map for a few thousand large cells).
 __global__ __launch_bounds__(256) void k_power_small(TermArrays G, const int32_t* cstart, const int32_t* cend, rt_grid g,
-                                                     int shard, int nshard, PowerParams P, double* power) {
+                                                     int shard, int nshard, PowerParams P, double* power, int32_t* big,
+                                                     unsigned* nbig) {
   const int64_t nxo = g.nx > shard ? (g.nx - shard + nshard - 1) / nshard : 0;
   const int64_t nown = nxo * g.ny * g.nz;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nown; t += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t jx = t % nxo, rest = t / nxo;
-    const int64_t c = rest * g.nx + shard + jx * nshard;
-    const int64_t lo = cstart[c], hi = cend[c];
-    if (hi - lo <= kPowSmall) power[c] = power_sparse(lo, hi, P, G);  // NaN when empty
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int lane = threadIdx.x & 63;
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); base < nown; base += stride) {
+    const int64_t t = base + lane;
+    bool is_big = false;
+    int64_t c = 0;
+    if (t < nown) {
+      const int64_t jx = t % nxo, rest = t / nxo;
+      c = rest * g.nx + shard + jx * nshard;
+      const int64_t lo = cstart[c], hi = cend[c];
+      if (hi - lo <= kPowSmall) power[c] = power_sparse(lo, hi, P, G);  // NaN when empty
+      else is_big = true;
+    }
+    const uint64_t m = __ballot(is_big);
+    if (m) {
+      unsigned b0 = 0;
+      if (lane == 0) b0 = atomicAdd(nbig, (unsigned)__popcll(m));
+      b0 = __shfl(b0, 0, 64);
+      if (is_big) {
+        const unsigned r = (unsigned)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        big[b0 + r] = (int32_t)c;
+      }
+    }
   }
 }
 
@@ -1154,22 +1176,19 @@ __device__ __forceinline__ double interval_sq(double Pv, double Qv, int64_t L, d
 // power_range.  Either way equal to the serial sweep up to the order of summation.  (One
 // thread per cell was a chain of dependent global loads per interval: the kernel lasted as long
 // as its slowest cell whatever the cell count.)
-__global__ __launch_bounds__(256) void k_power(TermArrays G, const int32_t* cstart, const int32_t* cend, rt_grid g,
-                                               int shard, int nshard, PowerParams P, double* power) {
+__global__ __launch_bounds__(256) void k_power(TermArrays G, const int32_t* cstart, const int32_t* cend,
+                                               const int32_t* big, const unsigned* nbig, PowerParams P, double* power) {
   __shared__ int32_t s_st[4][kPowLds], s_e1[4][kPowLds], s_m[4][kPowLds];
   __shared__ double s_pch[4][kPowLds + 1], s_pcl[4][kPowLds + 1], s_psh[4][kPowLds + 1], s_psl[4][kPowLds + 1];
   __shared__ double s_ev[4][4 * kPowLds];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t n = P.n_bins, half = P.half;
-  const int64_t nxo = g.nx > shard ? (g.nx - shard + nshard - 1) / nshard : 0;
-  const int64_t nown = nxo * g.ny * g.nz;
+  const int64_t nown = *nbig;
   double sn, cn;  // sin/cos at the sweep end
   sincos_turns(P.turns * (double)n, sn, cn);
   for (int64_t t = (int64_t)blockIdx.x * 4 + w; t < nown; t += (int64_t)gridDim.x * 4) {
-    const int64_t jx = t % nxo, rest = t / nxo;
-    const int64_t c = rest * g.nx + shard + jx * nshard;  // rest = iz*ny + iy
+    const int64_t c = big[t];
     const int64_t lo = cstart[c], hi = cend[c], K = hi - lo;
-    if (K <= kPowSmall) continue;  // k_power_small's (wave-uniform branch)
     double total = 0.0, tcomp = 0.0;
     int64_t count = 0;
     if (K <= kPowLds) {
@@ -1348,6 +1367,8 @@ struct rt_coverage {
   double *tcos = nullptr, *tsin = nullptr;  // per unique (cell, bin): phase terms of the power sweep
   double* ev = nullptr;                      // per unique (cell, bin): sin/cos at its start and end sample
   int32_t *cstart = nullptr, *cend = nullptr;  // per cell: its run in the unique keys
+  int32_t* bigcells = nullptr;  // per cell slot: the cells k_power sweeps (more than kPowSmall terms)
+  int32_t* runs = nullptr;  // exact run sums: [cap] head flags, [cap] their scan, [cap] run starts, [64] counters
   uint8_t* win = nullptr;
   uint8_t* first_flag = nullptr;
   float* trx = nullptr;
@@ -1375,11 +1396,263 @@ struct rt_coverage {
 
 namespace {
 
+// Exact per-bin sums.  tracer.py:116-117 adds a bin's amplitudes one by one in f64, in ray order.
+// Here every amplitude is converted exactly (truncated below 2^-136) to a 192-bit unsigned fixed
+// point number with unit 2^-136 and integer part below 2^56, the bin's values are added as
+// integers, and the sum is rounded once to f64 (correctly rounded).  Integer addition is
+// associative, so the result does not depend on the order of the records, on how the rays are
+// sharded over ranks, or on the thread timing of the reduction: ray-sharded maps equal the
+// one-GPU map bit for bit, and the sort needs no ray field in its key.  It differs from the
+// reference's sequential f64 sum by that sum's own rounding (~1e-16 relative); amplitudes below
+// ~1e-26 lose relative precision (they are 2^-136-quantised).
+//
+// (Round 1 summed doubles with hipcub::DeviceReduce::ReduceByKey, whose decoupled look-back
+// combines tile partials in a timing-dependent order: the transmitter cells' long runs changed in
+// the last bit from run to run.  Round 2 first moved to rocPRIM's deterministic_reduce_by_key over
+// a (cell, bin, ray) sort; the fixed point makes the ray field and the deterministic variant
+// unnecessary.  DESIGN.md §6.)
+struct Fx192 {
+  uint64_t w0, w1, w2;  // w0 least significant
+};
+struct FxPlus {
+  __host__ __device__ __forceinline__ Fx192 operator()(const Fx192& a, const Fx192& b) const {
+    Fx192 r;
+    r.w0 = a.w0 + b.w0;
+    const uint64_t c0 = r.w0 < a.w0;
+    const uint64_t t = a.w1 + b.w1;
+    const uint64_t c1 = t < a.w1;
+    r.w1 = t + c0;
+    r.w2 = a.w2 + b.w2 + (c1 | (r.w1 < t));
+    return r;
+  }
+};
+// amplitude (finite, >= 0) -> fixed point, truncated below the unit 2^-136; saturates at 2^56
+__host__ __device__ __forceinline__ Fx192 fx_from_double(double a) {
+  Fx192 r{0, 0, 0};
+  uint64_t bits;
+  memcpy(&bits, &a, 8);
+  bits &= ~(1ull << 63);
+  int e = (int)(bits >> 52);
+  uint64_t m = bits & ((1ull << 52) - 1);
+  if (e == 0x7ff) return r;  // not finite: no contribution (never produced by the replay)
+  if (e == 0) e = 1;         // subnormal
+  else m |= 1ull << 52;
+  const int sh = e - 939;  // a = m 2^(e-1075) = m 2^sh units of 2^-136
+  if (sh < 0) {
+    r.w0 = sh <= -64 ? 0 : m >> (-sh);
+  } else if (sh > 139) {
+    r.w0 = r.w1 = r.w2 = ~0ull;
+  } else {
+    const int w = sh >> 6, b = sh & 63;
+    const uint64_t lo = m << b, hi = b ? m >> (64 - b) : 0;
+    if (w == 0) {
+      r.w0 = lo;
+      r.w1 = hi;
+    } else if (w == 1) {
+      r.w1 = lo;
+      r.w2 = hi;
+    } else {
+      r.w2 = lo;
+    }
+  }
+  return r;
+}
+// fixed point -> the nearest double (round to nearest even, a sticky bit for the cut-off bits)
+__host__ __device__ __forceinline__ double fx_to_double(const Fx192& x) {
+  int top;
+  if (x.w2) top = 128 + 63 - __builtin_clzll(x.w2);
+  else if (x.w1) top = 64 + 63 - __builtin_clzll(x.w1);
+  else if (x.w0) top = 63 - __builtin_clzll(x.w0);
+  else return 0.0;
+  if (top < 64) return ldexp((double)x.w0, -136);
+  const int sh = top - 63;  // 1 .. 128: window = bits [sh, sh + 63]
+  uint64_t win, sticky;
+  if (sh < 64) {
+    win = (x.w0 >> sh) | (x.w1 << (64 - sh));
+    sticky = x.w0 & ((1ull << sh) - 1);
+    if (top >= 128) win = (x.w1 >> sh) | (x.w2 << (64 - sh)), sticky = x.w0 | (x.w1 & ((1ull << sh) - 1));
+  } else if (sh == 64) {
+    win = x.w1;
+    sticky = x.w0;
+  } else {
+    const int b = sh - 64;
+    win = (x.w1 >> b) | (x.w2 << (64 - b));
+    sticky = x.w0 | (x.w1 & ((1ull << b) - 1));
+  }
+  return ldexp((double)(win | (sticky ? 1ull : 0ull)), sh - 136);
+}
+
+// The exact sums of the runs of equal keys in sorted records, in place of a generic reduce-by-key
+// (rocPRIM's took 357 us per 7.9M records with the 24-B fixed-point value, 127 us with f64):
+//   k_run_flags   head flag of every record (its key differs from the previous one)
+//   inclusive scan of the flags (rocPRIM, int32): the run index of every record, and the run count
+//   k_run_starts  the first record of every run
+//   k_run_sums    one thread per run of <= 64 records: serial sum; longer runs get a long-run id
+//                 (the transmitter cells' bins collect ~1M records each)
+//   k_long_spans  one wave per span of 512 records, 64-record tiles: a tile meets at most two long
+//                 runs (its first and last record's); runs inside the span are summed whole, the
+//                 pieces of the runs crossing the span's edges go to per-span head/tail slots
+//   k_long_final  assembles the runs crossing spans from their pieces
+// Integer sums throughout, so neither the tiling nor the atomics' order changes a bit.
+constexpr int kShortRun = 64;  // > 64: a 64-record tile meets at most two such runs
+
+struct AmpVal {  // sorted replay records: f64 amplitudes
+  const double* a;
+  __device__ __forceinline__ Fx192 operator()(int64_t i) const { return fx_from_double(a[i]); }
+};
+struct SumVal {  // received records: fixed-point sums, in sorted-index order
+  const Fx192* sums;
+  const int64_t* idx;
+  __device__ __forceinline__ Fx192 operator()(int64_t i) const { return sums[idx[i]]; }
+};
+
+__global__ __launch_bounds__(256) void k_run_flags(const uint64_t* keys, int64_t n, int32_t* flags) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    flags[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1 : 0;
+}
+__global__ __launch_bounds__(256) void k_run_starts(const int32_t* flags, const int32_t* scan, int64_t n,
+                                                    int32_t* starts, int64_t* nuniq) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (flags[i]) starts[scan[i] - 1] = (int32_t)i;
+    if (i == n - 1) *nuniq = scan[i];
+  }
+}
+// longid (overwrites the flags, one per run): the run's long-run id, or -1; longu[lid] = run
+template <typename Val>
+__global__ __launch_bounds__(256) void k_run_sums(const uint64_t* keys, Val val, int64_t n, const int32_t* starts,
+                                                  const int64_t* nuniq, WideKey wk, uint64_t* ukeys, Fx192* usums,
+                                                  int32_t* longid, int32_t* longu, unsigned* nlong) {
+  const int64_t nu = *nuniq;
+  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < nu; u += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = starts[u], e = u + 1 < nu ? starts[u + 1] : n;
+    ukeys[u] = wk(keys[b]);
+    if (e - b > kShortRun) {
+      const unsigned lid = atomicAdd(nlong, 1u);
+      longid[u] = (int32_t)lid;
+      longu[lid] = (int32_t)u;
+      continue;
+    }
+    longid[u] = -1;
+    Fx192 acc = val(b);
+    for (int64_t i = b + 1; i < e; ++i) acc = FxPlus()(acc, val(i));
+    usums[u] = acc;
+  }
+}
+// wave sum of a Fx192 (xor butterfly; every lane ends with the total)
+__device__ __forceinline__ Fx192 wave_fx_sum(Fx192 x) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    Fx192 y;
+    y.w0 = __shfl_xor(x.w0, o, 64);
+    y.w1 = __shfl_xor(x.w1, o, 64);
+    y.w2 = __shfl_xor(x.w2, o, 64);
+    x = FxPlus()(x, y);
+  }
+  return x;
+}
+constexpr int kSpanTiles = 8;  // a wave's span: 8 tiles of 64 records
+constexpr int64_t kSpan = 64 * kSpanTiles;
+
+// One wave per span of kSpan sorted records: the pieces of the long runs in the span, tile by tile
+// (a 64-record tile meets at most two long runs, its first and its last record's).  A long run
+// inside the span is written whole; the piece of a run that began in an earlier span goes to
+// head[span], that of a run beginning here and running on to tail[span].
+template <typename Val>
+__global__ __launch_bounds__(256) void k_long_spans(Val val, int64_t n, const int32_t* scan, const int32_t* starts,
+                                                    const int64_t* nuniq, const int32_t* longid,
+                                                    const unsigned* nlong, Fx192* head, Fx192* tail, Fx192* usums) {
+  if (*nlong == 0) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t nspan = (n + kSpan - 1) / kSpan;
+  const int64_t nu = *nuniq;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t sp = wave; sp < nspan; sp += nwave) {
+    const int64_t s0 = sp * kSpan, s1 = s0 + kSpan < n ? s0 + kSpan : n;
+    int32_t cur = -1;  // run whose piece is being summed (uniform)
+    Fx192 acc{0, 0, 0};
+    auto flush = [&]() {
+      if (cur < 0 || lane != 0) return;
+      const int64_t b = starts[cur], e = cur + 1 < nu ? starts[cur + 1] : n;
+      if (b < s0) head[sp] = acc;       // began in an earlier span (may also run past this one)
+      else if (e > s1) tail[sp] = acc;  // runs on into the next span
+      else usums[cur] = acc;            // the whole run lies inside the span
+    };
+    for (int64_t t0 = s0; t0 < s1; t0 += 64) {
+      const int64_t t1 = t0 + 64 < s1 ? t0 + 64 : s1;
+      const int64_t i = t0 + lane;
+      const int32_t u = i < t1 ? scan[i] - 1 : -1;
+      const int32_t ua = __shfl(u, 0, 64), ub = __shfl(u, (int)(t1 - t0 - 1), 64);
+      const bool la = longid[ua] >= 0, lb = ub != ua && longid[ub] >= 0;
+      if (!la && !lb) continue;
+      const Fx192 z{0, 0, 0};
+      const Fx192 v = i < t1 ? val(i) : z;
+      const Fx192 A = wave_fx_sum(la && u == ua ? v : z);
+      const Fx192 Bv = wave_fx_sum(lb && u == ub ? v : z);
+      if (la) {
+        if (cur == ua) {
+          acc = FxPlus()(acc, A);
+        } else {
+          flush();
+          cur = ua;
+          acc = A;
+        }
+      }
+      if (lb) {
+        flush();
+        cur = ub;
+        acc = Bv;
+      }
+    }
+    flush();
+  }
+}
+// every long run crossing spans: tail[its first span] + head[every later span it reaches] (a run
+// inside one span was written whole by k_long_spans)
+__global__ __launch_bounds__(256) void k_long_final(const int32_t* starts, const int64_t* nuniq, int64_t n,
+                                                    const int32_t* longu, const unsigned* nlong, const Fx192* head,
+                                                    const Fx192* tail, Fx192* usums) {
+  // one wave per long run: the transmitter cells' bins cross hundreds of spans
+  const unsigned nl = *nlong;
+  const int64_t nu = *nuniq;
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t j = wave; j < nl; j += nwave) {
+    const int32_t u = longu[j];
+    const int64_t b = starts[u], e = u + 1 < nu ? starts[u + 1] : n;
+    const int64_t sa = b / kSpan, sb = (e - 1) / kSpan;
+    if (sa == sb) continue;  // uniform
+    Fx192 acc{0, 0, 0};
+    for (int64_t q = sa + 1 + lane; q <= sb; q += 64) acc = FxPlus()(acc, head[q]);
+    acc = wave_fx_sum(acc);
+    if (lane == 0) usums[u] = FxPlus()(acc, tail[sa]);
+  }
+}
+
+hipError_t scan_flags(void* tmp, size_t& bytes, const int32_t* flags, int32_t* scan, int64_t n, hipStream_t s) {
+  return rocprim::inclusive_scan(tmp, bytes, flags, scan, (size_t)n, rocprim::plus<int32_t>(), s);
+}
+
+__global__ __launch_bounds__(256) void k_fx_to_amps(const Fx192* usums, const int64_t* nuniq, double* uamps) {
+  const int64_t nu = *nuniq;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nu; i += (int64_t)gridDim.x * blockDim.x)
+    uamps[i] = fx_to_double(usums[i]);
+}
+__global__ __launch_bounds__(256) void k_amps_to_fx(const double* amps, int64_t n, Fx192* sums) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    sums[i] = fx_from_double(amps[i]);
+}
+__global__ __launch_bounds__(256) void k_iota(int64_t n, int64_t* out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = i;
+}
+
 void free_cands(rt_coverage* c) {
   for (void* q : {(void*)c->keys, (void*)c->keys_sorted, (void*)c->okeys, (void*)c->okeys_sorted, (void*)c->ukeys,
                   (void*)c->oamps, (void*)c->oamps_sorted, (void*)c->uamps, (void*)c->tcos, (void*)c->tsin, (void*)c->ev,
                   (void*)c->win, (void*)c->trx,
-                  (void*)c->list, (void*)c->first_flag, c->tmp, c->rord})
+                  (void*)c->list, (void*)c->first_flag, c->tmp, c->rord, (void*)c->runs})
     if (q) (void)hipFree(q);
   c->keys = c->keys_sorted = c->okeys = c->okeys_sorted = c->ukeys = nullptr;
   c->oamps = c->oamps_sorted = c->uamps = c->tcos = c->tsin = c->ev = nullptr;
@@ -1387,6 +1660,7 @@ void free_cands(rt_coverage* c) {
   c->first_flag = nullptr;
   c->trx = nullptr;
   c->list = nullptr;
+  c->runs = nullptr;
   c->tmp = nullptr;
   c->tmp_bytes = 0;
   c->rord = nullptr;
@@ -1407,7 +1681,8 @@ size_t rord_row_bytes(int64_t n) { return ((size_t)n * 4 + 255) / 256 * 256; }
 using OnesweepOnly =
     rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, rocprim::default_config, 0>;
 constexpr int64_t kOnesweepMinItems = 300000;
-hipError_t sort_records(void* tmp, size_t& bytes, const uint64_t* kin, uint64_t* kout, const double* vin, double* vout,
+template <typename V>
+hipError_t sort_records(void* tmp, size_t& bytes, const uint64_t* kin, uint64_t* kout, const V* vin, V* vout,
                         int64_t n, int end_bit, hipStream_t s) {
   if (n >= kOnesweepMinItems)
     return rocprim::radix_sort_pairs<OnesweepOnly>(tmp, bytes, kin, kout, vin, vout, (unsigned)n, 0u,
@@ -1415,8 +1690,6 @@ hipError_t sort_records(void* tmp, size_t& bytes, const uint64_t* kin, uint64_t*
   return rocprim::radix_sort_pairs(tmp, bytes, kin, kout, vin, vout, (unsigned)n, 0u, (unsigned)end_bit, s);
 }
 
-hipError_t reduce_records(void* tmp, size_t& bytes, const uint64_t* keys, const double* amps, int64_t n, WideKey wk,
-                          uint64_t* ukeys, double* uamps, int64_t* nuniq, hipStream_t s);
 
 int alloc_cands(rt_coverage* c, int64_t cap) {
   free_cands(c);
@@ -1434,6 +1707,7 @@ int alloc_cands(rt_coverage* c, int64_t cap) {
   RT_HIP(hipMalloc(&c->first_flag, cap));
   RT_HIP(hipMalloc(&c->trx, cap * 4));
   RT_HIP(hipMalloc(&c->list, cap * 8));
+  RT_HIP(hipMalloc(&c->runs, (cap * 3 + 64) * 4));  // run flags, their scan, run starts, long-run list
   size_t b1 = 0, b2 = 0, b3 = 0, b4 = 0;
   RT_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, b1, c->keys, c->keys_sorted, (int)cap, 0, 64));
   size_t b2m = 0;  // both sort_records paths: Onesweep at cap, the merge sort below its threshold
@@ -1441,8 +1715,11 @@ int alloc_cands(rt_coverage* c, int64_t cap) {
   RT_HIP(sort_records(nullptr, b2m, c->okeys, c->okeys_sorted, c->oamps, c->oamps_sorted,
                       std::min<int64_t>(cap, kOnesweepMinItems - 1), 64, 0));
   b2 = std::max(b2, b2m);
-  RT_HIP(reduce_records(nullptr, b3, c->okeys_sorted, c->oamps_sorted, cap, WideKey{0, 0, 0, 0}, c->ukeys, c->uamps,
-                        c->nuniq, 0));
+  size_t b2i = 0;  // the owner stage sorts (key, record index) pairs
+  RT_HIP(sort_records(nullptr, b2i, c->okeys, c->okeys_sorted, (const int64_t*)c->oamps, (int64_t*)c->oamps_sorted, cap,
+                      64, 0));
+  RT_HIP(scan_flags(nullptr, b3, c->runs, c->runs, cap, 0));
+  b3 = std::max(b3, b2i);
   RT_HIP(hipcub::DeviceSelect::Flagged(nullptr, b4, hipcub::CountingInputIterator<int64_t>(0), c->first_flag, c->list,
                                        (int64_t*)(c->counters + 2), (int)cap));
   c->tmp_bytes = std::max(std::max(b1, b2), std::max(b3, b4));
@@ -1481,7 +1758,9 @@ int poison_plan(rt_coverage* c, hipStream_t s) {
               {c->trx, (size_t)c->cap * 4}, {c->list, (size_t)c->cap * 8}, {c->items, (size_t)c->item_cap * 8},
               {c->tmp, c->tmp_bytes}, {c->rord, c->rord_bytes}, {c->counters, 32}, {c->nuniq, 8},
               {c->cstart, sizeof(int32_t) * (size_t)nc}, {c->cend, sizeof(int32_t) * (size_t)nc},
-              {c->bounds, c->bounds ? sizeof(int64_t) * (size_t)(c->nshard + 1) : 0}};
+              {c->bigcells, sizeof(int32_t) * (size_t)nc},
+              {c->bounds, c->bounds ? sizeof(int64_t) * (size_t)(c->nshard + 1) : 0},
+              {c->runs, ((size_t)c->cap * 3 + 64) * 4}};
   for (auto& q : bufs)
     if (q.p && q.n) RT_HIP(hipMemsetAsync(q.p, b, q.n, s));
   return rt::poison_pool((size_t)256 << 20, s);
@@ -1558,7 +1837,7 @@ struct KeyBits {
 };
 KeyBits key_bits(const rt_coverage* c, int64_t n_bins) {
   KeyBits k;
-  k.ray = std::max(1, bits_for((uint64_t)(c->n - 1)));
+  k.ray = 0;  // bins are summed exactly (Fx192), so the order within a bin needs no ray field
   k.bin = std::max(1, bits_for((uint64_t)(n_bins - 1)));
   k.cell = std::max(1, bits_for((uint64_t)(cov_ncell(c) - 1)));
   k.own = c->ray_mode ? bits_for((uint64_t)(c->nshard - 1)) : 0;
@@ -1670,7 +1949,6 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
     rt::set_error("rt_coverage_run: rays x cells x bins x ranks exceed the 63-bit record key");
     return RT_EINVAL;
   }
-  p.ray_bits = kb.ray;
   p.bin_bits = kb.bin;
   p.cell_bits = kb.cell;
   int64_t nrec = 0, nlist = 0;
@@ -1724,35 +2002,66 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
   return RT_OK;
 }
 
-// Stable radix sort of n records on their low sort_bits key bits (compact record keys, ~0 =
-// dropped, sorting last thanks to one extra key bit), then the sum of every run of equal
-// (owner, cell, bin) into c->ukeys (wide keys, wk) / c->uamps, count in c->nuniq.  Runs of one bin
-// arrive in ray order (the ray is the lowest key field).  The sums use rocPRIM's deterministic
-// reduce-by-key: its association is fixed by the record layout, so every run gives the same bits
-// run after run.  (hipcub::DeviceReduce::ReduceByKey, used in round 1, combines tile partials
-// through rocPRIM's non-deterministic decoupled look-back: a bin whose records span a tile
-// boundary -- the transmitter's cells put ~1M records in a few bins -- changed in the last bit from
-// run to run.  A one-thread-per-run sequential sum, the reference's exact order, took 11 ms on such
-// a run.  DESIGN.md §6.)  keys/amps may be caller buffers (records from other ranks).
-using WideIter = hipcub::TransformInputIterator<uint64_t, WideKey, const uint64_t*>;
+Fx192* plan_sums(rt_coverage* c) { return reinterpret_cast<Fx192*>(c->ev); }  // 32 B per slot, free until k_terms
 
-hipError_t reduce_records(void* tmp, size_t& bytes, const uint64_t* keys, const double* amps, int64_t n, WideKey wk,
-                          uint64_t* ukeys, double* uamps, int64_t* nuniq, hipStream_t s) {
-  return rocprim::deterministic_reduce_by_key(tmp, bytes, WideIter(keys, wk), amps, (size_t)n, ukeys, uamps, nuniq,
-                                              rocprim::plus<double>(), rocprim::equal_to<uint64_t>(), s);
+int grow_for(rt_coverage* c, int64_t n) {
+  // records gathered from several ranks can outgrow this rank's candidate buffers
+  return n > c->cap ? alloc_cands(c, n + n / 4 + 1024) : RT_OK;
 }
 
+// exact sums of the runs of sorted records (keys in c->okeys_sorted) into c->ukeys / plan_sums /
+// c->nuniq, then their f64 values into c->uamps
+template <typename Val>
+int run_sums(rt_coverage* c, Val val, int64_t n, WideKey wk, hipStream_t s) {
+  int32_t* flags = c->runs;  // then the long-run id of every run
+  int32_t* scan = c->runs + c->cap;
+  int32_t* starts = c->runs + 2 * c->cap;
+  unsigned* nlong = reinterpret_cast<unsigned*>(c->runs + 3 * c->cap);
+  int32_t* longu = reinterpret_cast<int32_t*>(c->list);  // free once the replay has run
+  // per span of kSpan records: head and tail pieces (tcos + tsin, 16 B per record, are free until k_terms)
+  Fx192* head = reinterpret_cast<Fx192*>(c->tcos);
+  Fx192* tail = head + (n + kSpan - 1) / kSpan;
+  const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 8192);
+  const unsigned g_span = (unsigned)std::min<int64_t>(((n + kSpan - 1) / kSpan + 3) / 4, 8192);
+  hipLaunchKernelGGL(k_run_flags, dim3(g), dim3(256), 0, s, c->okeys_sorted, n, flags);
+  size_t tb = c->tmp_bytes;
+  RT_HIP(scan_flags(c->tmp, tb, flags, scan, n, s));
+  hipLaunchKernelGGL(k_run_starts, dim3(g), dim3(256), 0, s, flags, scan, n, starts, c->nuniq);
+  RT_HIP(hipMemsetAsync(nlong, 0, 4, s));
+  hipLaunchKernelGGL(k_run_sums<Val>, dim3(g), dim3(256), 0, s, c->okeys_sorted, val, n, starts, c->nuniq, wk, c->ukeys,
+                     plan_sums(c), flags, longu, nlong);
+  hipLaunchKernelGGL(k_long_spans<Val>, dim3(g_span), dim3(256), 0, s, val, n, scan, starts, c->nuniq, flags, nlong,
+                     head, tail, plan_sums(c));
+  hipLaunchKernelGGL(k_long_final, dim3(g_span), dim3(256), 0, s, starts, c->nuniq, n, longu, nlong, head, tail,
+                     plan_sums(c));
+  hipLaunchKernelGGL(k_fx_to_amps, dim3(g), dim3(256), 0, s, plan_sums(c), c->nuniq, c->uamps);
+  RT_HIP(hipGetLastError());
+  return RT_OK;
+}
+
+// sort + exact reduce of this plan's records (c->okeys / c->oamps or caller buffers)
 int cov_reduce(rt_coverage* c, const uint64_t* keys, const double* amps, int64_t n, int sort_bits, WideKey wk,
                hipStream_t s) {
-  if (n > c->cap) {  // records gathered from several ranks can outgrow this rank's candidate buffers
-    int rc = alloc_cands(c, n + n / 4 + 1024);
-    if (rc) return rc;
-  }
+  int rc = grow_for(c, n);
+  if (rc) return rc;
   size_t tb = c->tmp_bytes;
   RT_HIP(sort_records(c->tmp, tb, keys, c->okeys_sorted, amps, c->oamps_sorted, n, sort_bits < 64 ? sort_bits : 64, s));
-  tb = c->tmp_bytes;
-  RT_HIP(reduce_records(c->tmp, tb, c->okeys_sorted, c->oamps_sorted, n, wk, c->ukeys, c->uamps, c->nuniq, s));
-  return RT_OK;
+  return run_sums(c, AmpVal{c->oamps_sorted}, n, wk, s);
+}
+
+// owner stage: received (compact key, Fx192 sum) records -> sorted by key (index payload), summed
+int cov_reduce_sums(rt_coverage* c, const uint64_t* keys, const Fx192* sums, int64_t n, int sort_bits, WideKey wk,
+                    hipStream_t s) {
+  int rc = grow_for(c, n);
+  if (rc) return rc;
+  int64_t* idx = reinterpret_cast<int64_t*>(c->oamps);
+  int64_t* idx_sorted = reinterpret_cast<int64_t*>(c->oamps_sorted);
+  const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_iota, dim3(g), dim3(256), 0, s, n, idx);
+  size_t tb = c->tmp_bytes;
+  RT_HIP(sort_records(c->tmp, tb, keys, c->okeys_sorted, (const int64_t*)idx, idx_sorted, n,
+                      sort_bits < 64 ? sort_bits : 64, s));
+  return run_sums(c, SumVal{sums, idx_sorted}, n, wk, s);
 }
 
 // Closed-form signal power of this plan's cells from the reduced records in c->ukeys / c->uamps
@@ -1780,11 +2089,14 @@ int cov_power(rt_coverage* c, int64_t nrec, int64_t n_bins, double alpha, double
     hipLaunchKernelGGL(k_terms, dim3(grid_u), dim3(256), 0, s, c->ukeys, c->uamps, c->nuniq, P, c->tcos, c->tsin, c->ev);
     hipLaunchKernelGGL(k_cell_ranges, dim3(grid_u), dim3(256), 0, s, c->ukeys, c->nuniq, ncell, c->cstart, c->cend);
   }
+  // cells with more than kPowSmall terms, listed by k_power_small for k_power
+  int32_t* big = c->bigcells;
+  unsigned* nbig = reinterpret_cast<unsigned*>(c->runs + 3 * c->cap + 1);
+  RT_HIP(hipMemsetAsync(nbig, 0, 4, s));
   hipLaunchKernelGGL(k_power_small, dim3(grid_small), dim3(64), 0, s, terms, c->cstart, c->cend, c->grid, c->shard,
-                     c->nshard, P, power);
+                     c->nshard, P, power, big, nbig);
   if (nrec > 0)
-    hipLaunchKernelGGL(k_power, dim3(grid_cells), dim3(256), 0, s, terms, c->cstart, c->cend, c->grid, c->shard,
-                       c->nshard, P, power);
+    hipLaunchKernelGGL(k_power, dim3(grid_cells), dim3(256), 0, s, terms, c->cstart, c->cend, big, nbig, P, power);
   RT_HIP(hipGetLastError());
   return RT_OK;
 }
@@ -1825,6 +2137,7 @@ int rt_coverage_create(int device, const rt_mesh* env, int max_bounces, int64_t 
   if (e == hipSuccess) e = hipMemset(c->nuniq, 0, 8);  // rt_coverage_received before any run: nothing
   if (e == hipSuccess) e = hipMalloc(&c->cstart, sizeof(int32_t) * nc);
   if (e == hipSuccess) e = hipMalloc(&c->cend, sizeof(int32_t) * nc);
+  if (e == hipSuccess) e = hipMalloc(&c->bigcells, sizeof(int32_t) * nc);
   if (e != hipSuccess) {
     rt_coverage_destroy(c);
     return rt::hip_fail(e, "rt_coverage_create");
@@ -1849,6 +2162,7 @@ int rt_coverage_destroy(rt_coverage* c) {
   if (c->nuniq) (void)hipFree(c->nuniq);
   if (c->cstart) (void)hipFree(c->cstart);
   if (c->cend) (void)hipFree(c->cend);
+  if (c->bigcells) (void)hipFree(c->bigcells);
   if (c->items) (void)hipFree(c->items);
   if (c->bounds) (void)hipFree(c->bounds);
   if (c->work) (void)hipFree(c->work);
@@ -1873,8 +2187,7 @@ int rt_coverage_run(rt_coverage* c, const float* tx_pos, double tx_power, double
   if (rc) return rc;
   rc = cov_records(c, tx_pos, tx_power, light_speed, sample_rate, flags, n_bins, s, &ncand, &nlist);
   if (rc) return rc;
-  // records are in (cell, ray, k) order; a stable sort on (cell, bin) keeps that order within a
-  // bin, so every bin's amplitudes are summed in ray order.  Dropped records (~0) sort last.
+  // records grouped by (cell, bin) and summed exactly (Fx192); dropped records (~0) sort last
   prof_mark(c, 6, s);
   if (nlist > 0) {
     const KeyBits kb = key_bits(c, n_bins);
@@ -1935,7 +2248,7 @@ int rt_coverage_trace_records(rt_coverage* c, const float* tx_pos, double tx_pow
   if (rc) return rc;
   rc = cov_records(c, tx_pos, tx_power, light_speed, sample_rate, flags, n_bins, s, &ncand, &nlist);
   if (rc) return rc;
-  // local sum per (owner, cell, bin), in ray order; runs of each owner are then contiguous
+  // local exact sum per (owner, cell, bin); runs of each owner are then contiguous
   std::vector<int64_t> b(world + 1, 0);
   prof_mark(c, 6, s);
   if (nlist > 0) {
@@ -1958,8 +2271,8 @@ int rt_coverage_trace_records(rt_coverage* c, const float* tx_pos, double tx_pow
   return RT_OK;
 }
 
-int rt_coverage_records(rt_coverage* c, uint64_t* keys_out, double* amps_out, int64_t max_out, void* stream) {
-  if (!c || !c->ray_mode || (c->n_out > 0 && (!keys_out || !amps_out)) || max_out < c->n_out) {
+int rt_coverage_records(rt_coverage* c, uint64_t* keys_out, uint64_t* sums_out, int64_t max_out, void* stream) {
+  if (!c || !c->ray_mode || (c->n_out > 0 && (!keys_out || !sums_out)) || max_out < c->n_out) {
     rt::set_error("rt_coverage_records: invalid arguments (max_out must hold the sum of the counts)");
     return RT_EINVAL;
   }
@@ -1970,13 +2283,25 @@ int rt_coverage_records(rt_coverage* c, uint64_t* keys_out, double* amps_out, in
   hipLaunchKernelGGL(k_strip_owner, dim3((unsigned)std::min<int64_t>((c->n_out + 255) / 256, 4096)), dim3(256), 0, s,
                      c->ukeys, c->n_out, own_shift(c), keys_out);
   RT_HIP(hipGetLastError());
-  RT_HIP(hipMemcpyAsync(amps_out, c->uamps, sizeof(double) * c->n_out, hipMemcpyDeviceToDevice, s));
+  RT_HIP(hipMemcpyAsync(sums_out, plan_sums(c), sizeof(Fx192) * c->n_out, hipMemcpyDeviceToDevice, s));
   return RT_OK;
 }
 
-int rt_coverage_power_records(rt_coverage* c, const uint64_t* keys, const double* amps, int64_t n, int64_t n_bins,
+int rt_coverage_amps_to_sums(const double* amps, int64_t n, uint64_t* sums, void* stream) {
+  if (n < 0 || (n > 0 && (!amps || !sums))) {
+    rt::set_error("rt_coverage_amps_to_sums: invalid arguments");
+    return RT_EINVAL;
+  }
+  if (n == 0) return RT_OK;
+  hipLaunchKernelGGL(k_amps_to_fx, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 8192)), dim3(256), 0,
+                     (hipStream_t)stream, amps, n, (Fx192*)sums);
+  RT_HIP(hipGetLastError());
+  return RT_OK;
+}
+
+int rt_coverage_power_records(rt_coverage* c, const uint64_t* keys, const uint64_t* sums, int64_t n, int64_t n_bins,
                               double alpha, double* power, void* stream) {
-  if (!c || !c->ray_mode || n < 0 || (n > 0 && (!keys || !amps)) || !power || n_bins < 1 ||
+  if (!c || !c->ray_mode || n < 0 || (n > 0 && (!keys || !sums)) || !power || n_bins < 1 ||
       n_bins >= ((int64_t)1 << 32) || n > ((int64_t)1 << 31) - 1) {
     rt::set_error("rt_coverage_power_records: invalid arguments");
     return RT_EINVAL;
@@ -1989,16 +2314,16 @@ int rt_coverage_power_records(rt_coverage* c, const uint64_t* keys, const double
   c->ev_rec[6] = c->ev_rec[7] = false;
   prof_mark(c, 6, s);
   if (n > 0) {
-    // received (cell << 32 | bin) keys -> compact [cell | bin]; runs from ranks r < r' hold lower
-    // ray ids, so the stable sort keeps every bin's partial sums in ray order
-    if (n > c->cap && (rc = alloc_cands(c, n + n / 4 + 1024))) return rc;
+    // received (cell << 32 | bin) keys -> compact [cell | bin]; the partial sums are exact
+    // fixed point, so their order is irrelevant
+    if ((rc = grow_for(c, n))) return rc;
     KeyBits kb = key_bits(c, n_bins);
     kb.ray = 0;
     kb.own = 0;
     hipLaunchKernelGGL(k_compact_keys, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 8192)), dim3(256), 0, s, keys,
                        n, kb.bin, c->keys_sorted);
     RT_HIP(hipGetLastError());
-    rc = cov_reduce(c, c->keys_sorted, amps, n, kb.total() + 1, wide_key(c, kb), s);
+    rc = cov_reduce_sums(c, c->keys_sorted, (const Fx192*)sums, n, kb.total() + 1, wide_key(c, kb), s);
   } else {
     RT_HIP(hipMemsetAsync(c->nuniq, 0, 8, s));
   }

@@ -10,8 +10,9 @@ Decompositions:
   sum-reduced: ``reduce_sum`` again (NaN of an owner survives).
 * coverage rays -- rank r traces its share of every cell's rays (``ray_range``), sums its
   first-win records per (cell, bin) and sends each record to the owner of its cell (the x-column
-  rule above): ``exchange_records``, one sparse all-to-all.  Owners sum what they receive, in
-  source-rank (= ray) order, compute their cells' power, and the maps are sum-reduced.
+  rule above): ``exchange_records``, one sparse all-to-all.  Owners sum what they receive (exact
+  fixed point, so the order is irrelevant), compute their cells' power, and the maps are
+  sum-reduced.
 """
 from __future__ import annotations
 
@@ -104,13 +105,14 @@ def reduce_max(value: float, device, group=None) -> float:
     return value
 
 
-def exchange_records(keys, amps, send_counts, group=None):
-    """Sparse all-to-all of coverage records: this rank's (key, amplitude) pairs, grouped by
-    destination rank with send_counts[d] for rank d, go to their owners.  Returns the received
-    (keys int64, amps float64), concatenated in source-rank order (= ray order, since rank r holds
-    ray ids below rank r+1's).  Keys and amplitudes travel as one (n, 2) int64 buffer: one
-    collective for the counts, one for the records.  (gloo, used by the CPU tests, moves device
-    tensors through host memory; "nccl" = RCCL sends them device to device over xGMI.)"""
+def exchange_records(keys, vals, send_counts, group=None):
+    """Sparse all-to-all of coverage records: this rank's (key, value) pairs, grouped by
+    destination rank with send_counts[d] for rank d, go to their owners.  vals is (n,) float64
+    or (n, k) int64 (the exact fixed-point sums of Coverage.trace_records).  Returns the received
+    (keys int64, vals of the same dtype and width), concatenated in source-rank order.  Keys and
+    values travel as one (n, 1 + k) int64 buffer: one collective for the counts, one for the
+    records.  (gloo, used by the CPU tests, moves device tensors through host memory; "nccl" =
+    RCCL sends them device to device over xGMI.)"""
     import torch
     import torch.distributed as dist
     home = keys.device
@@ -121,8 +123,13 @@ def exchange_records(keys, amps, send_counts, group=None):
     rc = torch.empty_like(sc)
     dist.all_to_all_single(rc, sc, group=group)
     recv_counts = [int(c) for c in rc.tolist()]
-    packed = torch.stack([keys[:n].view(torch.int64), amps[:n].contiguous().view(torch.int64)], dim=1).to(wire)
-    out = torch.empty((sum(recv_counts), 2), dtype=torch.int64, device=wire)
+    v = vals[:n]
+    is_f64 = v.dim() == 1 and v.dtype == torch.float64
+    v64 = v.contiguous().view(torch.int64).reshape(n, -1) if is_f64 else v.contiguous().reshape(n, -1).to(torch.int64)
+    width = 1 + v64.shape[1]
+    packed = torch.cat([keys[:n].view(torch.int64).reshape(n, 1), v64], dim=1).to(wire)
+    out = torch.empty((sum(recv_counts), width), dtype=torch.int64, device=wire)
     dist.all_to_all_single(out, packed, recv_counts, send_counts, group=group)
     out = out.to(home)
-    return out[:, 0].contiguous(), out[:, 1].contiguous().view(torch.float64)
+    rv = out[:, 1:].contiguous()
+    return out[:, 0].contiguous(), (rv.view(torch.float64).reshape(-1) if is_f64 else rv)

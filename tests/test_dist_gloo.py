@@ -111,6 +111,11 @@ def _a2a_worker(rank, world, port, out):
     keys = torch.tensor([rank * 1000 + d * 100 + i for d in range(world) for i in range(counts[d])], dtype=torch.int64)
     amps = keys.to(torch.float64) / 7.0
     k, a = rdist.exchange_records(keys, amps, counts)
+    # the fixed-point form of Coverage.trace_records: (n, 3) int64 sums travel with their keys
+    sums = torch.stack([keys, keys * 3, -keys], dim=1)
+    k3, s3 = rdist.exchange_records(keys, sums, counts)
+    assert k3.tolist() == k.tolist() and s3.shape == (len(k), 3)
+    assert s3[:, 0].tolist() == k.tolist() and (s3[:, 1] == 3 * s3[:, 0]).all() and (s3[:, 2] == -s3[:, 0]).all()
     out.put((rank, k.tolist(), a.tolist()))
     dist.destroy_process_group()
 

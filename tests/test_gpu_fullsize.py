@@ -138,8 +138,8 @@ def test_k2_compute_cir_full_size_vs_oracle(win):
 
 def test_k3_ray_sharded_equals_whole_at_full_size():
     """The bench's N>1 coverage decomposition at full K3 size, all 8 rank plans on one GPU with the
-    all-to-all done in process: same receiving cells and bins as the whole map, power to f64
-    summation order (each owner sums per-rank partial sums)."""
+    all-to-all done in process: bit-identical to the whole map (per-bin sums are exact fixed point,
+    so per-rank partial sums add up to the same integers)."""
     room = load_stl(os.path.join(REPO, "models", "room.stl"))
     grid = CoverageGrid.square(256, 15.0, 5.0)
     tx, B, win, W = (10.0, 0.0, 5.0), 3, 100e-9, 8
@@ -156,18 +156,16 @@ def test_k3_ray_sharded_equals_whole_at_full_size():
     total = torch.zeros(grid.num_cells, dtype=torch.float64, device="cuda:0")
     for d, p in enumerate(plans):
         keys = torch.cat([sent[r][d][0] for r in range(W)])
-        amps = torch.cat([sent[r][d][1] for r in range(W)])
-        total += p.power_from_records(keys, amps)
+        sums = torch.cat([sent[r][d][1] for r in range(W)])
+        total += p.power_from_records(keys, sums)
         p.close()
     got = total.cpu().numpy()
-    np.testing.assert_array_equal(np.isnan(got), np.isnan(ref))
-    ok = ~np.isnan(ref)
-    np.testing.assert_allclose(got[ok], ref[ok], rtol=1e-9)
+    np.testing.assert_array_equal(got, ref)  # NaN where the whole map has NaN, every other bit equal
 
 
 def test_k3_full_map_is_run_to_run_bit_identical():
     """The r1 nondeterminism, root-caused: rocPRIM's reduce-by-key (decoupled look-back) summed the
-    transmitter cells' long bins in a timing-dependent association.  The sequential per-run sum
+    transmitter cells' long bins in a timing-dependent association.  The exact fixed-point sums
     that replaced it must give the same bits on a re-used plan, a fresh plan and a third run."""
     import hashlib
     room = load_stl(os.path.join(REPO, "models", "room.stl"))
