@@ -442,6 +442,65 @@ __global__ __launch_bounds__(256, RT_COV_TRAJ_WAVES) void k_traj(CovParams p) {
   }
 }
 
+// k_traj for BVH scenes with few rays (a ray-sharded rank's share): four lanes per ray, each
+// walking its quarter of the tree below the root's grandchildren (rt::split_init); the group's
+// closest hit is the ray's.  Same trajectories bit for bit; the slowest ray's chain of dependent
+// node fetches is split over four lanes.
+__global__ __launch_bounds__(256, RT_COV_TRAJ_WAVES) void k_traj_split(CovParams p) {
+  const int j = threadIdx.x & 3;
+  const int64_t stride = ((int64_t)gridDim.x * blockDim.x) >> 2;
+  // every lane of a wave runs the same number of iterations (the shuffles need them all)
+  const int64_t nit = (p.n + stride - 1) / stride;
+  for (int64_t it = 0; it < nit; ++it) {
+    const int64_t ir = it * stride + (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2);
+    const bool valid = ir < p.n;
+    const int64_t r = valid ? (p.order ? (int64_t)p.order[ir] : ir) : 0;
+    float3 dir = rt::ray_dir(p.ray_offset + r);
+    float3 pos = make_float3(p.tx[0], p.tx[1], p.tx[2]);
+    int nseg = 0;
+    bool alive = valid;
+    for (int k = 0; k < p.B; ++k) {
+      const rt::Shear s = rt::make_shear(pos, dir);
+      rt::Walk4 w;
+      rt::WalkStack st;
+      bool active = false;
+      if (alive) {
+        rt::split_init(w, st, p.env_bvh, s, pos, dir, j);
+        active = true;
+      } else {
+        rt::hit_init(w.h);
+        w.tc = RT_MAX_T;
+      }
+      while (__any(active)) {
+        if (active) active = w.step(p.env_bvh, s, st);
+        w.tc = fminf(w.tc, rt::group_min_t(w.h.t));  // cull with the group's best hit so far
+      }
+      const rt::Hit he = rt::group_hit(w.h);
+      if (!alive) continue;
+      if (j == 0) {
+        float4* tp = p.traj + 2 * (r * p.B + k);
+        tp[0] = make_float4(pos.x, pos.y, pos.z, he.face < 0 ? INFINITY : he.t);
+        tp[1] = make_float4(dir.x, dir.y, dir.z, 0.0f);
+      }
+      nseg = k + 1;
+      if (he.face < 0) {
+        alive = false;  // escapes: this segment is infinite, later iterations repeat the miss
+        continue;
+      }
+      pos.x = fmaf(dir.x, he.t, pos.x);
+      pos.y = fmaf(dir.y, he.t, pos.y);
+      pos.z = fmaf(dir.z, he.t, pos.z);
+      const float4 n4 = p.env_nrm[he.face];
+      const float3 n = make_float3(n4.x, n4.y, n4.z);
+      const float sc = 2.0f * rt::dot3(dir, n);
+      dir.x = fmaf(-sc, n.x, dir.x);
+      dir.y = fmaf(-sc, n.y, dir.y);
+      dir.z = fmaf(-sc, n.z, dir.z);
+    }
+    if (valid && j == 0) p.nseg[r] = (uint8_t)nseg;
+  }
+}
+
 // ------------------------------------------------------------------ 2. candidate cells per segment
 // One atomic per 256-thread block: exclusive prefix of the threads' counts (wave scan + LDS),
 // thread 0 reserves the block's total.  Every thread of the block must call it (inactive: c = 0);
@@ -1792,6 +1851,15 @@ __global__ __launch_bounds__(256) void k_count_replay(const uint64_t* keys, cons
 
 // replay query order: receiver first and the environment query culled at its t (default), or
 // the reference's order, environment then receiver (RFRT_COV_RXFIRST=0, for A/B checks)
+// BVH trajectories of at most this many rays run four lanes per ray (RFRT_TRAJ_SPLIT_MAX, 0 = never)
+int64_t traj_split_max_rays() {
+  static const int64_t v = [] {
+    const char* e = getenv("RFRT_TRAJ_SPLIT_MAX");
+    return e ? (int64_t)atoll(e) : (int64_t)262144;
+  }();
+  return v;
+}
+
 bool replay_rx_first() {
   static const bool v = [] {
     const char* e = getenv("RFRT_COV_RXFIRST");
@@ -1894,7 +1962,11 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
     p.order = rt::dir_order(c->ray_offset, c->n, s, &ws);
     if (!p.order) return RT_EHIP;
     prof_mark(c, 0, s);
-    hipLaunchKernelGGL(k_traj<true>, dim3(grid_rays), dim3(256), lds, s, p);
+    if (c->n <= traj_split_max_rays())  // too few rays to fill the GPU: four lanes per ray
+      hipLaunchKernelGGL(k_traj_split, dim3((unsigned)std::min<int64_t>((4 * c->n + 255) / 256, 8192)), dim3(256), 0,
+                         s, p);
+    else
+      hipLaunchKernelGGL(k_traj<true>, dim3(grid_rays), dim3(256), lds, s, p);
     prof_mark(c, 1, s);
     RT_HIP(hipFreeAsync(ws, s));
     p.order = nullptr;
