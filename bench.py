@@ -1,11 +1,13 @@
 #!/usr/bin/env python3
 """Headline benchmark: ray-bounces/s on models/room.stl (BASELINE.json configs[1], "K2").
 
-One step = one pass of the hot path over one synthetic isotropic burst of 1M rays per GPU:
-  rt_trace   (trace_paths_kernel, kernel.py:38-98: ray generation, 3 bounces of closest hit vs
+One step = one pass of the hot path over one synthetic isotropic burst of 1M rays per GPU, one
+rt_trace_cir call (two launches):
+  trace kernel (trace_paths_kernel, kernel.py:38-98: ray generation, 3 bounces of closest hit vs
               receiver + environment, reflect, full reference output contract: traced_paths,
               received_paths, row_mask -- tracer.py:70-72)
-  rt_compact + rt_cir (tracer.py:87-117: received rows -> delay bins -> impulse response)
+  fused compaction + CIR (tracer.py:87-117: received rows in ray order -> delay bins -> impulse
+              response, zeroed and accumulated in ray order)
   RCCL all-reduce of the impulse response (N > 1: the job's CIR is the sum over ray shards).
 Rays are sharded by global ray id (rank r traces ids [r*N, (r+1)*N)): per-GPU work is fixed as
 GPUs are added ("weak").  Inputs (mesh tables) are resident in HBM before the timed region.
@@ -48,8 +50,11 @@ def d4_bytes(B):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--settle-steps", type=int, default=250,
+                    help="untimed steps before the warmup (~40 ms of K2): the GPU clock ramps up over the "
+                         "first tens of ms of load (K2 trace kernel 148 -> 141 us); the same count on every rank")
     ap.add_argument("--legs", default="k2,k3,k4,k5", help="comma list of k2 (always run), k3, k4, k5")
     ap.add_argument("--rays", type=int, default=1_000_000, help="rays per GPU per step (K2: 1M)")
     ap.add_argument("--bounces", type=int, default=3)
@@ -405,7 +410,8 @@ def main():
     mask = torch.empty(N, dtype=torch.int32, device=dev)
     index = torch.empty(N, dtype=torch.int64, device=dev)
     count = torch.empty(1, dtype=torch.int64, device=dev)
-    ws = torch.empty(int(lib().rt_compact_workspace_bytes(N)), dtype=torch.uint8, device=dev)
+    # rt_trace_cir's workspace: zero-filled once, left ready by every call
+    ws = torch.zeros(int(lib().rt_trace_cir_workspace_bytes(N)), dtype=torch.uint8, device=dev)
     # two impulse-response buffers: step i's RCCL all-reduce (on RCCL's own stream) overlaps step
     # i+1's trace; a buffer is reused only once the all-reduce issued on it two steps earlier is done
     irs = [torch.zeros(n_bins, dtype=torch.float64, device=dev) for _ in range(2)]
@@ -416,7 +422,6 @@ def main():
     L = lib()
     stream = torch.cuda.current_stream()
     sh = stream.cuda_stream
-    ev = []
 
     def drain():
         for j in range(2):
@@ -424,43 +429,49 @@ def main():
                 pending[j].wait()  # the current stream waits for that all-reduce
                 pending[j] = None
 
-    def step(i, timed):
+    def step(i):
+        # the whole hot path of one burst: trace (traced + received + row_mask, kernel.py:38-98),
+        # then one fused launch for the ordered compaction and the impulse response (overwritten;
+        # tracer.py:87-117) -- rt_trace_cir
         ir = irs[i % 2]
         if pending[i % 2] is not None:
             pending[i % 2].wait()
             pending[i % 2] = None
-        ir.zero_()
-        if timed:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-        check(L.rt_trace(env.handle, tx32.ctypes.data, rxd.handle, B, ray_offset, N, ptr(traced), ptr(received),
-                         ptr(mask), None, None, sh), "rt_trace")
-        if timed:
-            e1.record(stream)
-            ev.append((e0, e1))
-        check(L.rt_compact(ptr(mask), N, ptr(ws), ws.numel(), ptr(index), ptr(count), sh), "rt_compact")
-        check(L.rt_cir(ptr(received), ptr(index), ptr(count), N, B, amp0, c, fs, flags, n_bins, ptr(ir), None, None,
-                       sh), "rt_cir")
+        check(L.rt_trace_cir(env.handle, tx32.ctypes.data, rxd.handle, B, ray_offset, N, ptr(traced), ptr(received),
+                             ptr(mask), amp0, c, fs, flags, n_bins, ptr(ir), ptr(index), ptr(count), ptr(ws),
+                             ws.numel(), sh), "rt_trace_cir")
         if world > 1:
             pending[i % 2] = dist.all_reduce(ir, async_op=True)
 
+    settle = max(0, args.settle_steps)
+    for i in range(settle):
+        step(i)
+        if i % 32 == 31:
+            drain()
+            torch.cuda.synchronize()
     for i in range(args.warmup):
-        step(i, False)
+        step(i)
     drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    # trace-kernel time from the events its own dispatch packets carry (no marker packets in the
+    # timed stream; rt_trace_profile_stats after the loop)
+    L.rt_profile(1)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(i, True)
+        step(i)
     drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    L.rt_profile(0)
+    pst = np.zeros(4, np.float64)
+    check(L.rt_trace_profile_stats(pst.ctypes.data, 4), "rt_trace_profile_stats")
+    kern_ms = float(pst[1])
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -517,8 +528,8 @@ def main():
             "dtype": "f32",
             "data": "models/room.stl (reference mesh) + synthetic isotropic burst (PCG ray ids, kernel.py:51-52)",
             "config": {"workload": "K2: room.stl, 1 TX (10,0,5), RX (-10,0,5) r=0.1, 1M rays/GPU, 3 bounces, "
-                                   "traced+received+row_mask + CIR (10000 bins)",
-                       "rays_per_gpu": N, "bounces": B, "rays_total": N * world,
+                                   "traced+received+row_mask + ordered compaction + CIR (10000 bins), rt_trace_cir",
+                       "rays_per_gpu": N, "bounces": B, "rays_total": N * world, "settle_steps": settle,
                        "parallelism": f"ray-id shards x{world}, RCCL all-reduce of the CIR"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -85,6 +85,18 @@ int rt_cir(const float* received, const int64_t* index, const int64_t* count, in
            double amp0, double light_speed, double sample_rate, int flags, int64_t n_bins, double* impulse_response,
            int32_t* out_bin, double* out_amp, void* stream);
 
+/* The whole compute_cir hot path of one burst in two launches (tracer.py:67-117): rt_trace's
+ * outputs (traced optional, received and row_mask required), then -- in one fused launch -- the
+ * ordered compaction of rt_compact (out_index / *out_count, ray order) and rt_cir's impulse response,
+ * which is OVERWRITTEN (zeroed, then the paths added in ray order), not accumulated.  workspace:
+ * rt_trace_cir_workspace_bytes(n) bytes, 8-B aligned, zero-filled once before its first use (the
+ * call leaves it ready for the next one); one workspace per stream.  n <= 2^25 rays per call. */
+int64_t rt_trace_cir_workspace_bytes(int64_t n);
+int rt_trace_cir(const rt_mesh* env, const float* tx_pos, const rt_mesh* rx, int max_bounces, int64_t ray_offset,
+                 int64_t n, float* traced, float* received, uint32_t* row_mask, double amp0, double light_speed,
+                 double sample_rate, int flags, int64_t n_bins, double* impulse_response, int64_t* out_index,
+                 int64_t* out_count, void* workspace, int64_t workspace_bytes, void* stream);
+
 /* ---------------------------------------------------------------- coverage (coverage.py:38-57)
  * Receiver cells on a lattice: cell (i,j,k), index (k*ny + j)*nx + i, centre
  * (x0 + i*dx, y0 + j*dy, z0 + k*dz) computed in double.  Each cell is the reference's
@@ -156,10 +168,14 @@ int rt_power_dense(const double* impulse_responses, int64_t rows, int64_t n_bins
  * traced ray-bounces (trajectory segments), replayed ray-bounces (sum over first-win records of
  * B - k0), candidates and first-win records.  Unrecorded entries are NaN; synchronises. */
 int rt_coverage_profile(rt_coverage* cov, int enable);
-/* Process-wide rt_trace timing: rt_profile(1) records HIP events around every later rt_trace's
- * trace kernel and (BVH meshes) its ray-order sort; rt_trace_last_profile fills out[0] = trace
- * kernel ms, out[1] = ray-order sort ms (NaN when not recorded) of the last call; synchronises. */
+/* Process-wide rt_trace / rt_trace_cir timing: rt_profile(1) (re)starts recording the start and
+ * stop of every later trace kernel through its own dispatch packet (hipExtLaunchKernelGGL: no
+ * marker packets in the stream) and brackets BVH ray-order sorts with events.
+ * rt_trace_last_profile fills out[0] = trace kernel ms, out[1] = ray-order sort ms (NaN when not
+ * recorded) of the last call; rt_trace_profile_stats out = [launches, mean, min, max ms] over the
+ * (last 512) kernels recorded since rt_profile(1).  Both synchronise. */
 int rt_profile(int enable);
+int rt_trace_profile_stats(double* out, int n);
 int rt_trace_last_profile(double* out, int n);
 int rt_coverage_last_profile(rt_coverage* cov, double* out, int n);
 

@@ -25,7 +25,7 @@ int hip_fail(hipError_t e, const char* what) {
 }
 int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B, int64_t ray_offset, int64_t n,
                  float* traced, float* received, uint32_t* mask, int32_t* hit_kind, int32_t* hit_face,
-                 hipStream_t stream);
+                 hipStream_t stream, int32_t* chunk_counts = nullptr, bool* counted = nullptr);
 int build_bvh(rt_mesh* m, const std::vector<float>& tri);      // bvh.hip (host, binned SAH)
 int build_bvh_gpu(rt_mesh* m, const std::vector<float>& tri);  // bvh_gpu.hip (device LBVH)
 
@@ -48,6 +48,8 @@ __global__ void k_pack_leaf_refs(float4* nodes, const int2* leaves, int64_t nnod
 int g_poison = -1;
 extern bool g_profile;                      // trace.hip
 int trace_last_profile(double* out, int n);  // trace.hip
+int trace_profile_stats(double* out, int n);  // trace.hip
+void profile_reset();                        // trace.hip
 void keep_pool_memory();  // trace.hip
 
 int poison_pool(size_t bytes, hipStream_t s) {
@@ -79,8 +81,17 @@ const char* rt_last_error(void) { return rt::g_err.c_str(); }
 int rt_version(void) { return RFRT_VERSION; }
 
 int rt_profile(int enable) {
+  if (enable && !rt::g_profile) rt::profile_reset();
   rt::g_profile = enable != 0;
   return RT_OK;
+}
+
+int rt_trace_profile_stats(double* out, int n) {
+  if (!out || n < 1) {
+    rt::set_error("rt_trace_profile_stats: invalid arguments");
+    return RT_EINVAL;
+  }
+  return rt::trace_profile_stats(out, n);
 }
 
 int rt_trace_last_profile(double* out, int n) {

@@ -17,6 +17,8 @@
 // atomic add gave run-to-run different last bits for bins with several paths).
 #include <math.h>
 
+#include <algorithm>
+
 #include "../../include/rfrt.h"
 #include "rt_internal.h"
 
@@ -229,6 +231,151 @@ __global__ __launch_bounds__(1024) void k_cir_accum(const int32_t* bins, const d
   }
 }
 
+// ------------------------------------------------------------------ fused compaction + CIR (rt_trace_cir)
+// K2's step after the trace kernel was five launches of a few microseconds each (count, scatter,
+// per-path CIR, ordered accumulation, impulse-response zeroing) for ~1 received row per 1M rays.
+// Here the trace kernel leaves received rows per 256-row chunk, and ONE launch of kFusedBlocks
+// blocks does the rest:
+//   block b owns chunks [b*C, (b+1)*C): the rows before them (a block reduction of the counts),
+//   its chunks' offsets (an LDS scan), the ordered indices of its received rows (wave ballots),
+//   and each of those rows' (bin, amplitude) -- computed by the lane that found the row;
+//   the last block to finish (an agent-scope release by every block, one atomic ticket) zeroes
+//   the impulse response and adds the amplitudes in path order (tracer.py:116-117), as k_cir_accum.
+constexpr int kFusedBlocks = 64;
+constexpr int kChunk = 256;
+
+// received rows of every 256-row chunk from the mask (BVH / generic kernels, which do not count)
+__global__ __launch_bounds__(256) void k_chunk_counts(const uint32_t* mask, int64_t n, int32_t* counts) {
+  __shared__ int32_t w4[4];
+  for (int64_t ch = blockIdx.x; ch * kChunk < n; ch += gridDim.x) {
+    const int64_t i = ch * kChunk + threadIdx.x;
+    const uint64_t m = __ballot(i < n && mask[i] != 0u);
+    if ((threadIdx.x & 63) == 0) w4[threadIdx.x >> 6] = (int32_t)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) counts[ch] = w4[0] + w4[1] + w4[2] + w4[3];
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ int64_t block_sum_i64(int64_t v, int64_t* red) {
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_down(v, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const int64_t t = red[0] + red[1] + red[2] + red[3];
+  __syncthreads();
+  return t;
+}
+
+struct CirArgs {
+  const uint32_t* mask;
+  const int32_t* counts;
+  int64_t nchunks, n, cpb;  // cpb: chunks per block (<= kFusedMaxCpb)
+  const float* received;
+  int P;
+  double amp0;
+  float c32, fs32;
+  double c64, fs64;
+  int flags;
+  int64_t n_bins;
+  double* ir;
+  int64_t* index;
+  int64_t* count;
+  int32_t* pbin;
+  double* pamp;
+  unsigned* done;
+};
+constexpr int kFusedMaxCpb = 2048;  // 256-row chunks per block: up to 2^25 rows per call
+
+__global__ __launch_bounds__(256) void k_compact_cir(CirArgs a) {
+  __shared__ int32_t off[kFusedMaxCpb];
+  __shared__ int64_t red[4];
+  __shared__ int32_t wofs[4];
+  __shared__ bool last;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int64_t c0 = (int64_t)blockIdx.x * a.cpb;
+  const int64_t c1 = c0 + a.cpb < a.nchunks ? c0 + a.cpb : a.nchunks;
+  // rows received before this block's chunks
+  int64_t before = 0;
+  for (int64_t j = t; j < c0 && j < a.nchunks; j += 256) before += a.counts[j];
+  const int64_t base = block_sum_i64(before, red);
+  // exclusive scan of this block's chunk counts (serial over <= 2048 entries by thread 0 after a
+  // parallel load: the counts are almost all zero and the block has little else to do)
+  const int m = c1 > c0 ? (int)(c1 - c0) : 0;
+  for (int j = t; j < m; j += 256) off[j] = a.counts[c0 + j];
+  __syncthreads();
+  __shared__ int32_t btotal;
+  if (t == 0) {
+    int32_t acc = 0;
+    for (int j = 0; j < m; ++j) {
+      const int32_t c = off[j];
+      off[j] = acc;
+      acc += c;
+    }
+    btotal = acc;
+  }
+  __syncthreads();
+  for (int j = 0; j < m; ++j) {
+    const int64_t ch = c0 + j;
+    if ((j + 1 < m ? off[j + 1] : btotal) == off[j]) continue;  // block-uniform: no received row
+    const int64_t i = ch * kChunk + t;
+    const bool got = i < a.n && a.mask[i] != 0u;
+    const uint64_t bm = __ballot(got);
+    if (lane == 0) wofs[w] = (int32_t)__popcll(bm);
+    __syncthreads();
+    int32_t pre = 0;
+    for (int q = 0; q < w; ++q) pre += wofs[q];
+    __syncthreads();
+    if (got) {
+      const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+      const int64_t k = base + off[j] + pre + rank;
+      a.index[k] = i;
+      cir_one(a.received, a.index, k, a.P, a.amp0, a.c32, a.fs32, a.c64, a.fs64, a.flags, a.n_bins, nullptr,
+              a.pbin, a.pamp);
+    }
+  }
+  // publish, then the last block accumulates.  Only blocks that wrote rows release them: an
+  // agent-scope release writes back the XCD's whole L2, full of the trace kernel's dirty rows
+  // (64 releases took the launch from ~5 to 18 us on K2, where ~1 block has a received row).
+  if (btotal > 0) __threadfence();
+  __syncthreads();
+  if (t == 0) last = atomicAdd(a.done, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  int64_t tot = 0;
+  for (int64_t j = t; j < a.nchunks; j += 256) tot += a.counts[j];
+  const int64_t cnt = block_sum_i64(tot, red);
+  if (t == 0) {
+    *a.count = cnt;
+    *a.done = 0u;  // ready for the next call on this workspace
+  }
+  if (!a.ir) return;
+  for (int64_t b = t; b < a.n_bins; b += 256) a.ir[b] = 0.0;
+  __syncthreads();
+  __shared__ int32_t sb[256];
+  __shared__ double sa[256];
+  for (int64_t b0 = 0; b0 < cnt; b0 += 256) {  // k_cir_accum's order, 256 paths at a time
+    const int64_t k = b0 + t;
+    const int32_t bb = k < cnt ? a.pbin[k] : -1;
+    sb[t] = (bb >= 0 && bb < a.n_bins) ? bb : -1;
+    sa[t] = k < cnt ? a.pamp[k] : 0.0;
+    __syncthreads();
+    const int32_t mb = sb[t];
+    if (mb >= 0) {
+      bool leader = true;
+      for (int j = 0; j < t && leader; ++j) leader = sb[j] != mb;
+      if (leader) {
+        const int mm = (int)(cnt - b0 < 256 ? cnt - b0 : 256);
+        double v = a.ir[mb];
+        for (int j = t; j < mm; ++j)
+          if (sb[j] == mb) v += sa[j];
+        a.ir[mb] = v;
+      }
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -264,6 +411,11 @@ int rt_compact(const uint32_t* row_mask, int64_t n, void* workspace, int64_t wor
   return RT_OK;
 }
 
+int64_t rt_trace_cir_workspace_bytes(int64_t n) {
+  const int64_t nch = (n + kChunk - 1) / kChunk;
+  return 64 + nch * 4 + n * 12 + 64;  // done ticket, chunk counts, per-path bins + amplitudes
+}
+
 int rt_cir(const float* received, const int64_t* index, const int64_t* count, int64_t max_count, int max_bounces,
            double amp0, double light_speed, double sample_rate, int flags, int64_t n_bins, double* impulse_response,
            int32_t* out_bin, double* out_amp, void* stream) {
@@ -297,4 +449,81 @@ int rt_cir(const float* received, const int64_t* index, const int64_t* count, in
   return RT_OK;
 }
 
+
 }  // extern "C"
+
+namespace rt {
+int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B, int64_t ray_offset, int64_t n,
+                 float* traced, float* received, uint32_t* mask, int32_t* hit_kind, int32_t* hit_face,
+                 hipStream_t stream, int32_t* chunk_counts, bool* counted);
+}
+
+extern "C" int rt_trace_cir(const rt_mesh* env, const float* tx_pos, const rt_mesh* rx, int max_bounces,
+                            int64_t ray_offset, int64_t n, float* traced, float* received, uint32_t* row_mask,
+                            double amp0, double light_speed, double sample_rate, int flags, int64_t n_bins,
+                            double* impulse_response, int64_t* out_index, int64_t* out_count, void* workspace,
+                            int64_t workspace_bytes, void* stream) {
+  if (!env || !tx_pos || max_bounces < 1 || n < 0 || ray_offset < 0 || !received || !row_mask || !out_index ||
+      !out_count || n_bins < 0 || (n_bins > 0 && !impulse_response) || !workspace) {
+    rt::set_error("rt_trace_cir: invalid arguments");
+    return RT_EINVAL;
+  }
+  if (workspace_bytes < rt_trace_cir_workspace_bytes(n) || ((uintptr_t)workspace & 7)) {
+    rt::set_error("rt_trace_cir: workspace too small or misaligned (rt_trace_cir_workspace_bytes, 8-B aligned)");
+    return RT_EINVAL;
+  }
+  const int64_t nch = (n + kChunk - 1) / kChunk;
+  const int64_t cpb = (nch + kFusedBlocks - 1) / kFusedBlocks;
+  if (cpb > kFusedMaxCpb) {
+    rt::set_error("rt_trace_cir: more than 2^25 rays per call; shard the burst");
+    return RT_EINVAL;
+  }
+  if (rx && (rx->nf > RT_PERM_MAX_FACES || !rx->perm || rx->device != env->device)) {
+    rt::set_error("rt_trace_cir: receiver mesh too large or on another device");
+    return RT_EINVAL;
+  }
+  rt::DeviceGuard dg(env->device);
+  RT_HIP(dg.err);
+  hipStream_t s = (hipStream_t)stream;
+  if (n == 0) {
+    RT_HIP(hipMemsetAsync(out_count, 0, 8, s));
+    if (n_bins > 0) RT_HIP(hipMemsetAsync(impulse_response, 0, n_bins * 8, s));
+    return RT_OK;
+  }
+  char* ws = (char*)workspace;
+  unsigned* done = (unsigned*)ws;  // zero on entry: the caller zero-fills the workspace once
+  int32_t* counts = (int32_t*)(ws + 64);
+  double* pamp = (double*)(ws + 64 + ((nch * 4 + 7) / 8) * 8);
+  int32_t* pbin = (int32_t*)(pamp + n);
+  bool counted = false;
+  int rc = rt::launch_trace(env, tx_pos, rx, max_bounces, ray_offset, n, traced, received, row_mask, nullptr, nullptr,
+                            s, counts, &counted);
+  if (rc) return rc;
+  if (!counted)
+    hipLaunchKernelGGL(k_chunk_counts, dim3((unsigned)std::min<int64_t>(nch, 4096)), dim3(256), 0, s, row_mask, n,
+                       counts);
+  CirArgs a;
+  a.mask = row_mask;
+  a.counts = counts;
+  a.nchunks = nch;
+  a.n = n;
+  a.cpb = cpb;
+  a.received = received;
+  a.P = max_bounces + 1;
+  a.amp0 = amp0;
+  a.c32 = (float)light_speed;
+  a.fs32 = (float)sample_rate;
+  a.c64 = light_speed;
+  a.fs64 = sample_rate;
+  a.flags = flags;
+  a.n_bins = n_bins;
+  a.ir = n_bins > 0 ? impulse_response : nullptr;
+  a.index = out_index;
+  a.count = out_count;
+  a.pbin = pbin;
+  a.pamp = pamp;
+  a.done = done;
+  hipLaunchKernelGGL(k_compact_cir, dim3(kFusedBlocks), dim3(256), 0, s, a);
+  RT_HIP(hipGetLastError());
+  return RT_OK;
+}

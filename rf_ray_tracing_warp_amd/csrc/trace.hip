@@ -13,6 +13,7 @@
 // no t_min (Q3), no renormalisation after reflect (Q4), traced_paths is scratch (Q6).
 #include <math.h>
 
+#include <hip/hip_ext.h>
 #include <hipcub/hipcub.hpp>
 #include <algorithm>
 #include <cstdlib>
@@ -42,6 +43,7 @@ struct TraceArgs {
   int32_t* hit_kind;  // (n, B) or null
   int32_t* hit_face;  // (n, B) or null
   const int32_t* order;  // processing order of the rows (null = identity), see launch_trace
+  int32_t* chunk_counts;  // brute-force kernels: received rows per 256-row chunk (rt_trace_cir), or null
 };
 
 // Closest hit over a brute-force face list whose permuted table lives at `tab`
@@ -112,8 +114,12 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
   stage_env<USE_BVH>(a, lds_tab);
 
   const float qnan = __builtin_nanf("");
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t irow = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; irow < a.n; irow += stride) {
+  // block-uniform loop over 256-row chunks (the same rows per thread as a grid-stride loop), so the
+  // block can count its chunk's received rows for rt_trace_cir
+  for (int64_t chunk = blockIdx.x; chunk * 256 < a.n; chunk += gridDim.x) {
+    const int64_t irow = chunk * 256 + threadIdx.x;
+    bool got = false;
+    if (irow < a.n) {
     const int64_t row = a.order ? (int64_t)a.order[irow] : irow;
     const int64_t gid = a.ray_offset + row;
     float3 dir = rt::ray_dir(gid);
@@ -183,6 +189,16 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
       store_row(a.received + row * (P * 3), rec, P);
     }
     if (a.mask) a.mask[row] = last_rx >= 0 ? 1u : 0u;
+    got = last_rx >= 0;
+    }
+    if (!USE_BVH && a.chunk_counts) {  // row order == chunk order here (no direction sort)
+      __shared__ int32_t wcnt[4];
+      const uint64_t m = __ballot(got);
+      if ((threadIdx.x & 63) == 0) wcnt[threadIdx.x >> 6] = (int32_t)__popcll(m);
+      __syncthreads();
+      if (threadIdx.x == 0) a.chunk_counts[chunk] = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+      __syncthreads();
+    }
   }
 }
 
@@ -351,10 +367,14 @@ const int32_t* dir_order(int64_t ray_offset, int64_t n, hipStream_t stream, void
 }
 
 void trace_mark(int i, hipStream_t s);
+void trace_events(hipEvent_t* e0, hipEvent_t* e1);
 
+// chunk_counts (optional, rt_trace_cir): received rows per 256-row chunk, written by the
+// brute-force kernels as they go; *counted tells whether they did (BVH and generic kernels: no)
 int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B, int64_t ray_offset, int64_t n,
                  float* traced, float* received, uint32_t* mask, int32_t* hit_kind, int32_t* hit_face,
-                 hipStream_t stream) {
+                 hipStream_t stream, int32_t* chunk_counts, bool* counted) {
+  if (counted) *counted = false;
   if (n == 0) return 0;
   TraceArgs a;
   a.env_perm = env->perm;
@@ -377,6 +397,8 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
   a.hit_kind = hit_kind;
   a.hit_face = hit_face;
   a.order = nullptr;
+  a.chunk_counts = (!bvh && B <= 8) ? chunk_counts : nullptr;
+  if (counted) *counted = a.chunk_counts != nullptr;
   const size_t lds = bvh ? 0 : (size_t)env->nf * 18 * sizeof(float4);
   int dev_cu = 256;
   const int64_t want = (n + 255) / 256;
@@ -395,56 +417,104 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
     const int rc = poison_pool((size_t)256 << 20, stream);
     if (rc) return rc;
   }
-  trace_mark(0, stream);
-  if (bvh && n >= kSortMinRays && n <= INT32_MAX) {
+  const bool sort = bvh && n >= kSortMinRays && n <= INT32_MAX;
+  if (sort) trace_mark(0, stream);
+  if (sort) {
     a.order = dir_order(ray_offset, n, stream, &sort_ws);
     if (!a.order) return -1;
+    trace_mark(1, stream);
   }
-  trace_mark(1, stream);
+  // profiling: the kernel's own dispatch packet carries the start/stop timestamps
+  // (hipExtLaunchKernelGGL), so timing adds no marker packets -- and no gaps -- to the stream
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  trace_events(&ev0, &ev1);
+#define RT_LAUNCH(K, ...)                                                                                \
+  do {                                                                                                   \
+    if (ev0) hipExtLaunchKernelGGL(K, dim3(grid), blk, lds, stream, ev0, ev1, 0, __VA_ARGS__);           \
+    else hipLaunchKernelGGL(K, dim3(grid), blk, lds, stream, __VA_ARGS__);                              \
+  } while (0)
   switch (B) {
-#define RT_CASE(BB)                                                                             \
-  case BB:                                                                                      \
-    if (bvh)                                                                                    \
-      hipLaunchKernelGGL((k_trace_bvh<BB>), dim3(grid), blk, lds, stream, a);                   \
-    else                                                                                        \
-      hipLaunchKernelGGL((k_trace_bf<BB, false>), dim3(grid), blk, lds, stream, a);             \
+#define RT_CASE(BB)                                         \
+  case BB:                                                  \
+    if (bvh) RT_LAUNCH((k_trace_bvh<BB>), a);               \
+    else RT_LAUNCH((k_trace_bf<BB, false>), a);             \
     break;
     RT_CASE(1) RT_CASE(2) RT_CASE(3) RT_CASE(4) RT_CASE(5) RT_CASE(6) RT_CASE(7) RT_CASE(8)
 #undef RT_CASE
     default:
-      if (bvh)
-        hipLaunchKernelGGL(k_trace_bf_generic<true>, dim3(grid), blk, lds, stream, a, B);
-      else
-        hipLaunchKernelGGL(k_trace_bf_generic<false>, dim3(grid), blk, lds, stream, a, B);
+      if (bvh) RT_LAUNCH(k_trace_bf_generic<true>, a, B);
+      else RT_LAUNCH(k_trace_bf_generic<false>, a, B);
       break;
   }
+#undef RT_LAUNCH
   RT_HIP(hipGetLastError());
-  trace_mark(2, stream);
   if (sort_ws) RT_HIP(hipFreeAsync(sort_ws, stream));
   return 0;
 }
 
-// rt_profile / rt_trace_last_profile: HIP events around the last rt_trace's ray-order sort and
-// trace kernel (process-wide, for measurement; not thread-safe)
+// rt_profile / rt_trace_last_profile / rt_trace_profile_stats: while profiling is on, every trace
+// kernel launch records its start/stop in a ring of event pairs (through its dispatch packet), and
+// BVH launches bracket their ray-order sort with markers.  Process-wide, for measurement; not
+// thread-safe.
 bool g_profile = false;
-static hipEvent_t g_tev[3] = {};
-static bool g_trec[3] = {};
+constexpr int kRing = 512;
+static hipEvent_t g_ring[kRing][2] = {};
+static int64_t g_ring_n = 0;
+static hipEvent_t g_tev[2] = {};
+static bool g_trec[2] = {};
+void profile_reset() {
+  g_ring_n = 0;
+  g_trec[0] = g_trec[1] = false;
+}
+void trace_events(hipEvent_t* e0, hipEvent_t* e1) {
+  *e0 = *e1 = nullptr;
+  if (!g_profile) return;
+  hipEvent_t* p = g_ring[g_ring_n % kRing];
+  for (int i = 0; i < 2; ++i)
+    if (!p[i] && hipEventCreate(&p[i]) != hipSuccess) return;
+  *e0 = p[0];
+  *e1 = p[1];
+  ++g_ring_n;
+}
 void trace_mark(int i, hipStream_t s) {
   if (!g_profile) return;
   if (!g_tev[i] && hipEventCreate(&g_tev[i]) != hipSuccess) return;
   g_trec[i] = hipEventRecord(g_tev[i], s) == hipSuccess;
 }
+static double ring_ms(int64_t j) {
+  float ms = 0.0f;
+  hipEvent_t* p = g_ring[j % kRing];
+  if (hipEventSynchronize(p[1]) != hipSuccess || hipEventElapsedTime(&ms, p[0], p[1]) != hipSuccess) return NAN;
+  return (double)ms;
+}
+// out[0]: the last trace kernel (ms), out[1]: its ray-order sort (ms, BVH meshes; NaN otherwise)
 int trace_last_profile(double* out, int n) {
   for (int i = 0; i < n; ++i) out[i] = NAN;
-  auto span = [](int a, int b) -> double {
+  if (n > 0 && g_ring_n > 0) out[0] = ring_ms(g_ring_n - 1);
+  if (n > 1 && g_trec[0] && g_trec[1]) {
     float ms = 0.0f;
-    if (!g_trec[a] || !g_trec[b] || hipEventSynchronize(g_tev[b]) != hipSuccess ||
-        hipEventElapsedTime(&ms, g_tev[a], g_tev[b]) != hipSuccess)
-      return NAN;
-    return (double)ms;
-  };
-  if (n > 0) out[0] = span(1, 2);
-  if (n > 1) out[1] = span(0, 1);
+    if (hipEventSynchronize(g_tev[1]) == hipSuccess && hipEventElapsedTime(&ms, g_tev[0], g_tev[1]) == hipSuccess)
+      out[1] = (double)ms;
+  }
+  return 0;
+}
+// over the trace kernels profiled since profiling was (re)enabled, at most the last 512:
+// out = [launches, mean ms, min ms, max ms]
+int trace_profile_stats(double* out, int n) {
+  for (int i = 0; i < n; ++i) out[i] = NAN;
+  const int64_t m = g_ring_n < kRing ? g_ring_n : kRing;
+  if (n > 0) out[0] = (double)m;
+  if (m == 0) return 0;
+  double sum = 0.0, lo = INFINITY, hi = 0.0;
+  for (int64_t j = g_ring_n - m; j < g_ring_n; ++j) {
+    const double v = ring_ms(j);
+    sum += v;
+    lo = fmin(lo, v);
+    hi = fmax(hi, v);
+  }
+  if (n > 1) out[1] = sum / (double)m;
+  if (n > 2) out[2] = lo;
+  if (n > 3) out[3] = hi;
   return 0;
 }
 

@@ -131,6 +131,32 @@ class Tracer:
                            ptr(impulse_response), None, None, s), "rt_cir")
         return index, count
 
+    def trace_cir_device(self, tx_pos, rx_mesh, received, mask, tx_power, impulse_response, traced=None,
+                         ray_offset=0, n=None, index=None, count=None, amp_rays=None):
+        """tracer.py:67-117 on the device in two launches (rt_trace_cir): the trace, then the ordered
+        compaction + impulse response (overwritten).  amp_rays: the burst size of the amplitude
+        tx_power / amp_rays (default tx_num_rays).  Returns (index, count) device tensors."""
+        import torch
+
+        n = self.tx_num_rays if n is None else int(n)
+        dev = f"cuda:{self.device}"
+        if index is None:
+            index = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+        if count is None:
+            count = torch.empty(1, dtype=torch.int64, device=dev)
+        need = int(lib().rt_trace_cir_workspace_bytes(n))
+        if getattr(self, "_tc_ws", None) is None or self._tc_ws.numel() < need:
+            self._tc_ws = torch.zeros(need, dtype=torch.uint8, device=dev)  # zeroed once, kept ready by the calls
+        tx = np.ascontiguousarray(np.asarray(tx_pos, dtype=np.float64).astype(np.float32))
+        amp0 = tx_power / (self.tx_num_rays if amp_rays is None else amp_rays)
+        check(lib().rt_trace_cir(self.env.handle, tx.ctypes.data, rx_mesh.handle if rx_mesh is not None else None,
+                                 self.max_bounces, int(ray_offset), n, ptr(traced), ptr(received), ptr(mask),
+                                 float(amp0), float(self.light_speed_mps), float(self.sample_rate_hz),
+                                 cir_flags(self.light_speed_mps, self.sample_rate_hz), impulse_response.numel(),
+                                 ptr(impulse_response), ptr(index), ptr(count), ptr(self._tc_ws),
+                                 self._tc_ws.numel(), _lib.stream_handle(self.device)), "rt_trace_cir")
+        return index, count
+
     def n_bins(self) -> int:
         return int(self.sample_window_s * self.sample_rate_hz)  # tracer.py:101
 
@@ -149,8 +175,7 @@ class Tracer:
             traced = torch.empty((N, P, 3), dtype=torch.float32, device=dev)
         else:
             traced = None  # scratch in the reference (Q6); kept in registers here
-        self.trace_device(tx_pos, rx_mesh, received, mask, traced=traced)
-        index, count = self.cir_device(received, mask, tx_power, ir)
+        index, count = self.trace_cir_device(tx_pos, rx_mesh, received, mask, tx_power, ir, traced=traced)
         k = int(count.item())  # synchronises (tracer.py:80)
         rows = received.index_select(0, index[:k]).cpu().numpy() if k else np.zeros((0, P, 3), np.float32)
         cleaned_paths = []
