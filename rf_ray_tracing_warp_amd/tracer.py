@@ -224,8 +224,8 @@ class Tracer:
         k = 0
         rows = np.zeros((0, P, 3), np.float32)
         if n > 0:
-            self.trace_device(tx_pos, rx_mesh, received, mask, traced=traced, ray_offset=lo, n=n)
-            index, count = self.cir_device(received, mask, tx_power, ir, n=n)
+            index, count = self.trace_cir_device(tx_pos, rx_mesh, received, mask, tx_power, ir, traced=traced,
+                                                 ray_offset=lo, n=n)
             k = int(count.item())
             if k:
                 rows = received.index_select(0, index[:k]).cpu().numpy()
