@@ -446,13 +446,18 @@ __global__ __launch_bounds__(256, RT_COV_TRAJ_WAVES) void k_traj(CovParams p) {
 // walking its quarter of the tree below the root's grandchildren (rt::split_init); the group's
 // closest hit is the ray's.  Same trajectories bit for bit; the slowest ray's chain of dependent
 // node fetches is split over four lanes.
+#ifndef RT_TRAJ_SPLIT_G
+#define RT_TRAJ_SPLIT_G 4
+#endif
+template <int G>
 __global__ __launch_bounds__(256, RT_COV_TRAJ_WAVES) void k_traj_split(CovParams p) {
-  const int j = threadIdx.x & 3;
-  const int64_t stride = ((int64_t)gridDim.x * blockDim.x) >> 2;
+  constexpr int LG = G == 16 ? 4 : 2;
+  const int j = threadIdx.x & (G - 1);
+  const int64_t stride = ((int64_t)gridDim.x * blockDim.x) >> LG;
   // every lane of a wave runs the same number of iterations (the shuffles need them all)
   const int64_t nit = (p.n + stride - 1) / stride;
   for (int64_t it = 0; it < nit; ++it) {
-    const int64_t ir = it * stride + (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2);
+    const int64_t ir = it * stride + (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> LG);
     const bool valid = ir < p.n;
     const int64_t r = valid ? (p.order ? (int64_t)p.order[ir] : ir) : 0;
     float3 dir = rt::ray_dir(p.ray_offset + r);
@@ -465,7 +470,7 @@ __global__ __launch_bounds__(256, RT_COV_TRAJ_WAVES) void k_traj_split(CovParams
       rt::WalkStack st;
       bool active = false;
       if (alive) {
-        rt::split_init(w, st, p.env_bvh, s, pos, dir, j);
+        rt::split_init<G>(w, st, p.env_bvh, s, pos, dir, j);
         active = true;
       } else {
         rt::hit_init(w.h);
@@ -473,9 +478,9 @@ __global__ __launch_bounds__(256, RT_COV_TRAJ_WAVES) void k_traj_split(CovParams
       }
       while (__any(active)) {
         if (active) active = w.step(p.env_bvh, s, st);
-        w.tc = fminf(w.tc, rt::group_min_t(w.h.t));  // cull with the group's best hit so far
+        w.tc = fminf(w.tc, rt::group_min_t<G>(w.h.t));  // cull with the group's best hit so far
       }
-      const rt::Hit he = rt::group_hit(w.h);
+      const rt::Hit he = rt::group_hit<G>(w.h);
       if (!alive) continue;
       if (j == 0) {
         float4* tp = p.traj + 2 * (r * p.B + k);
@@ -1963,7 +1968,8 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
     if (!p.order) return RT_EHIP;
     prof_mark(c, 0, s);
     if (c->n <= traj_split_max_rays())  // too few rays to fill the GPU: four lanes per ray
-      hipLaunchKernelGGL(k_traj_split, dim3((unsigned)std::min<int64_t>((4 * c->n + 255) / 256, 8192)), dim3(256), 0,
+      hipLaunchKernelGGL(k_traj_split<RT_TRAJ_SPLIT_G>,
+                         dim3((unsigned)std::min<int64_t>((RT_TRAJ_SPLIT_G * c->n + 255) / 256, 8192)), dim3(256), 0,
                          s, p);
     else
       hipLaunchKernelGGL(k_traj<true>, dim3(grid_rays), dim3(256), lds, s, p);

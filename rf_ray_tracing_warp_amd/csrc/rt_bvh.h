@@ -279,37 +279,42 @@ struct Walk4 {
   }
 };
 
-// Lane j (0..G-1, G = 4) of a group of G lanes that trace ONE ray together: it walks the subtrees
-// of the grandchildren slots g == j of the root (and the root's leaf children c with c % G == j),
-// so the group's lanes split the ray's traversal; the group's (t, face) minimum (group_hit) is the
-// ray's closest hit.  Each lane culls with the group's best t so far (share_cull), which is exact
-// for the same reason tcull is.  Used where a burst is too small to fill the GPU (a ray-sharded
-// rank traces 1/8 of the rays and the slowest ray's chain of dependent fetches sets the time).
+// Lane j (0..G-1) of a group of G lanes (G = 4 or 16) that trace ONE ray together.  G = 4: lane j
+// walks the subtrees of grandchild slot j of every inner child of the root (and the root's leaf
+// children c with c % 4 == j); G = 16: lane j walks grandchild slot j % 4 of root child j / 4 only
+// (a leaf child c by lane 4c).  The group's (t, face) minimum (group_hit) is the ray's closest hit;
+// each lane culls with the group's best t so far (group_min_t), exact for the same reason tcull is.
+// Used where a burst is too small to fill the GPU (a ray-sharded rank traces 1/8 of the rays and the
+// slowest ray's chain of dependent fetches sets the time).
+template <int G>
 __device__ __forceinline__ void split_init(Walk4& w, WalkStack& st, const BvhView& b, const Shear& s, float3 o,
                                            float3 d, int j, float tcull = RT_MAX_T) {
+  static_assert(G == 4 || G == 16, "split over 4 or 16 lanes");
   w.init(o, d, tcull);
   w.cur = -1;
-  const float4* rw = b.wide;
-  const float4 rf = rw[6];
+  const float4 rf = b.wide[6];
   const int rc[4] = {__float_as_int(rf.x), __float_as_int(rf.y), __float_as_int(rf.z), __float_as_int(rf.w)};
+  const int gslot = j & 3;
 #pragma unroll 1
   for (int c = 0; c < 4; ++c) {
+    if (G == 16 && c != (j >> 2)) continue;
     const int ref = rc[c];
-    if (ref < -1) {  // leaf child of the root: lane c % 4
-      if ((c & 3) == j) {
+    if (ref < -1) {  // leaf child of the root
+      if ((G == 4 && (c & 3) == j) || (G == 16 && gslot == 0)) {
         const int pk = ~ref;
         leaf4(b, s, pk >> 3, pk & 7, w.h);
       }
-    } else if (ref >= 0) {  // inner child: its slot j (grandchild)
+    } else if (ref >= 0) {  // inner child: its grandchild slot
       const float4* cw = b.wide + 8 * (int64_t)ref;
       const float4 lx = cw[0], hx = cw[1], ly = cw[2], hy = cw[3], lz = cw[4], hz = cw[5], cr = cw[6];
-      const float sel_lx = j == 0 ? lx.x : j == 1 ? lx.y : j == 2 ? lx.z : lx.w;
-      const float sel_ly = j == 0 ? ly.x : j == 1 ? ly.y : j == 2 ? ly.z : ly.w;
-      const float sel_lz = j == 0 ? lz.x : j == 1 ? lz.y : j == 2 ? lz.z : lz.w;
-      const float sel_hx = j == 0 ? hx.x : j == 1 ? hx.y : j == 2 ? hx.z : hx.w;
-      const float sel_hy = j == 0 ? hy.x : j == 1 ? hy.y : j == 2 ? hy.z : hy.w;
-      const float sel_hz = j == 0 ? hz.x : j == 1 ? hz.y : j == 2 ? hz.z : hz.w;
-      const int g = __float_as_int(j == 0 ? cr.x : j == 1 ? cr.y : j == 2 ? cr.z : cr.w);
+      const int q = gslot;
+      const float sel_lx = q == 0 ? lx.x : q == 1 ? lx.y : q == 2 ? lx.z : lx.w;
+      const float sel_ly = q == 0 ? ly.x : q == 1 ? ly.y : q == 2 ? ly.z : ly.w;
+      const float sel_lz = q == 0 ? lz.x : q == 1 ? lz.y : q == 2 ? lz.z : lz.w;
+      const float sel_hx = q == 0 ? hx.x : q == 1 ? hx.y : q == 2 ? hx.z : hx.w;
+      const float sel_hy = q == 0 ? hy.x : q == 1 ? hy.y : q == 2 ? hy.z : hy.w;
+      const float sel_hz = q == 0 ? hz.x : q == 1 ? hz.y : q == 2 ? hz.z : hz.w;
+      const int g = __float_as_int(q == 0 ? cr.x : q == 1 ? cr.y : q == 2 ? cr.z : cr.w);
       const float t = slab(w.r, sel_lx, sel_ly, sel_lz, sel_hx, sel_hy, sel_hz);
       if (g < -1) {
         if (t <= cull_limit(w.h, w.tc)) {
@@ -322,16 +327,18 @@ __device__ __forceinline__ void split_init(Walk4& w, WalkStack& st, const BvhVie
     }
   }
 }
-// the group's best t so far (xor butterfly over the G = 4 lanes of the group); every lane of the
-// wave must call it
+// the group's best t so far (xor butterfly over the G lanes); every lane of the wave must call it
+template <int G>
 __device__ __forceinline__ float group_min_t(float t) {
-  t = fminf(t, __shfl_xor(t, 1, 64));
-  return fminf(t, __shfl_xor(t, 2, 64));
+#pragma unroll
+  for (int o = 1; o < G; o <<= 1) t = fminf(t, __shfl_xor(t, o, 64));
+  return t;
 }
 // lexicographic (t, face) minimum over the group; every lane of the wave must call it
+template <int G>
 __device__ __forceinline__ Hit group_hit(Hit h) {
 #pragma unroll
-  for (int o = 1; o <= 2; o <<= 1) {
+  for (int o = 1; o < G; o <<= 1) {
     const float t2 = __shfl_xor(h.t, o, 64);
     const int f2 = __shfl_xor(h.face, o, 64);
     const bool better = f2 >= 0 && (h.face < 0 || t2 < h.t || (t2 == h.t && f2 < h.face));

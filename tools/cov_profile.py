@@ -34,18 +34,20 @@ def main():
             if mode == "rays" and S > 1:
                 rays_case(case, m, grid, tx, win, B, env, S, reps)
                 continue
-            cov = Coverage(m, 2.998e8, 100e9, win, B, 1_000_000, grid, 0.1, device=0, shard_index=0, shard_count=S,
-                           env_mesh=env)
-            cov.run_device(tx)
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(reps):
+            per_rank = []
+            for r in range(S):  # cell shards: every rank's plan in turn (the slowest defines the map)
+                cov = Coverage(m, 2.998e8, 100e9, win, B, 1_000_000, grid, 0.1, device=0, shard_index=r,
+                               shard_count=S, env_mesh=env)
                 cov.run_device(tx)
-            torch.cuda.synchronize()
-            dt = (time.perf_counter() - t0) / reps
-            print(json.dumps({"case": case, "shards": S, "ms_per_map_rank0": dt * 1e3,
-                              "candidates_rank0": cov.last_candidates}), flush=True)
-            cov.close()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(reps):
+                    cov.run_device(tx)
+                torch.cuda.synchronize()
+                per_rank.append((time.perf_counter() - t0) / reps * 1e3)
+                cov.close()
+            print(json.dumps({"case": case, "mode": "cells", "shards": S, "ms_per_map_max_rank": max(per_rank),
+                              "ms_per_rank": [round(x, 3) for x in per_rank]}), flush=True)
         env.close()
 
 
