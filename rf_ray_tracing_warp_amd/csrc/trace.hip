@@ -53,6 +53,10 @@ __device__ __forceinline__ rt::Hit query_faces(Ptr tab, int nf, const rt::Shear&
   rt::Hit h;
   rt::hit_init(h);
   const int off = s.kcase * 3;
+#ifndef RT_FACE_UNROLL
+#define RT_FACE_UNROLL 2  // fewer loop branches / SALU per face (K2 170 -> 164 us with RT_BF_WAVES)
+#endif
+#pragma unroll RT_FACE_UNROLL
   for (int f = 0; f < nf; ++f) {
     const float4 q0 = tab[f * 18 + off + 0];
     const float4 q1 = tab[f * 18 + off + 1];
@@ -202,8 +206,14 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
   }
 }
 
+// brute-force kernels up to B = 3 are built for 7 waves per SIMD (72 VGPRs): with the face loop
+// unrolled by two (RT_FACE_UNROLL) the K2 kernel took 73 VGPRs (6 waves); bounded, 164 vs 170 us per
+// launch, bit-identical.  Longer paths keep their registers (their path points would spill).
+#ifndef RT_BF_WAVES
+#define RT_BF_WAVES 7
+#endif
 template <int B, bool USE_BVH>
-__global__ __launch_bounds__(256) void k_trace_bf(TraceArgs a) {
+__global__ __launch_bounds__(256, (B <= 3 ? RT_BF_WAVES : 1)) void k_trace_bf(TraceArgs a) {
   trace_body<B, USE_BVH>(a);
 }
 // BVH meshes: traversal is latency-bound (dependent node fetches), so the kernel is built for
