@@ -23,9 +23,6 @@ int hip_fail(hipError_t e, const char* what) {
   g_err = std::string(what) + ": " + hipGetErrorString(e);
   return RT_EHIP;
 }
-int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B, int64_t ray_offset, int64_t n,
-                 float* traced, float* received, uint32_t* mask, int32_t* hit_kind, int32_t* hit_face,
-                 hipStream_t stream, int32_t* chunk_counts = nullptr, bool* counted = nullptr);
 int build_bvh(rt_mesh* m, const std::vector<float>& tri);      // bvh.hip (host, binned SAH)
 int build_bvh_gpu(rt_mesh* m, const std::vector<float>& tri);  // bvh_gpu.hip (device LBVH)
 

@@ -20,9 +20,22 @@
 #include <algorithm>
 
 #include "../../include/rfrt.h"
+#include "rt_cir.h"
 #include "rt_internal.h"
 
 namespace {
+
+rt::CirConsts cir_consts(double amp0, double light_speed, double sample_rate, int flags, int64_t n_bins) {
+  rt::CirConsts k;
+  k.amp0 = amp0;
+  k.c32 = (float)light_speed;
+  k.fs32 = (float)sample_rate;
+  k.c64 = light_speed;
+  k.fs64 = sample_rate;
+  k.flags = flags;
+  k.n_bins = n_bins;
+  return k;
+}
 
 constexpr int TILE = 2048;  // flags per compaction tile (256 threads x 8)
 
@@ -125,79 +138,17 @@ __global__ __launch_bounds__(256) void k_scatter_fused(const uint32_t* mask, int
   }
 }
 
-// np.dot(float32[3], float32[3]): f32 products, summed in double left to right, rounded once
-__device__ __forceinline__ float npdot(const float* a, const float* b) {
-  const float p0 = a[0] * b[0], p1 = a[1] * b[1], p2 = a[2] * b[2];
-  return (float)(((double)p0 + (double)p1) + (double)p2);
+__device__ __forceinline__ void cir_one(const float* received, const int64_t* index, int64_t k, int P,
+                                        const rt::CirConsts& kc, int32_t* out_bin, double* out_amp) {
+  rt::cir_row(received + index[k] * (int64_t)(P * 3), P, kc, out_bin ? out_bin + k : nullptr,
+              out_amp ? out_amp + k : nullptr);
 }
-__device__ __forceinline__ float npnorm(const float* a) { return sqrtf(npdot(a, a)); }
-
-// Tracer._bounce_amplitude (tracer.py:34-61) for a float32 angle
-__device__ __forceinline__ double bounce_amplitude(float angle) {
-  if (isnan(angle)) return 0.0;
-  const float theta32 = 1.57079637050628662109375f - angle / 2.0f;  // f32(pi/2) - angle/2 in f32
-  const double theta = (double)theta32;
-  const double theta_i = asin(sin(theta) / 5.0);
-  const double num = cos(theta_i) - 5.0 * cos(theta);
-  const double den = cos(theta_i) + 5.0 * cos(theta);
-  const double q = num / den;
-  double amp = -(q * q);
-  if (amp < -1.0) amp = -1.0;
-  if (isnan(amp)) return 0.0;
-  return -amp;
-}
-
-__device__ void cir_one(const float* received, const int64_t* index, int64_t k, int P, double amp0, float c32,
-                        float fs32, double c64, double fs64, int flags, int64_t n_bins, double* ir, int32_t* out_bin,
-                        double* out_amp);
 
 __global__ __launch_bounds__(256) void k_cir(const float* received, const int64_t* index, const int64_t* count,
-                                             int P, double amp0, float c32, float fs32, double c64, double fs64,
-                                             int flags, int64_t n_bins, double* ir, int32_t* out_bin,
-                                             double* out_amp) {
+                                             int P, rt::CirConsts kc, int32_t* out_bin, double* out_amp) {
   const int64_t cnt = *count;
   for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < cnt; k += (int64_t)gridDim.x * blockDim.x)
-    cir_one(received, index, k, P, amp0, c32, fs32, c64, fs64, flags, n_bins, ir, out_bin, out_amp);
-}
-
-__device__ void cir_one(const float* received, const int64_t* index, int64_t k, int P, double amp0, float c32,
-                        float fs32, double c64, double fs64, int flags, int64_t n_bins, double* ir, int32_t* out_bin,
-                        double* out_amp) {
-  const float* row = received + index[k] * (int64_t)(P * 3);
-  // tracer.py:90-97: cut at the first point with a NaN component
-  int L = 0;
-  while (L < P && !(isnan(row[3 * L]) || isnan(row[3 * L + 1]) || isnan(row[3 * L + 2]))) ++L;
-  double amp = amp0;
-  float dist = 0.0f;
-  for (int j = 0; j + 2 < L; ++j) {
-    const float* p1 = row + 3 * j;
-    const float* p2 = p1 + 3;
-    const float* p3 = p2 + 3;
-    const float s1[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
-    const float s2[3] = {p3[0] - p2[0], p3[1] - p2[1], p3[2] - p2[2]};
-    const float l1 = npnorm(s1);
-    const float cosv = npdot(s1, s2) / (l1 * npnorm(s2));
-    const float angle = (float)acos((double)cosv);
-    amp *= bounce_amplitude(angle);
-    dist += l1;
-  }
-  if (L >= 2) {
-    const float* a = row + 3 * (L - 2);
-    const float d[3] = {a[0] - a[3], a[1] - a[4], a[2] - a[5]};
-    dist += npnorm(d);
-  }
-  // delay_samples = int((distance / light_speed_mps) * sample_rate_hz)   (tracer.py:115)
-  double dl;
-  if (flags & RT_CIR_C_F64) {
-    const double q = (double)dist / c64;
-    dl = q * fs64;
-  } else {
-    const float q = dist / c32;
-    dl = (flags & RT_CIR_FS_F64) ? (double)q * fs64 : (double)(q * fs32);
-  }
-  const int64_t bin = (int64_t)dl;  // int() truncates toward zero
-  if (out_bin) out_bin[k] = (int32_t)(bin < 2147483647 ? bin : 2147483647);
-  if (out_amp) out_amp[k] = amp;
+    cir_one(received, index, k, P, kc, out_bin, out_amp);
 }
 
 // impulse_response[bin] += amp for paths k = 0 .. count-1 in order (tracer.py:116-117): chunks of
@@ -234,15 +185,19 @@ __global__ __launch_bounds__(1024) void k_cir_accum(const int32_t* bins, const d
 // ------------------------------------------------------------------ fused compaction + CIR (rt_trace_cir)
 // K2's step after the trace kernel was five launches of a few microseconds each (count, scatter,
 // per-path CIR, ordered accumulation, impulse-response zeroing) for ~1 received row per 1M rays.
-// Here the trace kernel leaves received rows per 256-row chunk, and ONE launch of kFusedBlocks
-// blocks does the rest:
+// Brute-force meshes: the trace kernel itself finishes the step (trace.hip, fused tail): it lists
+// each 256-row chunk's received rows as it goes, and its last block to finish compacts them in
+// order and accumulates the impulse response.  BVH meshes trace in direction-sorted order, so
+// k_chunk_counts counts each chunk's rows from the mask and ONE launch of kFusedBlocks blocks does
+// the rest:
 //   block b owns chunks [b*C, (b+1)*C): the rows before them (a block reduction of the counts),
 //   its chunks' offsets (an LDS scan), the ordered indices of its received rows (wave ballots),
 //   and each of those rows' (bin, amplitude) -- computed by the lane that found the row;
-//   the last block to finish (an agent-scope release by every block, one atomic ticket) zeroes
-//   the impulse response and adds the amplitudes in path order (tracer.py:116-117), as k_cir_accum.
+//   the last block to finish (an agent-scope release by every block with rows, one atomic ticket)
+//   zeroes the impulse response and adds the amplitudes in path order (tracer.py:116-117).
+// Both leave the workspace's chunk counts zero and its ticket reset for the next call.
 constexpr int kFusedBlocks = 64;
-constexpr int kChunk = 256;
+constexpr int kChunk = (int)rt::kCirChunk;
 
 // received rows of every 256-row chunk from the mask (BVH / generic kernels, which do not count)
 __global__ __launch_bounds__(256) void k_chunk_counts(const uint32_t* mask, int64_t n, int32_t* counts) {
@@ -268,15 +223,11 @@ __device__ __forceinline__ int64_t block_sum_i64(int64_t v, int64_t* red) {
 
 struct CirArgs {
   const uint32_t* mask;
-  const int32_t* counts;
+  int32_t* counts;
   int64_t nchunks, n, cpb;  // cpb: chunks per block (<= kFusedMaxCpb)
   const float* received;
   int P;
-  double amp0;
-  float c32, fs32;
-  double c64, fs64;
-  int flags;
-  int64_t n_bins;
+  rt::CirConsts k;
   double* ir;
   int64_t* index;
   int64_t* count;
@@ -284,7 +235,7 @@ struct CirArgs {
   double* pamp;
   unsigned* done;
 };
-constexpr int kFusedMaxCpb = 2048;  // 256-row chunks per block: up to 2^25 rows per call
+constexpr int kFusedMaxCpb = (int)(rt::kCirMaxChunks / kFusedBlocks);  // up to 2^25 rows per call
 
 __global__ __launch_bounds__(256) void k_compact_cir(CirArgs a) {
   __shared__ int32_t off[kFusedMaxCpb];
@@ -296,6 +247,7 @@ __global__ __launch_bounds__(256) void k_compact_cir(CirArgs a) {
   const int64_t c1 = c0 + a.cpb < a.nchunks ? c0 + a.cpb : a.nchunks;
   // rows received before this block's chunks
   int64_t before = 0;
+#pragma unroll 8
   for (int64_t j = t; j < c0 && j < a.nchunks; j += 256) before += a.counts[j];
   const int64_t base = block_sum_i64(before, red);
   // exclusive scan of this block's chunk counts (serial over <= 2048 entries by thread 0 after a
@@ -329,8 +281,7 @@ __global__ __launch_bounds__(256) void k_compact_cir(CirArgs a) {
       const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
       const int64_t k = base + off[j] + pre + rank;
       a.index[k] = i;
-      cir_one(a.received, a.index, k, a.P, a.amp0, a.c32, a.fs32, a.c64, a.fs64, a.flags, a.n_bins, nullptr,
-              a.pbin, a.pamp);
+      cir_one(a.received, a.index, k, a.P, a.k, a.pbin, a.pamp);
     }
   }
   // publish, then the last block accumulates.  Only blocks that wrote rows release them: an
@@ -343,37 +294,16 @@ __global__ __launch_bounds__(256) void k_compact_cir(CirArgs a) {
   if (!last) return;
   __threadfence();
   int64_t tot = 0;
-  for (int64_t j = t; j < a.nchunks; j += 256) tot += a.counts[j];
+  for (int64_t j = t; j < a.nchunks; j += 256) {
+    tot += a.counts[j];
+    a.counts[j] = 0;  // every block has read its counts (ticket): leave them zero for the next call
+  }
   const int64_t cnt = block_sum_i64(tot, red);
   if (t == 0) {
     *a.count = cnt;
     *a.done = 0u;  // ready for the next call on this workspace
   }
-  if (!a.ir) return;
-  for (int64_t b = t; b < a.n_bins; b += 256) a.ir[b] = 0.0;
-  __syncthreads();
-  __shared__ int32_t sb[256];
-  __shared__ double sa[256];
-  for (int64_t b0 = 0; b0 < cnt; b0 += 256) {  // k_cir_accum's order, 256 paths at a time
-    const int64_t k = b0 + t;
-    const int32_t bb = k < cnt ? a.pbin[k] : -1;
-    sb[t] = (bb >= 0 && bb < a.n_bins) ? bb : -1;
-    sa[t] = k < cnt ? a.pamp[k] : 0.0;
-    __syncthreads();
-    const int32_t mb = sb[t];
-    if (mb >= 0) {
-      bool leader = true;
-      for (int j = 0; j < t && leader; ++j) leader = sb[j] != mb;
-      if (leader) {
-        const int mm = (int)(cnt - b0 < 256 ? cnt - b0 : 256);
-        double v = a.ir[mb];
-        for (int j = t; j < mm; ++j)
-          if (sb[j] == mb) v += sa[j];
-        a.ir[mb] = v;
-      }
-    }
-    __syncthreads();
-  }
+  if (a.ir) rt::ir_accumulate_block(a.pbin, a.pamp, cnt, a.k.n_bins, a.ir);
 }
 
 }  // namespace
@@ -412,8 +342,8 @@ int rt_compact(const uint32_t* row_mask, int64_t n, void* workspace, int64_t wor
 }
 
 int64_t rt_trace_cir_workspace_bytes(int64_t n) {
-  const int64_t nch = (n + kChunk - 1) / kChunk;
-  return 64 + nch * 4 + n * 12 + 64;  // done ticket, chunk counts, per-path bins + amplitudes
+  // ticket, chunk counts (fixed size), per-path amplitudes + bins, row within chunk; see rt_cir.h
+  return rt::kCirAmpOff + (n > 0 ? n : 0) * 25 + 64;
 }
 
 int rt_cir(const float* received, const int64_t* index, const int64_t* count, int64_t max_count, int max_bounces,
@@ -439,9 +369,8 @@ int rt_cir(const float* received, const int64_t* index, const int64_t* count, in
   // grid-stride loop covers larger counts; empty blocks cost launch time, not work
   const int64_t want = (max_count + 255) / 256;
   const unsigned grid = (unsigned)(want < 256 ? want : 256);
-  hipLaunchKernelGGL(k_cir, dim3(grid), dim3(256), 0, s, received, index, count, max_bounces + 1, amp0,
-                     (float)light_speed, (float)sample_rate, light_speed, sample_rate, flags, n_bins, nullptr, bins,
-                     amps);
+  hipLaunchKernelGGL(k_cir, dim3(grid), dim3(256), 0, s, received, index, count, max_bounces + 1,
+                     cir_consts(amp0, light_speed, sample_rate, flags, n_bins), bins, amps);
   if (impulse_response)
     hipLaunchKernelGGL(k_cir_accum, dim3(1), dim3(1024), 0, s, bins, amps, count, n_bins, impulse_response);
   RT_HIP(hipGetLastError());
@@ -452,11 +381,6 @@ int rt_cir(const float* received, const int64_t* index, const int64_t* count, in
 
 }  // extern "C"
 
-namespace rt {
-int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B, int64_t ray_offset, int64_t n,
-                 float* traced, float* received, uint32_t* mask, int32_t* hit_kind, int32_t* hit_face,
-                 hipStream_t stream, int32_t* chunk_counts, bool* counted);
-}
 
 extern "C" int rt_trace_cir(const rt_mesh* env, const float* tx_pos, const rt_mesh* rx, int max_bounces,
                             int64_t ray_offset, int64_t n, float* traced, float* received, uint32_t* row_mask,
@@ -474,7 +398,7 @@ extern "C" int rt_trace_cir(const rt_mesh* env, const float* tx_pos, const rt_me
   }
   const int64_t nch = (n + kChunk - 1) / kChunk;
   const int64_t cpb = (nch + kFusedBlocks - 1) / kFusedBlocks;
-  if (cpb > kFusedMaxCpb) {
+  if (nch > rt::kCirMaxChunks || cpb > kFusedMaxCpb) {
     rt::set_error("rt_trace_cir: more than 2^25 rays per call; shard the burst");
     return RT_EINVAL;
   }
@@ -490,39 +414,43 @@ extern "C" int rt_trace_cir(const rt_mesh* env, const float* tx_pos, const rt_me
     if (n_bins > 0) RT_HIP(hipMemsetAsync(impulse_response, 0, n_bins * 8, s));
     return RT_OK;
   }
+  // workspace (rt_cir.h): zero on entry -- the caller zero-fills it once, every call leaves the
+  // ticket and the chunk counts zero again
   char* ws = (char*)workspace;
-  unsigned* done = (unsigned*)ws;  // zero on entry: the caller zero-fills the workspace once
-  int32_t* counts = (int32_t*)(ws + 64);
-  double* pamp = (double*)(ws + 64 + ((nch * 4 + 7) / 8) * 8);
-  int32_t* pbin = (int32_t*)(pamp + n);
-  bool counted = false;
+  rt::TraceCirFused fz;
+  fz.done = (unsigned*)ws;
+  fz.counts = (int32_t*)(ws + rt::kCirCountsOff);
+  fz.pamp = (double*)(ws + rt::kCirAmpOff);
+  fz.pbin = (int32_t*)(fz.pamp + n);
+  fz.lrow = (uint8_t*)(fz.pbin + n);
+  fz.camp = (double*)(ws + rt::kCirAmpOff + ((n * 13 + 7) / 8) * 8);
+  fz.cbin = (int32_t*)(fz.camp + n);
+  fz.index = out_index;
+  fz.count = out_count;
+  fz.ir = n_bins > 0 ? impulse_response : nullptr;
+  fz.k = cir_consts(amp0, light_speed, sample_rate, flags, n_bins);
+  bool fused = false;
   int rc = rt::launch_trace(env, tx_pos, rx, max_bounces, ray_offset, n, traced, received, row_mask, nullptr, nullptr,
-                            s, counts, &counted);
+                            s, &fz, &fused);
   if (rc) return rc;
-  if (!counted)
-    hipLaunchKernelGGL(k_chunk_counts, dim3((unsigned)std::min<int64_t>(nch, 4096)), dim3(256), 0, s, row_mask, n,
-                       counts);
+  if (fused) return RT_OK;  // the trace kernel's last block did the compaction and the CIR
+  hipLaunchKernelGGL(k_chunk_counts, dim3((unsigned)std::min<int64_t>(nch, 4096)), dim3(256), 0, s, row_mask, n,
+                     fz.counts);
   CirArgs a;
   a.mask = row_mask;
-  a.counts = counts;
+  a.counts = fz.counts;
   a.nchunks = nch;
   a.n = n;
   a.cpb = cpb;
   a.received = received;
   a.P = max_bounces + 1;
-  a.amp0 = amp0;
-  a.c32 = (float)light_speed;
-  a.fs32 = (float)sample_rate;
-  a.c64 = light_speed;
-  a.fs64 = sample_rate;
-  a.flags = flags;
-  a.n_bins = n_bins;
-  a.ir = n_bins > 0 ? impulse_response : nullptr;
+  a.k = fz.k;
+  a.ir = fz.ir;
   a.index = out_index;
   a.count = out_count;
-  a.pbin = pbin;
-  a.pamp = pamp;
-  a.done = done;
+  a.pbin = fz.pbin;
+  a.pamp = fz.pamp;
+  a.done = fz.done;
   hipLaunchKernelGGL(k_compact_cir, dim3(kFusedBlocks), dim3(256), 0, s, a);
   RT_HIP(hipGetLastError());
   return RT_OK;

@@ -78,6 +78,12 @@ inline BvhView bvh_view(const rt_mesh* m) {
 int pack_leaf_refs(rt_mesh* m);
 // After pack_leaf_refs: the 4-wide copy of the tree that rt::bvh4_query traverses (bvh_wide.hip)
 int build_wide(rt_mesh* m);
+// rt_trace's launch (trace.hip).  fused (rt_trace_cir, optional): the brute-force kernels finish
+// the CIR step in their last block (rt_cir.h); *fused_done tells whether this launch did.
+struct TraceCirFused;
+int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B, int64_t ray_offset, int64_t n,
+                 float* traced, float* received, uint32_t* mask, int32_t* hit_kind, int32_t* hit_face,
+                 hipStream_t stream, const TraceCirFused* fused = nullptr, bool* fused_done = nullptr);
 }  // namespace rt
 
 #define RT_HIP(call)                                                   \

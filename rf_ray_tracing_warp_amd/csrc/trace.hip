@@ -20,6 +20,7 @@
 #include <mutex>
 
 #include "rt_bvh.h"
+#include "rt_cir.h"
 #include "rt_device.h"
 #include "rt_internal.h"
 
@@ -43,7 +44,8 @@ struct TraceArgs {
   int32_t* hit_kind;  // (n, B) or null
   int32_t* hit_face;  // (n, B) or null
   const int32_t* order;  // processing order of the rows (null = identity), see launch_trace
-  int32_t* chunk_counts;  // brute-force kernels: received rows per 256-row chunk (rt_trace_cir), or null
+  bool fused;             // brute-force kernels under rt_trace_cir: finish the CIR step (fused_tail)
+  rt::TraceCirFused fz;
 };
 
 // Closest hit over a brute-force face list whose permuted table lives at `tab`
@@ -111,6 +113,70 @@ __device__ __forceinline__ void stage_env(const TraceArgs& a, float4* lds_tab) {
   }
 }
 
+// rt_trace_cir's tail (tracer.py:87-117), run by the last block of the trace kernel to finish.
+// A block that finds received rows computes their (bin, amplitude) itself, in chunk-local slots,
+// and releases them (an agent-scope release writes its XCD's L2 back: rare, ~1 block per 1M-ray
+// K2 burst) before taking its ticket.  The last ticket holder acquires, scans the chunk counts
+// into the ordered index list (tracer.py:87, ray order), compacts the slots in that order, zeroes
+// the counts it used and accumulates the impulse response in path order (rt_cir.h).  This
+// replaces a second launch (its ~5 us gap and ~18 us of latency-bound work): K2 step 153 -> 142 us
+// (tools/k2_fused_variants.py).  Measured pieces: tickets + release + acquire ~2 us, the tail's
+// scan/compaction/impulse response ~3 us; the per-path double arithmetic after the bounce loop
+// costs the trace loop ~2 us in spilled registers, but in the tail (one thread per path, serial
+// on the critical path) the step took 149-159 us depending on where the compiler spilled.
+template <int B>
+__device__ __forceinline__ void fused_tail(const TraceArgs& a, bool published) {
+  __shared__ int s_last;
+  __shared__ int64_t wsum[4];
+  if (published) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(a.fz.done, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int64_t nch = (a.n + 255) / 256;
+  const int64_t q = (nch + 255) / 256;  // contiguous chunks per thread
+  const int64_t c0 = (int64_t)t * q < nch ? (int64_t)t * q : nch;
+  const int64_t c1 = c0 + q < nch ? c0 + q : nch;
+  int64_t own = 0;
+#pragma unroll 8
+  for (int64_t c = c0; c < c1; ++c) own += a.fz.counts[c];
+  // exclusive scan of the per-thread sums over the block
+  int64_t incl = own;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t v = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += v;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  int64_t k = incl - own;
+  for (int j = 0; j < w; ++j) k += wsum[j];
+  const int64_t total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  if (own > 0) {
+    for (int64_t c = c0; c < c1; ++c) {
+      const int32_t v = a.fz.counts[c];
+      if (v == 0) continue;
+      for (int32_t r = 0; r < v; ++r) {
+        const int64_t slot = c * 256 + r;
+        const int64_t row = c * 256 + a.fz.lrow[slot];
+        a.fz.index[k + r] = row;
+        a.fz.cbin[k + r] = a.fz.pbin[slot];
+        a.fz.camp[k + r] = a.fz.pamp[slot];
+      }
+      a.fz.counts[c] = 0;
+      k += v;
+    }
+  }
+  if (t == 0) {
+    *a.fz.count = total;
+    *a.fz.done = 0u;  // ready for the next call on this workspace
+  }
+  if (!a.fz.ir) return;
+  __syncthreads();
+  rt::ir_accumulate_block(a.fz.cbin, a.fz.camp, total, a.fz.k.n_bins, a.fz.ir);
+}
+
 template <int B, bool USE_BVH>
 __device__ __forceinline__ void trace_body(const TraceArgs& a) {
   constexpr int P = B + 1;
@@ -118,8 +184,9 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
   stage_env<USE_BVH>(a, lds_tab);
 
   const float qnan = __builtin_nanf("");
+  bool published = false;  // this block listed received rows (rt_trace_cir)
   // block-uniform loop over 256-row chunks (the same rows per thread as a grid-stride loop), so the
-  // block can count its chunk's received rows for rt_trace_cir
+  // block can list its chunk's received rows for rt_trace_cir
   for (int64_t chunk = blockIdx.x; chunk * 256 < a.n; chunk += gridDim.x) {
     const int64_t irow = chunk * 256 + threadIdx.x;
     bool got = false;
@@ -195,13 +262,41 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
     if (a.mask) a.mask[row] = last_rx >= 0 ? 1u : 0u;
     got = last_rx >= 0;
     }
-    if (!USE_BVH && a.chunk_counts) {  // row order == chunk order here (no direction sort)
+    if (!USE_BVH && a.fused) {  // row order == chunk order here (no direction sort)
+      // list this chunk's received rows (row within the chunk, in row order) and count them; the
+      // counts stay zero (the workspace invariant) for chunks without one
       __shared__ int32_t wcnt[4];
       const uint64_t m = __ballot(got);
       if ((threadIdx.x & 63) == 0) wcnt[threadIdx.x >> 6] = (int32_t)__popcll(m);
       __syncthreads();
-      if (threadIdx.x == 0) a.chunk_counts[chunk] = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+      const int32_t tot = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+      if (tot > 0) {  // block-uniform
+        if (got) {  // the row's slot in its chunk
+          const int w = threadIdx.x >> 6;
+          int32_t r = (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+          for (int q = 0; q < w; ++q) r += wcnt[q];
+          a.fz.lrow[chunk * 256 + r] = (uint8_t)threadIdx.x;
+        }
+        if (threadIdx.x == 0) a.fz.counts[chunk] = tot;
+        published = true;
+      }
       __syncthreads();
+    }
+  }
+  if constexpr (!USE_BVH) {
+    if (a.fused) {
+      if (published) {  // block-uniform: each listed path's (bin, amplitude) in its chunk slot,
+                        // after the bounce loop so its double arithmetic does not share registers
+        for (int64_t chunk = blockIdx.x; chunk * 256 < a.n; chunk += gridDim.x) {
+          const int32_t c = a.fz.counts[chunk];  // this block's own (zero unless listed here)
+          if (threadIdx.x < c) {
+            const int64_t slot = chunk * 256 + threadIdx.x;
+            rt::cir_row(a.received + (chunk * 256 + a.fz.lrow[slot]) * (B + 1) * 3, B + 1, a.fz.k,
+                        a.fz.pbin + slot, a.fz.pamp + slot);
+          }
+        }
+      }
+      fused_tail<B>(a, published);
     }
   }
 }
@@ -379,14 +474,15 @@ const int32_t* dir_order(int64_t ray_offset, int64_t n, hipStream_t stream, void
 void trace_mark(int i, hipStream_t s);
 void trace_events(hipEvent_t* e0, hipEvent_t* e1);
 
-// chunk_counts (optional, rt_trace_cir): received rows per 256-row chunk, written by the
-// brute-force kernels as they go; *counted tells whether they did (BVH and generic kernels: no)
+// fused (optional, rt_trace_cir): the brute-force kernels list each chunk's received rows as they go
+// and their last block finishes the CIR step; *fused_done tells whether they did (BVH and generic
+// kernels: no, rt_trace_cir then launches k_chunk_counts + k_compact_cir)
 int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B, int64_t ray_offset, int64_t n,
                  float* traced, float* received, uint32_t* mask, int32_t* hit_kind, int32_t* hit_face,
-                 hipStream_t stream, int32_t* chunk_counts, bool* counted) {
-  if (counted) *counted = false;
+                 hipStream_t stream, const TraceCirFused* fused, bool* fused_done) {
+  if (fused_done) *fused_done = false;
   if (n == 0) return 0;
-  TraceArgs a;
+  TraceArgs a{};
   a.env_perm = env->perm;
   a.env_nrm = env->nrm;
   a.env_nf = (int)env->nf;
@@ -407,8 +503,9 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
   a.hit_kind = hit_kind;
   a.hit_face = hit_face;
   a.order = nullptr;
-  a.chunk_counts = (!bvh && B <= 8) ? chunk_counts : nullptr;
-  if (counted) *counted = a.chunk_counts != nullptr;
+  a.fused = fused && !bvh && B <= 8;  // the register-resident brute-force kernels
+  if (a.fused) a.fz = *fused;
+  if (fused_done) *fused_done = a.fused;
   const size_t lds = bvh ? 0 : (size_t)env->nf * 18 * sizeof(float4);
   int dev_cu = 256;
   const int64_t want = (n + 255) / 256;
