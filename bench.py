@@ -2,12 +2,12 @@
 """Headline benchmark: ray-bounces/s on models/room.stl (BASELINE.json configs[1], "K2").
 
 One step = one pass of the hot path over one synthetic isotropic burst of 1M rays per GPU, one
-rt_trace_cir call (two launches):
+rt_trace_cir call (one launch on room.stl's brute-force mesh):
   trace kernel (trace_paths_kernel, kernel.py:38-98: ray generation, 3 bounces of closest hit vs
               receiver + environment, reflect, full reference output contract: traced_paths,
-              received_paths, row_mask -- tracer.py:70-72)
-  fused compaction + CIR (tracer.py:87-117: received rows in ray order -> delay bins -> impulse
-              response, zeroed and accumulated in ray order)
+              received_paths, row_mask -- tracer.py:70-72), whose last block to finish does the
+              compaction + CIR (tracer.py:87-117: received rows in ray order -> delay bins ->
+              impulse response, zeroed and accumulated in ray order)
   RCCL all-reduce of the impulse response (N > 1: the job's CIR is the sum over ray shards).
 Rays are sharded by global ray id (rank r traces ids [r*N, (r+1)*N)): per-GPU work is fixed as
 GPUs are added ("weak").  Inputs (mesh tables) are resident in HBM before the timed region.
@@ -55,6 +55,9 @@ def parse():
     ap.add_argument("--settle-steps", type=int, default=250,
                     help="untimed steps before the warmup (~40 ms of K2): the GPU clock ramps up over the "
                          "first tens of ms of load (K2 trace kernel 148 -> 141 us); the same count on every rank")
+    ap.add_argument("--profile-every", type=int, default=8,
+                    help="K2: every k-th launch of the timed loop carries the start/stop events the kernel "
+                         "time comes from (each such launch costs the stream a few us; 1 = all)")
     ap.add_argument("--legs", default="k2,k3,k4,k5", help="comma list of k2 (always run), k3, k4, k5")
     ap.add_argument("--rays", type=int, default=1_000_000, help="rays per GPU per step (K2: 1M)")
     ap.add_argument("--bounces", type=int, default=3)
@@ -458,7 +461,7 @@ def main():
     torch.cuda.synchronize()
     # trace-kernel time from the events its own dispatch packets carry (no marker packets in the
     # timed stream; rt_trace_profile_stats after the loop)
-    L.rt_profile(1)
+    L.rt_profile(args.profile_every)
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i)
@@ -534,6 +537,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": f"k_trace_bf<{B}>", "kernel_ms": kern_ms,
+                         "launches_timed": int(pst[0]), "launch_sampling": f"every {args.profile_every}",
                          "algorithmic_bytes_per_launch": bytes_per_launch},
             "compute_roofline": valu,
             "received_rows_last_step": received_rows,

@@ -170,7 +170,9 @@ int rt_power_dense(const double* impulse_responses, int64_t rows, int64_t n_bins
 int rt_coverage_profile(rt_coverage* cov, int enable);
 /* Process-wide rt_trace / rt_trace_cir timing: rt_profile(1) (re)starts recording the start and
  * stop of every later trace kernel through its own dispatch packet (hipExtLaunchKernelGGL: no
- * marker packets in the stream) and brackets BVH ray-order sorts with events.
+ * marker packets in the stream) and brackets BVH ray-order sorts with events; rt_profile(k), k > 1,
+ * records every k-th launch only (a launch that carries events costs the stream a few us);
+ * rt_profile(0) stops.
  * rt_trace_last_profile fills out[0] = trace kernel ms, out[1] = ray-order sort ms (NaN when not
  * recorded) of the last call; rt_trace_profile_stats out = [launches, mean, min, max ms] over the
  * (last 512) kernels recorded since rt_profile(1).  Both synchronise. */

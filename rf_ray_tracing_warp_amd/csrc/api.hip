@@ -44,6 +44,7 @@ __global__ void k_pack_leaf_refs(float4* nodes, const int2* leaves, int64_t nnod
 
 int g_poison = -1;
 extern bool g_profile;                      // trace.hip
+extern int g_profile_every;                 // trace.hip
 int trace_last_profile(double* out, int n);  // trace.hip
 int trace_profile_stats(double* out, int n);  // trace.hip
 void profile_reset();                        // trace.hip
@@ -78,8 +79,13 @@ const char* rt_last_error(void) { return rt::g_err.c_str(); }
 int rt_version(void) { return RFRT_VERSION; }
 
 int rt_profile(int enable) {
-  if (enable && !rt::g_profile) rt::profile_reset();
+  if (enable < 0) {
+    rt::set_error("rt_profile: enable must be 0, 1 or a sampling period > 1");
+    return RT_EINVAL;
+  }
+  if (enable && (!rt::g_profile || rt::g_profile_every != enable)) rt::profile_reset();
   rt::g_profile = enable != 0;
+  rt::g_profile_every = enable > 1 ? enable : 1;
   return RT_OK;
 }
 

@@ -560,10 +560,12 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
 }
 
 // rt_profile / rt_trace_last_profile / rt_trace_profile_stats: while profiling is on, every trace
-// kernel launch records its start/stop in a ring of event pairs (through its dispatch packet), and
-// BVH launches bracket their ray-order sort with markers.  Process-wide, for measurement; not
-// thread-safe.
+// kernel launch (or every g_profile_every-th, rt_profile(k > 1)) records its start/stop in a ring of
+// event pairs (through its dispatch packet), and BVH launches bracket their ray-order sort with
+// markers.  Process-wide, for measurement; not thread-safe.
 bool g_profile = false;
+int g_profile_every = 1;
+static int64_t g_launches = 0;
 constexpr int kRing = 512;
 static hipEvent_t g_ring[kRing][2] = {};
 static int64_t g_ring_n = 0;
@@ -571,11 +573,12 @@ static hipEvent_t g_tev[2] = {};
 static bool g_trec[2] = {};
 void profile_reset() {
   g_ring_n = 0;
+  g_launches = 0;
   g_trec[0] = g_trec[1] = false;
 }
 void trace_events(hipEvent_t* e0, hipEvent_t* e1) {
   *e0 = *e1 = nullptr;
-  if (!g_profile) return;
+  if (!g_profile || g_launches++ % g_profile_every != 0) return;
   hipEvent_t* p = g_ring[g_ring_n % kRing];
   for (int i = 0; i < 2; ++i)
     if (!p[i] && hipEventCreate(&p[i]) != hipSuccess) return;

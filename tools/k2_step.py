@@ -35,18 +35,24 @@ def main():
         check(L.rt_trace_cir(env.handle, tx.ctypes.data, rx.handle, B, 0, N, ptr(tr), ptr(rc), ptr(mk), 1e-6, 2.998e8,
                              100e9, cir_flags(2.998e8, 100e9), 10000, ptr(ir), ptr(idx), ptr(cnt), ptr(ws), ws.numel(),
                              s), "rt_trace_cir")
-    for prof in (0, 1, 0, 1):
+    for _ in range(250):  # settle the clock
+        step()
+    torch.cuda.synchronize()
+    for prof in (0, 1, 8, 0, 1, 8):
         for _ in range(5):
             step()
         torch.cuda.synchronize()
         L.rt_profile(prof)
         t0 = time.perf_counter()
-        for _ in range(50):
+        for _ in range(200):
             step()
         torch.cuda.synchronize()
-        dt = (time.perf_counter() - t0) / 50
+        dt = (time.perf_counter() - t0) / 200
+        st = np.zeros(4)
+        L.rt_trace_profile_stats(st.ctypes.data, 4)
         L.rt_profile(0)
-        print(f"profile={prof}: {dt * 1e6:.1f} us/step", flush=True)
+        print(f"profile={prof}: {dt * 1e6:.1f} us/step, {int(st[0]) if prof else 0} launches timed, "
+              f"kernel {st[1] * 1e3 if prof else float('nan'):.1f} us", flush=True)
 
 
 if __name__ == "__main__":
