@@ -343,7 +343,7 @@ int rt_compact(const uint32_t* row_mask, int64_t n, void* workspace, int64_t wor
 
 int64_t rt_trace_cir_workspace_bytes(int64_t n) {
   // ticket, chunk counts (fixed size), per-path amplitudes + bins, row within chunk; see rt_cir.h
-  return rt::kCirAmpOff + (n > 0 ? n : 0) * 25 + 64;
+  return rt::kCirAmpOff + (n > 0 ? n : 0) * 24 + 64;
 }
 
 int rt_cir(const float* received, const int64_t* index, const int64_t* count, int64_t max_count, int max_bounces,
@@ -422,8 +422,9 @@ extern "C" int rt_trace_cir(const rt_mesh* env, const float* tx_pos, const rt_me
   fz.counts = (int32_t*)(ws + rt::kCirCountsOff);
   fz.pamp = (double*)(ws + rt::kCirAmpOff);
   fz.pbin = (int32_t*)(fz.pamp + n);
-  fz.lrow = (uint8_t*)(fz.pbin + n);
-  fz.camp = (double*)(ws + rt::kCirAmpOff + ((n * 13 + 7) / 8) * 8);
+  fz.masks = (uint64_t*)(ws + rt::kCirMasksOff);
+  fz.gcounts = (int32_t*)(ws + rt::kCirGroupCountsOff);
+  fz.camp = (double*)(ws + rt::kCirAmpOff + ((n * 12 + 7) / 8) * 8);
   fz.cbin = (int32_t*)(fz.camp + n);
   fz.index = out_index;
   fz.count = out_count;
@@ -433,7 +434,7 @@ extern "C" int rt_trace_cir(const rt_mesh* env, const float* tx_pos, const rt_me
   int rc = rt::launch_trace(env, tx_pos, rx, max_bounces, ray_offset, n, traced, received, row_mask, nullptr, nullptr,
                             s, &fz, &fused);
   if (rc) return rc;
-  if (fused) return RT_OK;  // the trace kernel's last block did the compaction and the CIR
+  if (fused) return RT_OK;  // the trace kernel and its tail kernel did the compaction and the CIR
   hipLaunchKernelGGL(k_chunk_counts, dim3((unsigned)std::min<int64_t>(nch, 4096)), dim3(256), 0, s, row_mask, n,
                      fz.counts);
   CirArgs a;

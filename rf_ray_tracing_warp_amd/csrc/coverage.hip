@@ -93,17 +93,28 @@ __device__ __forceinline__ void cell_center(const rt_grid& g, int64_t cell, doub
 
 // environment closest hit from the LDS table (same code path as the trace kernel)
 __device__ __forceinline__ rt::Hit env_query_lds(const float4* tab, int nf, const rt::Shear& s) {
+#if RT_LAZY_HIT
+  rt::LazyHit h;  // faces in ascending order: the division waits for the winner (rt_device.h)
+  rt::lazy_init(h);
+#else
   rt::Hit h;
   rt::hit_init(h);
+#endif
   const int off = s.kcase * 3;
   for (int f = 0; f < nf; ++f) {
     const float4 q0 = tab[f * 18 + off + 0];
     const float4 q1 = tab[f * 18 + off + 1];
     const float c2 = tab[f * 18 + off + 2].x;
     float T, det;
+#if RT_LAZY_HIT
+    if (rt::tri_test(s, q0, q1, c2, T, det)) rt::lazy_consider(h, T, det, f);
+  }
+  return rt::lazy_finish(h);
+#else
     if (rt::tri_test(s, q0, q1, c2, T, det)) rt::hit_consider(h, T, det, f);
   }
   return h;
+#endif
 }
 
 template <bool USE_BVH>

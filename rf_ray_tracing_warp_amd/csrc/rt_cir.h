@@ -117,24 +117,56 @@ __device__ __forceinline__ void ir_accumulate_block(const int32_t* pbin, const d
   }
 }
 
+// One wave (64 lanes), no block barriers: the same result as ir_accumulate_block, 64 paths at a
+// time; a lane whose bin no earlier lane of the batch holds adds that bin's amplitudes in path
+// order (through wave shuffles).
+__device__ __forceinline__ void ir_accumulate_wave(const int32_t* pbin, const double* pamp, int64_t cnt,
+                                                   int64_t n_bins, double* ir, bool zero = true) {
+  const int lane = threadIdx.x & 63;
+  if (zero)  // else the caller zeroed ir and synchronised
+    for (int64_t b = lane; b < n_bins; b += 64) ir[b] = 0.0;
+  for (int64_t b0 = 0; b0 < cnt; b0 += 64) {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // this wave's earlier ir stores first
+    const int64_t k = b0 + lane;
+    const int32_t bb = k < cnt ? pbin[k] : -1;
+    const int32_t mb = (bb >= 0 && bb < n_bins) ? bb : -1;
+    const double am = k < cnt ? pamp[k] : 0.0;
+    bool leader = mb >= 0;
+    for (int j = 0; j < 64; ++j) {  // wave-uniform trip counts: every lane takes part in the shuffles
+      const int32_t bj = __shfl(mb, j, 64);
+      if (j < lane && bj == mb) leader = false;
+    }
+    double v = (leader && b0 > 0) ? ir[mb] : 0.0;  // the first 64 paths add to the zeros just written
+    for (int j = 0; j < 64; ++j) {
+      const int32_t bj = __shfl(mb, j, 64);
+      const double aj = __shfl(am, j, 64);
+      if (j >= lane && bj == mb) v += aj;
+    }
+    if (leader) ir[mb] = v;
+  }
+}
+
 // rt_trace_cir's workspace: [0, 64) done ticket | counts of received rows per 256-row chunk,
-// kCirMaxChunks slots at a fixed offset (all zero between calls, whatever n the workspace was
-// last used with) | per path f64 amplitude [n] | per path int32 bin [n] | row within its chunk, u8
-// [n] -- the last three in chunk-local slots (chunk * 256 + rank in the chunk) when the trace
-// kernel fills them, in path order otherwise | the fused tail's path-ordered f64 amplitudes [n]
-// and int32 bins [n]
+// kCirMaxChunks int32 | the same per group of 64 chunks | per chunk a 256-bit mask of its received rows, kCirMaxChunks x 4 u64 --
+// both at fixed offsets and all zero between calls, whatever n the workspace was last used with |
+// per path f64 amplitude [n] | per path int32 bin [n] (at the row's index when the trace kernel
+// fills them, in path order otherwise) | the fused tail's path-ordered f64 amplitudes [n] and
+// int32 bins [n]
 constexpr int64_t kCirChunk = 256;
 constexpr int64_t kCirMaxChunks = (int64_t)1 << 17;  // 2^25 rows per call
 constexpr int64_t kCirCountsOff = 64;
-constexpr int64_t kCirAmpOff = kCirCountsOff + kCirMaxChunks * 4;
+constexpr int64_t kCirGroupCountsOff = kCirCountsOff + kCirMaxChunks * 4;  // per 64 chunks (fused tail)
+constexpr int64_t kCirMasksOff = kCirGroupCountsOff + kCirMaxChunks / 64 * 4;
+constexpr int64_t kCirAmpOff = kCirMasksOff + kCirMaxChunks * 32;
 
 // The brute-force trace kernel's fused tail (trace.hip): set by rt_trace_cir, consumed by
 // launch_trace when the kernel can count its chunks in row order
 struct TraceCirFused {
   int32_t* counts;
+  int32_t* gcounts;  // per 64 chunks
   double* pamp;
   int32_t* pbin;
-  uint8_t* lrow;
+  uint64_t* masks;
   double* camp;  // path order
   int32_t* cbin;
   unsigned* done;

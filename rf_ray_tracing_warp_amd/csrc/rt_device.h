@@ -14,6 +14,9 @@
 #include <stdint.h>
 
 #define RT_MAX_T 1.0e6f  // kernel.py:71,82 max_t
+#ifndef RT_LAZY_HIT
+#define RT_LAZY_HIT 1  // brute-force face loops defer the IEEE division (LazyHit); 0 = per-face screen
+#endif
 
 namespace rt {
 
@@ -175,6 +178,52 @@ __device__ __forceinline__ void hit_update_exact(Hit& h, float T, float det, int
 __device__ __forceinline__ void hit_consider(Hit& h, float T, float det, int face) {
   const float a = fabsf(T) * __builtin_amdgcn_rcpf(fabsf(det));
   if (!(a > h.t * 1.0000153f)) hit_update_exact(h, T, det, face);
+}
+
+// Closest hit over faces tested in ASCENDING face order (the brute-force loops), with the IEEE
+// division deferred.  A later face can only win by a strictly smaller t (ties keep the lower face
+// id, which came first), so the state is the best candidate's (T, det), its approximate t
+// a = |T| * v_rcp(|det|) (within ~2^-21 of the exact T * (1/det) for normal values), and its face.
+//   a > best.a * (1 + 2^-16)                  cannot win: skip (as hit_consider)
+//   a < best.a * (1 - 2^-16), both normal     wins outright (exact t < exact best t); a self-hit
+//                                             at T == 0 against a normal best also wins outright
+//   otherwise (near tie, tiny, odd det)       the exact rule of hit_update_exact
+// An accepted T == 0 is t = +-0, which no later face can beat, so the lane then skips the rest.
+// lazy_finish computes the winner's t = T * (1/det) once per query: the decision and every output
+// bit equal hit_update_exact's, with one division per query instead of one per competitive face.
+struct LazyHit {
+  float T, det, a;
+  int face;
+};
+__device__ __forceinline__ void lazy_init(LazyHit& h) {
+  h.T = RT_MAX_T;  // the "no hit" sentinel t = 1e6 * (1 / 1) = 1e6, face -1
+  h.det = 1.0f;
+  h.a = RT_MAX_T;
+  h.face = -1;
+}
+__device__ __forceinline__ void lazy_consider(LazyHit& h, float T, float det, int face) {
+  const float a = fabsf(T) * __builtin_amdgcn_rcpf(fabsf(det));
+  if ((a > h.a * 1.0000153f) | (h.T == 0.0f)) return;
+  bool take;
+  if ((a < h.a * 0.9999847f) &
+      ((a >= 1e-30f) | ((T == 0.0f) & (fabsf(det) >= 0x1p-125f) & (h.a >= 1e-30f)))) {
+    take = true;
+  } else {
+    const float t = T * (1.0f / det), tb = h.T * (1.0f / h.det);
+    take = (t < tb) & (t >= 0.0f) & (t < RT_MAX_T);
+  }
+  if (take) {
+    h.T = T;
+    h.det = det;
+    h.a = a;
+    h.face = face;
+  }
+}
+__device__ __forceinline__ Hit lazy_finish(const LazyHit& h) {
+  Hit r;
+  r.t = h.T * (1.0f / h.det);
+  r.face = h.face;
+  return r;
 }
 
 }  // namespace rt

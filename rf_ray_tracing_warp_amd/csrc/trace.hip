@@ -44,7 +44,7 @@ struct TraceArgs {
   int32_t* hit_kind;  // (n, B) or null
   int32_t* hit_face;  // (n, B) or null
   const int32_t* order;  // processing order of the rows (null = identity), see launch_trace
-  bool fused;             // brute-force kernels under rt_trace_cir: finish the CIR step (fused_tail)
+  bool fused;             // brute-force kernels under rt_trace_cir: list received rows, per-path CIR
   rt::TraceCirFused fz;
 };
 
@@ -52,8 +52,13 @@ struct TraceArgs {
 // (LDS for the environment, global for the receiver).
 template <typename Ptr>
 __device__ __forceinline__ rt::Hit query_faces(Ptr tab, int nf, const rt::Shear& s) {
+#if RT_LAZY_HIT
+  rt::LazyHit h;  // faces in ascending order: the division waits for the winner (rt_device.h)
+  rt::lazy_init(h);
+#else
   rt::Hit h;
   rt::hit_init(h);
+#endif
   const int off = s.kcase * 3;
 #ifndef RT_FACE_UNROLL
 #define RT_FACE_UNROLL 2  // fewer loop branches / SALU per face (K2 170 -> 164 us with RT_BF_WAVES)
@@ -64,9 +69,15 @@ __device__ __forceinline__ rt::Hit query_faces(Ptr tab, int nf, const rt::Shear&
     const float4 q1 = tab[f * 18 + off + 1];
     const float c2 = tab[f * 18 + off + 2].x;
     float T, det;
+#if RT_LAZY_HIT
+    if (rt::tri_test(s, q0, q1, c2, T, det)) rt::lazy_consider(h, T, det, f);
+  }
+  return rt::lazy_finish(h);
+#else
     if (rt::tri_test(s, q0, q1, c2, T, det)) rt::hit_consider(h, T, det, f);
   }
   return h;
+#endif
 }
 
 // Can a receiver hit possibly be nearer than t_limit?  Conservative: the receiver's faces all
@@ -104,6 +115,87 @@ __device__ __forceinline__ rt::Hit env_hit_query(const TraceArgs& a, const float
   }
 }
 
+// ------------------------------------------------------------------ bounce-0 candidate faces
+// Every ray of a burst starts at the TX, so the directions that can hit face f at bounce 0 form
+// the cone spanned by the TX and the face's corners: d must lie on the inner side of the three
+// planes through the TX and each edge -- the signs the watertight test's U, V, W compute, up to
+// rounding.  Each block stages, per face, the three unit inner edge normals e_i (double, from the
+// identity-permuted corners) and a margin m; a lane keeps face f as a bounce-0 candidate when
+// e_i . d >= -m for all three.  m = 1e-3 rad plus 64 ulp of the scene's coordinate scale over the
+// face's nearest corner distance -- far wider than the watertight test's rounding of U, V, W, so
+// no face the test could accept is dropped; faces that are degenerate or within 1e-3 * scale of
+// the TX get zero normals (always candidates).  The lane then runs the exact test over its
+// candidates only, in ascending face order (room.stl: 1.8 candidates per ray, 4.1 per wave, of
+// 44 faces), so every output bit is unchanged.
+constexpr int kConeMaxFaces = 64;  // candidate set = one 64-bit mask per lane
+#ifndef RT_CONE
+#define RT_CONE 1  // 0: bounce 0 tests every face (A/B builds)
+#endif
+
+__device__ __forceinline__ void stage_cones(const TraceArgs& a, float4* cone) {
+  for (int f = threadIdx.x; f < a.env_nf; f += blockDim.x) {
+    const float4 q0 = a.env_perm[f * 18 + 12], q1 = a.env_perm[f * 18 + 13];  // case 4: kx,ky,kz = x,y,z
+    const float c2 = a.env_perm[f * 18 + 14].x;
+    const double o[3] = {a.tx[0], a.tx[1], a.tx[2]};
+    const double v[3][3] = {{q0.x - o[0], q0.y - o[1], q0.z - o[2]},
+                            {q0.w - o[0], q1.x - o[1], q1.y - o[2]},
+                            {q1.z - o[0], q1.w - o[1], c2 - o[2]}};
+    double scale = fmax(fmax(fabs(o[0]), fabs(o[1])), fabs(o[2]));
+    scale = fmax(scale, fmax(fmax(fabs((double)q0.x), fabs((double)q0.y)), fabs((double)q0.z)));
+    scale = fmax(scale, fmax(fmax(fabs((double)q0.w), fabs((double)q1.x)), fabs((double)q1.y)));
+    scale = fmax(scale, fmax(fmax(fabs((double)q1.z), fabs((double)q1.w)), fabs((double)c2)));
+    double len[3], n[3][3];
+    for (int i = 0; i < 3; ++i) {
+      const double* p = v[i];
+      const double* q = v[(i + 1) % 3];
+      n[i][0] = p[1] * q[2] - p[2] * q[1];
+      n[i][1] = p[2] * q[0] - p[0] * q[2];
+      n[i][2] = p[0] * q[1] - p[1] * q[0];
+      len[i] = sqrt(p[0] * p[0] + p[1] * p[1] + p[2] * p[2]);
+    }
+    const double det = n[0][0] * v[2][0] + n[0][1] * v[2][1] + n[0][2] * v[2][2];
+    const double dmin = fmin(fmin(len[0], len[1]), len[2]);
+    bool cull = dmin > 1e-3 * scale && det != 0.0 && isfinite(det);
+    float4 e[3];
+    const double m = 1e-3 + 64.0 * 0x1p-23 * scale / dmin;
+    for (int i = 0; i < 3; ++i) {
+      const double nl = sqrt(n[i][0] * n[i][0] + n[i][1] * n[i][1] + n[i][2] * n[i][2]);
+      cull = cull && nl > 0.0;
+      const double k = det > 0.0 ? 1.0 / nl : -1.0 / nl;  // inner side: the opposite corner's
+      e[i] = make_float4((float)(n[i][0] * k), (float)(n[i][1] * k), (float)(n[i][2] * k), (float)m);
+    }
+    for (int i = 0; i < 3; ++i) cone[3 * f + i] = cull ? e[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  }
+}
+
+// bounce-0 closest hit: this lane's candidate faces only, ascending (LazyHit's order rule)
+__device__ __forceinline__ rt::Hit query_cone(const float4* tab, const float4* cone, int nf, const rt::Shear& s,
+                                              float3 d) {
+  uint64_t cand = 0;
+#pragma unroll 4
+  for (int f = 0; f < nf; ++f) {
+    const float4 e0 = cone[3 * f], e1 = cone[3 * f + 1], e2 = cone[3 * f + 2];
+    const float d0 = fmaf(e0.z, d.z, fmaf(e0.y, d.y, e0.x * d.x));
+    const float d1 = fmaf(e1.z, d.z, fmaf(e1.y, d.y, e1.x * d.x));
+    const float d2 = fmaf(e2.z, d.z, fmaf(e2.y, d.y, e2.x * d.x));
+    const bool in = fminf(fminf(d0, d1), d2) >= -e0.w;
+    cand |= (uint64_t)in << f;
+  }
+  rt::LazyHit h;
+  rt::lazy_init(h);
+  const int off = s.kcase * 3;
+  while (cand) {
+    const int f = __builtin_ctzll(cand);
+    cand &= cand - 1;
+    const float4 q0 = tab[f * 18 + off + 0];
+    const float4 q1 = tab[f * 18 + off + 1];
+    const float c2 = tab[f * 18 + off + 2].x;
+    float T, det;
+    if (rt::tri_test(s, q0, q1, c2, T, det)) rt::lazy_consider(h, T, det, f);
+  }
+  return rt::lazy_finish(h);
+}
+
 template <bool USE_BVH>
 __device__ __forceinline__ void stage_env(const TraceArgs& a, float4* lds_tab) {
   if constexpr (!USE_BVH) {  // stage the environment table (coalesced float4 copy)
@@ -113,80 +205,91 @@ __device__ __forceinline__ void stage_env(const TraceArgs& a, float4* lds_tab) {
   }
 }
 
-// rt_trace_cir's tail (tracer.py:87-117), run by the last block of the trace kernel to finish.
-// A block that finds received rows computes their (bin, amplitude) itself, in chunk-local slots,
-// and releases them (an agent-scope release writes its XCD's L2 back: rare, ~1 block per 1M-ray
-// K2 burst) before taking its ticket.  The last ticket holder acquires, scans the chunk counts
-// into the ordered index list (tracer.py:87, ray order), compacts the slots in that order, zeroes
-// the counts it used and accumulates the impulse response in path order (rt_cir.h).  This
-// replaces a second launch (its ~5 us gap and ~18 us of latency-bound work): K2 step 153 -> 142 us
-// (tools/k2_fused_variants.py).  Measured pieces: tickets + release + acquire ~2 us, the tail's
-// scan/compaction/impulse response ~3 us; the per-path double arithmetic after the bounce loop
-// costs the trace loop ~2 us in spilled registers, but in the tail (one thread per path, serial
-// on the critical path) the step took 149-159 us depending on where the compiler spilled.
-template <int B>
-__device__ __forceinline__ void fused_tail(const TraceArgs& a, bool published) {
-  __shared__ int s_last;
-  __shared__ int64_t wsum[4];
-  if (published) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  __syncthreads();
-  if (threadIdx.x == 0) s_last = atomicAdd(a.fz.done, 1u) == gridDim.x - 1;
-  __syncthreads();
-  if (!s_last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int64_t nch = (a.n + 255) / 256;
-  const int64_t q = (nch + 255) / 256;  // contiguous chunks per thread
-  const int64_t c0 = (int64_t)t * q < nch ? (int64_t)t * q : nch;
-  const int64_t c1 = c0 + q < nch ? c0 + q : nch;
-  int64_t own = 0;
-#pragma unroll 8
-  for (int64_t c = c0; c < c1; ++c) own += a.fz.counts[c];
-  // exclusive scan of the per-thread sums over the block
-  int64_t incl = own;
-  for (int o = 1; o < 64; o <<= 1) {
-    const int64_t v = __shfl_up(incl, o, 64);
-    if (lane >= o) incl += v;
-  }
-  if (lane == 63) wsum[w] = incl;
-  __syncthreads();
-  int64_t k = incl - own;
-  for (int j = 0; j < w; ++j) k += wsum[j];
-  const int64_t total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-  if (own > 0) {
-    for (int64_t c = c0; c < c1; ++c) {
-      const int32_t v = a.fz.counts[c];
-      if (v == 0) continue;
-      for (int32_t r = 0; r < v; ++r) {
-        const int64_t slot = c * 256 + r;
-        const int64_t row = c * 256 + a.fz.lrow[slot];
-        a.fz.index[k + r] = row;
-        a.fz.cbin[k + r] = a.fz.pbin[slot];
-        a.fz.camp[k + r] = a.fz.pamp[slot];
+// rt_trace_cir on brute-force meshes (tracer.py:87-117): the trace kernel lists each wave's
+// received rows as it goes -- bits of the chunk's 256-bit row mask, the chunk's count and its
+// group-of-64-chunks count (lane 0, three atomics, rare).  No block barriers on this path (a
+// barrier per chunk held every early wave's registers until its block's slowest wave was done).
+// Then ONE small kernel, k_trace_cir_tail, compacts the rows in ray order (chunk order, then bit
+// order), computes each path's (bin, amplitude) and accumulates the impulse response in path
+// order.  Measured alternatives (tools/k2_fused_variants.py, K2 room, 1M rays):
+//   * finishing in the trace kernel's last block (an atomic ticket per block, the last one does
+//     the tail) cost the step 11 us in tickets alone -- every block waits on its ticket's round
+//     trip before it frees its slot -- plus 12 us of tail; a ticket per wave doubled the step;
+//   * the per-path double arithmetic in the trace kernel (by the lane that found the row) runs
+//     inside a 72-VGPR budget, spilled, and kept that wave -- often one of the last -- busy for
+//     ~10 us after its rays were done.
+// One block of 1024: wave 0 scans the group counts (two levels, only groups with rows are
+// expanded), writes the ordered index list and zeroes the counts and masks it used, while the other
+// waves zero the impulse response; then every thread computes received paths' (bin, amplitude)
+// (rt_cir.h, in registers: no spills here), and wave 0 accumulates them in path order.
+__global__ __launch_bounds__(1024) void k_trace_cir_tail(rt::TraceCirFused fz, int64_t n, const float* received,
+                                                         int P) {
+  __shared__ int64_t s_total;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (wave > 0) {
+    if (fz.ir)
+      for (int64_t b = threadIdx.x - 64; b < fz.k.n_bins; b += blockDim.x - 64) fz.ir[b] = 0.0;
+  } else {
+    const int64_t nch = (n + 255) / 256;
+    const int64_t ngrp = (nch + 63) / 64;
+    int64_t base = 0;  // rows before the current row of groups (wave-uniform)
+    for (int64_t g0 = 0; g0 < ngrp; g0 += 64) {
+      const int64_t g = g0 + lane;
+      const int32_t gc = g < ngrp ? fz.gcounts[g] : 0;
+      int64_t gincl = gc;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int64_t v = __shfl_up(gincl, o, 64);
+        if (lane >= o) gincl += v;
       }
-      a.fz.counts[c] = 0;
-      k += v;
+      for (uint64_t gm = __ballot(gc > 0); gm; gm &= gm - 1) {  // groups with rows, in order
+        const int gl = __builtin_ctzll(gm);
+        const int64_t gg = g0 + gl;
+        const int64_t gbase = base + __shfl(gincl, gl, 64) - __shfl((int64_t)gc, gl, 64);
+        const int64_t c = gg * 64 + lane;
+        const int32_t cc = c < nch ? fz.counts[c] : 0;
+        int64_t cincl = cc;
+        for (int o = 1; o < 64; o <<= 1) {
+          const int64_t v = __shfl_up(cincl, o, 64);
+          if (lane >= o) cincl += v;
+        }
+        if (cc > 0) {
+          int64_t k = gbase + cincl - cc;
+          for (int w = 0; w < 4; ++w) {
+            for (uint64_t bits = fz.masks[c * 4 + w]; bits; bits &= bits - 1)
+              fz.index[k++] = c * 256 + w * 64 + __builtin_ctzll(bits);
+            fz.masks[c * 4 + w] = 0;  // ready for the next call on this workspace
+          }
+          fz.counts[c] = 0;
+        }
+        if (lane == 0) fz.gcounts[gg] = 0;
+      }
+      base += __shfl(gincl, 63, 64);
+    }
+    if (lane == 0) {
+      *fz.count = base;
+      s_total = base;
     }
   }
-  if (t == 0) {
-    *a.fz.count = total;
-    *a.fz.done = 0u;  // ready for the next call on this workspace
-  }
-  if (!a.fz.ir) return;
   __syncthreads();
-  rt::ir_accumulate_block(a.fz.cbin, a.fz.camp, total, a.fz.k.n_bins, a.fz.ir);
+  const int64_t total = s_total;
+  for (int64_t k = threadIdx.x; k < total; k += blockDim.x)
+    rt::cir_row(received + fz.index[k] * P * 3, P, fz.k, fz.cbin + k, fz.camp + k);
+  __syncthreads();
+  if (wave == 0 && fz.ir) rt::ir_accumulate_wave(fz.cbin, fz.camp, total, fz.k.n_bins, fz.ir, false);
 }
 
 template <int B, bool USE_BVH>
 __device__ __forceinline__ void trace_body(const TraceArgs& a) {
   constexpr int P = B + 1;
   extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
+  float4* cone = lds_tab + (size_t)a.env_nf * 18;  // bounce-0 edge normals after the face table
+  const bool use_cone = RT_CONE && !USE_BVH && a.env_nf <= kConeMaxFaces;
+  if (use_cone) stage_cones(a, cone);  // made visible by stage_env's barrier
   stage_env<USE_BVH>(a, lds_tab);
 
   const float qnan = __builtin_nanf("");
-  bool published = false;  // this block listed received rows (rt_trace_cir)
-  // block-uniform loop over 256-row chunks (the same rows per thread as a grid-stride loop), so the
-  // block can list its chunk's received rows for rt_trace_cir
+  // block-uniform loop over 256-row chunks (the same rows per thread as a grid-stride loop), so a
+  // wave can list its part of a chunk's received rows for rt_trace_cir
   for (int64_t chunk = blockIdx.x; chunk * 256 < a.n; chunk += gridDim.x) {
     const int64_t irow = chunk * 256 + threadIdx.x;
     bool got = false;
@@ -208,7 +311,8 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
       int kind = 0, face = -1;
       if (alive) {
         const rt::Shear s = rt::make_shear(pos, dir);
-        const rt::Hit he = env_hit_query<USE_BVH>(a, lds_tab, s, pos, dir);
+        const rt::Hit he = (b == 0 && use_cone) ? query_cone(lds_tab, cone, a.env_nf, s, dir)
+                                                : env_hit_query<USE_BVH>(a, lds_tab, s, pos, dir);
         const bool env_hit = he.face >= 0;
         rt::Hit hr;
         rt::hit_init(hr);
@@ -263,40 +367,14 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
     got = last_rx >= 0;
     }
     if (!USE_BVH && a.fused) {  // row order == chunk order here (no direction sort)
-      // list this chunk's received rows (row within the chunk, in row order) and count them; the
-      // counts stay zero (the workspace invariant) for chunks without one
-      __shared__ int32_t wcnt[4];
       const uint64_t m = __ballot(got);
-      if ((threadIdx.x & 63) == 0) wcnt[threadIdx.x >> 6] = (int32_t)__popcll(m);
-      __syncthreads();
-      const int32_t tot = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
-      if (tot > 0) {  // block-uniform
-        if (got) {  // the row's slot in its chunk
-          const int w = threadIdx.x >> 6;
-          int32_t r = (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-          for (int q = 0; q < w; ++q) r += wcnt[q];
-          a.fz.lrow[chunk * 256 + r] = (uint8_t)threadIdx.x;
-        }
-        if (threadIdx.x == 0) a.fz.counts[chunk] = tot;
-        published = true;
-      }
-      __syncthreads();
-    }
-  }
-  if constexpr (!USE_BVH) {
-    if (a.fused) {
-      if (published) {  // block-uniform: each listed path's (bin, amplitude) in its chunk slot,
-                        // after the bounce loop so its double arithmetic does not share registers
-        for (int64_t chunk = blockIdx.x; chunk * 256 < a.n; chunk += gridDim.x) {
-          const int32_t c = a.fz.counts[chunk];  // this block's own (zero unless listed here)
-          if (threadIdx.x < c) {
-            const int64_t slot = chunk * 256 + threadIdx.x;
-            rt::cir_row(a.received + (chunk * 256 + a.fz.lrow[slot]) * (B + 1) * 3, B + 1, a.fz.k,
-                        a.fz.pbin + slot, a.fz.pamp + slot);
-          }
+      if (m) {  // wave-uniform: list this wave's received rows (bits of the chunk's row mask)
+        if ((threadIdx.x & 63) == 0) {
+          atomicAdd(a.fz.counts + chunk, (int32_t)__popcll(m));
+          atomicAdd(a.fz.gcounts + (chunk >> 6), (int32_t)__popcll(m));
+          atomicOr((unsigned long long*)a.fz.masks + chunk * 4 + (threadIdx.x >> 6), (unsigned long long)m);
         }
       }
-      fused_tail<B>(a, published);
     }
   }
 }
@@ -506,7 +584,8 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
   a.fused = fused && !bvh && B <= 8;  // the register-resident brute-force kernels
   if (a.fused) a.fz = *fused;
   if (fused_done) *fused_done = a.fused;
-  const size_t lds = bvh ? 0 : (size_t)env->nf * 18 * sizeof(float4);
+  // brute force: the face table, then the bounce-0 cone normals (3 float4 per face, <= 64 faces)
+  const size_t lds = bvh ? 0 : (size_t)env->nf * (env->nf <= kConeMaxFaces ? 21 : 18) * sizeof(float4);
   int dev_cu = 256;
   const int64_t want = (n + 255) / 256;
   const int64_t cap = (int64_t)dev_cu * 16;
@@ -554,6 +633,7 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
       break;
   }
 #undef RT_LAUNCH
+  if (a.fused) hipLaunchKernelGGL(k_trace_cir_tail, dim3(1), dim3(1024), 0, stream, a.fz, n, received, B + 1);
   RT_HIP(hipGetLastError());
   if (sort_ws) RT_HIP(hipFreeAsync(sort_ws, stream));
   return 0;
