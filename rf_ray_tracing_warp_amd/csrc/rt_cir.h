@@ -132,12 +132,15 @@ __device__ __forceinline__ void ir_accumulate_wave(const int32_t* pbin, const do
     const int32_t mb = (bb >= 0 && bb < n_bins) ? bb : -1;
     const double am = k < cnt ? pamp[k] : 0.0;
     bool leader = mb >= 0;
-    for (int j = 0; j < 64; ++j) {  // wave-uniform trip counts: every lane takes part in the shuffles
+    // wave-uniform trip counts (every lane takes part in the shuffles), only over this batch's
+    // paths: each shuffle is a dependent LDS round trip, 2 x 64 of them took ~3 us for one path
+    const int m = cnt - b0 < 64 ? (int)(cnt - b0) : 64;
+    for (int j = 0; j < m; ++j) {
       const int32_t bj = __shfl(mb, j, 64);
       if (j < lane && bj == mb) leader = false;
     }
     double v = (leader && b0 > 0) ? ir[mb] : 0.0;  // the first 64 paths add to the zeros just written
-    for (int j = 0; j < 64; ++j) {
+    for (int j = 0; j < m; ++j) {
       const int32_t bj = __shfl(mb, j, 64);
       const double aj = __shfl(am, j, 64);
       if (j >= lane && bj == mb) v += aj;

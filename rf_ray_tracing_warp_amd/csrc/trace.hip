@@ -119,7 +119,7 @@ __device__ __forceinline__ rt::Hit env_hit_query(const TraceArgs& a, const float
 // Every ray of a burst starts at the TX, so the directions that can hit face f at bounce 0 form
 // the cone spanned by the TX and the face's corners: d must lie on the inner side of the three
 // planes through the TX and each edge -- the signs the watertight test's U, V, W compute, up to
-// rounding.  Each block stages, per face, the three unit inner edge normals e_i (double, from the
+// rounding.  Each block stages, per face, the three unit inner edge normals e_i (from the
 // identity-permuted corners) and a margin m; a lane keeps face f as a bounce-0 candidate when
 // e_i . d >= -m for all three.  m = 1e-3 rad plus 64 ulp of the scene's coordinate scale over the
 // face's nearest corner distance -- far wider than the watertight test's rounding of U, V, W, so
@@ -136,33 +136,33 @@ __device__ __forceinline__ void stage_cones(const TraceArgs& a, float4* cone) {
   for (int f = threadIdx.x; f < a.env_nf; f += blockDim.x) {
     const float4 q0 = a.env_perm[f * 18 + 12], q1 = a.env_perm[f * 18 + 13];  // case 4: kx,ky,kz = x,y,z
     const float c2 = a.env_perm[f * 18 + 14].x;
-    const double o[3] = {a.tx[0], a.tx[1], a.tx[2]};
-    const double v[3][3] = {{q0.x - o[0], q0.y - o[1], q0.z - o[2]},
-                            {q0.w - o[0], q1.x - o[1], q1.y - o[2]},
-                            {q1.z - o[0], q1.w - o[1], c2 - o[2]}};
-    double scale = fmax(fmax(fabs(o[0]), fabs(o[1])), fabs(o[2]));
-    scale = fmax(scale, fmax(fmax(fabs((double)q0.x), fabs((double)q0.y)), fabs((double)q0.z)));
-    scale = fmax(scale, fmax(fmax(fabs((double)q0.w), fabs((double)q1.x)), fabs((double)q1.y)));
-    scale = fmax(scale, fmax(fmax(fabs((double)q1.z), fabs((double)q1.w)), fabs((double)c2)));
-    double len[3], n[3][3];
+    const float o[3] = {a.tx[0], a.tx[1], a.tx[2]};
+    const float v[3][3] = {{q0.x - o[0], q0.y - o[1], q0.z - o[2]},
+                           {q0.w - o[0], q1.x - o[1], q1.y - o[2]},
+                           {q1.z - o[0], q1.w - o[1], c2 - o[2]}};
+    float scale = fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fabsf(o[2]));
+    scale = fmaxf(scale, fmaxf(fmaxf(fabsf(q0.x), fabsf(q0.y)), fabsf(q0.z)));
+    scale = fmaxf(scale, fmaxf(fmaxf(fabsf(q0.w), fabsf(q1.x)), fabsf(q1.y)));
+    scale = fmaxf(scale, fmaxf(fmaxf(fabsf(q1.z), fabsf(q1.w)), fabsf(c2)));
+    float len[3], n[3][3];
     for (int i = 0; i < 3; ++i) {
-      const double* p = v[i];
-      const double* q = v[(i + 1) % 3];
+      const float* p = v[i];
+      const float* q = v[(i + 1) % 3];
       n[i][0] = p[1] * q[2] - p[2] * q[1];
       n[i][1] = p[2] * q[0] - p[0] * q[2];
       n[i][2] = p[0] * q[1] - p[1] * q[0];
-      len[i] = sqrt(p[0] * p[0] + p[1] * p[1] + p[2] * p[2]);
+      len[i] = sqrtf(p[0] * p[0] + p[1] * p[1] + p[2] * p[2]);
     }
-    const double det = n[0][0] * v[2][0] + n[0][1] * v[2][1] + n[0][2] * v[2][2];
-    const double dmin = fmin(fmin(len[0], len[1]), len[2]);
-    bool cull = dmin > 1e-3 * scale && det != 0.0 && isfinite(det);
+    const float det = n[0][0] * v[2][0] + n[0][1] * v[2][1] + n[0][2] * v[2][2];
+    const float dmin = fminf(fminf(len[0], len[1]), len[2]);
+    bool cull = dmin > 1e-3f * scale && det != 0.0f && isfinite(det);
     float4 e[3];
-    const double m = 1e-3 + 64.0 * 0x1p-23 * scale / dmin;
+    const float m = 1e-3f + 64.0f * 0x1p-23f * scale / dmin;  // f32 rounding here is ~1e-6 rad
     for (int i = 0; i < 3; ++i) {
-      const double nl = sqrt(n[i][0] * n[i][0] + n[i][1] * n[i][1] + n[i][2] * n[i][2]);
-      cull = cull && nl > 0.0;
-      const double k = det > 0.0 ? 1.0 / nl : -1.0 / nl;  // inner side: the opposite corner's
-      e[i] = make_float4((float)(n[i][0] * k), (float)(n[i][1] * k), (float)(n[i][2] * k), (float)m);
+      const float nl = sqrtf(n[i][0] * n[i][0] + n[i][1] * n[i][1] + n[i][2] * n[i][2]);
+      cull = cull && nl > 0.0f && isfinite(nl);
+      const float k = det > 0.0f ? 1.0f / nl : -1.0f / nl;  // inner side: the opposite corner's
+      e[i] = make_float4(n[i][0] * k, n[i][1] * k, n[i][2] * k, m);
     }
     for (int i = 0; i < 3; ++i) cone[3 * f + i] = cull ? e[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   }
@@ -218,13 +218,19 @@ __device__ __forceinline__ void stage_env(const TraceArgs& a, float4* lds_tab) {
 //   * the per-path double arithmetic in the trace kernel (by the lane that found the row) runs
 //     inside a 72-VGPR budget, spilled, and kept that wave -- often one of the last -- busy for
 //     ~10 us after its rays were done.
-// One block of 1024: wave 0 scans the group counts (two levels, only groups with rows are
-// expanded), writes the ordered index list and zeroes the counts and masks it used, while the other
-// waves zero the impulse response; then every thread computes received paths' (bin, amplitude)
-// (rt_cir.h, in registers: no spills here), and wave 0 accumulates them in path order.
-__global__ __launch_bounds__(1024) void k_trace_cir_tail(rt::TraceCirFused fz, int64_t n, const float* received,
+// One block of 512.  Wave 0 scans the group counts (two levels: only groups with rows are
+// expanded into their chunks' counts and row masks), writes the ordered index list, zeroes the
+// counts and masks it used and -- while a row of 64 groups (1M rays) holds at most 256 received
+// paths -- computes each path's (bin, amplitude) on the lane that found it; the other waves zero
+// the impulse response meanwhile.  Denser bursts leave the per-path arithmetic to all 512
+// threads after the barrier.  Then wave 0 accumulates in path order.  K2 (one received path per
+// burst), rocprofv3: an empty kernel in this place takes 5.1 us, the scan and compaction add 0.2 us,
+// the path's double arithmetic 2.8 us, the accumulation (before its shuffle loops were cut to the
+// batch's paths) 4.5 us.
+__global__ __launch_bounds__(512) void k_trace_cir_tail(rt::TraceCirFused fz, int64_t n, const float* received,
                                                          int P) {
   __shared__ int64_t s_total;
+  __shared__ int s_parallel;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (wave > 0) {
     if (fz.ir)
@@ -233,6 +239,7 @@ __global__ __launch_bounds__(1024) void k_trace_cir_tail(rt::TraceCirFused fz, i
     const int64_t nch = (n + 255) / 256;
     const int64_t ngrp = (nch + 63) / 64;
     int64_t base = 0;  // rows before the current row of groups (wave-uniform)
+    bool parallel = false;
     for (int64_t g0 = 0; g0 < ngrp; g0 += 64) {
       const int64_t g = g0 + lane;
       const int32_t gc = g < ngrp ? fz.gcounts[g] : 0;
@@ -241,6 +248,8 @@ __global__ __launch_bounds__(1024) void k_trace_cir_tail(rt::TraceCirFused fz, i
         const int64_t v = __shfl_up(gincl, o, 64);
         if (lane >= o) gincl += v;
       }
+      const bool inline_cir = __shfl(gincl, 63, 64) <= 256;
+      parallel |= !inline_cir;
       for (uint64_t gm = __ballot(gc > 0); gm; gm &= gm - 1) {  // groups with rows, in order
         const int gl = __builtin_ctzll(gm);
         const int64_t gg = g0 + gl;
@@ -254,10 +263,18 @@ __global__ __launch_bounds__(1024) void k_trace_cir_tail(rt::TraceCirFused fz, i
         }
         if (cc > 0) {
           int64_t k = gbase + cincl - cc;
+          uint64_t mw[4];
+#pragma unroll
+          for (int w = 0; w < 4; ++w) mw[w] = fz.masks[c * 4 + w];  // four independent loads
+#pragma unroll
           for (int w = 0; w < 4; ++w) {
-            for (uint64_t bits = fz.masks[c * 4 + w]; bits; bits &= bits - 1)
-              fz.index[k++] = c * 256 + w * 64 + __builtin_ctzll(bits);
-            fz.masks[c * 4 + w] = 0;  // ready for the next call on this workspace
+            for (uint64_t bits = mw[w]; bits; bits &= bits - 1) {
+              const int64_t row = c * 256 + w * 64 + __builtin_ctzll(bits);
+              fz.index[k] = row;
+              if (inline_cir) rt::cir_row(received + row * P * 3, P, fz.k, fz.cbin + k, fz.camp + k);
+              ++k;
+            }
+            if (mw[w]) fz.masks[c * 4 + w] = 0;  // ready for the next call on this workspace
           }
           fz.counts[c] = 0;
         }
@@ -268,13 +285,16 @@ __global__ __launch_bounds__(1024) void k_trace_cir_tail(rt::TraceCirFused fz, i
     if (lane == 0) {
       *fz.count = base;
       s_total = base;
+      s_parallel = parallel;
     }
   }
   __syncthreads();
   const int64_t total = s_total;
-  for (int64_t k = threadIdx.x; k < total; k += blockDim.x)
-    rt::cir_row(received + fz.index[k] * P * 3, P, fz.k, fz.cbin + k, fz.camp + k);
-  __syncthreads();
+  if (s_parallel) {  // dense bursts: every path's arithmetic over the whole block (same values)
+    for (int64_t k = threadIdx.x; k < total; k += blockDim.x)
+      rt::cir_row(received + fz.index[k] * P * 3, P, fz.k, fz.cbin + k, fz.camp + k);
+    __syncthreads();
+  }
   if (wave == 0 && fz.ir) rt::ir_accumulate_wave(fz.cbin, fz.camp, total, fz.k.n_bins, fz.ir, false);
 }
 
@@ -633,7 +653,7 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
       break;
   }
 #undef RT_LAUNCH
-  if (a.fused) hipLaunchKernelGGL(k_trace_cir_tail, dim3(1), dim3(1024), 0, stream, a.fz, n, received, B + 1);
+  if (a.fused) hipLaunchKernelGGL(k_trace_cir_tail, dim3(1), dim3(512), 0, stream, a.fz, n, received, B + 1);
   RT_HIP(hipGetLastError());
   if (sort_ws) RT_HIP(hipFreeAsync(sort_ws, stream));
   return 0;
