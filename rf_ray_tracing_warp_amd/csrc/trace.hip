@@ -95,6 +95,40 @@ __device__ __forceinline__ bool rx_maybe(const TraceArgs& a, float3 o, float3 d,
   return t_enter <= t_limit * 1.0001f + 1e-4f;
 }
 
+// Row stores of the register-resident kernels.  RT_NT_ROWS: non-temporal (streaming) stores --
+// the rows are written once and not read back by this step, so they need not sit dirty in L2
+// until the end-of-kernel writeback.
+#ifndef RT_NT_ROWS
+#define RT_NT_ROWS 1
+#endif
+template <int P>
+__device__ __forceinline__ void store_row_fixed(float* dst, const float (*pts)[3]) {
+  if constexpr ((P * 3) % 4 == 0) {  // 16-B aligned rows (P = 4, 8): 16-byte stores
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    f4v* d4 = reinterpret_cast<f4v*>(dst);
+#pragma unroll
+    for (int j = 0; j < P * 3 / 4; ++j) {
+      const int i = 4 * j;
+      const f4v v = {pts[i / 3][i % 3], pts[(i + 1) / 3][(i + 1) % 3], pts[(i + 2) / 3][(i + 2) % 3],
+                     pts[(i + 3) / 3][(i + 3) % 3]};
+#if RT_NT_ROWS
+      __builtin_nontemporal_store(v, d4 + j);
+#else
+      d4[j] = v;
+#endif
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < P * 3; ++i) {
+#if RT_NT_ROWS
+      __builtin_nontemporal_store(pts[i / 3][i % 3], dst + i);
+#else
+      dst[i] = pts[i / 3][i % 3];
+#endif
+    }
+  }
+}
+
 __device__ __forceinline__ void store_row(float* dst, const float (*pts)[3], int P) {
   // rows are 12*P bytes; use 16-byte stores whenever the row start allows it
   for (int i = 0; i < P; ++i) {
@@ -371,7 +405,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
       if (a.hit_kind) a.hit_kind[row * B + b] = kind;
       if (a.hit_face) a.hit_face[row * B + b] = face;
     }
-    if (a.traced) store_row(a.traced + row * (P * 3), path, P);
+    if (a.traced) store_row_fixed<P>(a.traced + row * (P * 3), path);
     if (a.received) {
       float rec[P][3];
 #pragma unroll
@@ -381,9 +415,15 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
         rec[i][1] = keep ? path[i][1] : qnan;
         rec[i][2] = keep ? path[i][2] : qnan;
       }
-      store_row(a.received + row * (P * 3), rec, P);
+      store_row_fixed<P>(a.received + row * (P * 3), rec);
     }
-    if (a.mask) a.mask[row] = last_rx >= 0 ? 1u : 0u;
+    if (a.mask) {
+#if RT_NT_ROWS
+      __builtin_nontemporal_store(last_rx >= 0 ? 1u : 0u, a.mask + row);
+#else
+      a.mask[row] = last_rx >= 0 ? 1u : 0u;
+#endif
+    }
     got = last_rx >= 0;
     }
     if (!USE_BVH && a.fused) {  // row order == chunk order here (no direction sort)
