@@ -1753,8 +1753,23 @@ size_t rord_row_bytes(int64_t n) { return ((size_t)n * 4 + 255) / 256 * 256; }
 // stage's ~0.7M records on 51 bits take 238 us merged vs ~205 us by Onesweep; the owner stage's
 // ~0.2M (31 bits) are faster merged (owner stage 0.23 vs 0.29 ms) and K5's ~0.47M (36 bits) by
 // Onesweep (0.46 vs 0.50 ms).  So: Onesweep from 300k items, rocprim's default below.
-using OnesweepOnly =
-    rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, rocprim::default_config, 0>;
+#ifndef RT_SORT_RADIX_BITS
+#define RT_SORT_RADIX_BITS 10  // 0: rocprim's gfx950 default, 8 bits per pass (tools/gpu_sortvar.sh: 10 bits, 1024-thread blocks, K5 rank of 8 1.58 -> 1.53 ms)
+#endif
+#if RT_SORT_RADIX_BITS
+#ifndef RT_SORT_HIST_BLOCK
+#define RT_SORT_HIST_BLOCK 1024
+#endif
+#ifndef RT_SORT_BLOCK
+#define RT_SORT_BLOCK 1024
+#endif
+using OnesweepCfg =
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<RT_SORT_HIST_BLOCK, 8>, rocprim::kernel_config<RT_SORT_BLOCK, 8>,
+                                        RT_SORT_RADIX_BITS, rocprim::block_radix_rank_algorithm::match>;
+#else
+using OnesweepCfg = rocprim::default_config;
+#endif
+using OnesweepOnly = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, OnesweepCfg, 0>;
 constexpr int64_t kOnesweepMinItems = 300000;
 template <typename V>
 hipError_t sort_records(void* tmp, size_t& bytes, const uint64_t* kin, uint64_t* kout, const V* vin, V* vout,
@@ -1865,8 +1880,6 @@ __global__ __launch_bounds__(256) void k_count_replay(const uint64_t* keys, cons
   if ((threadIdx.x & 63) == 0 && acc) atomicAdd(out, acc);
 }
 
-// replay query order: receiver first and the environment query culled at its t (default), or
-// the reference's order, environment then receiver (RFRT_COV_RXFIRST=0, for A/B checks)
 // BVH trajectories of at most this many rays run four lanes per ray (RFRT_TRAJ_SPLIT_MAX, 0 = never)
 int64_t traj_split_max_rays() {
   static const int64_t v = [] {
@@ -1876,6 +1889,8 @@ int64_t traj_split_max_rays() {
   return v;
 }
 
+// replay query order on BVH scenes: receiver first and the traversal culled at its t (default), or
+// the reference's order, environment then receiver (RFRT_COV_RXFIRST=0, for A/B checks)
 bool replay_rx_first() {
   static const bool v = [] {
     const char* e = getenv("RFRT_COV_RXFIRST");
@@ -2069,7 +2084,9 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
                                                 (int)nlist, 0, 16, s));
       prof_mark(c, 4, s);
       // BVH scenes: receiver first, the traversal culled at its t (K5 replay 3.47 -> 2.7 ms); the
-      // LDS brute force tests every face anyway (a plane-culled variant measured 5% slower on K3)
+      // LDS brute force tests every face anyway (a plane-culled variant measured 5% slower on K3,
+      // a receiver-first one skipping faces beyond the receiver's t 5% slower too: 2.50 vs 2.63 ms,
+      // profiles/r2x_cov_rxfirst_lds_ab.jsonl)
       if (bvh && replay_rx_first())
         hipLaunchKernelGGL((k_replay<true, true>), dim3(grid_l), dim3(256), 0, s, p, c->keys, c->trx, c->list, nlist,
                            v_out, c->okeys, c->oamps);

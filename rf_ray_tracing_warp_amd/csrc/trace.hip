@@ -439,6 +439,167 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
   }
 }
 
+// ------------------------------------------------------------------ active-ray compaction
+// Brute-force meshes, bounces >= 1.  A wave runs the 44-face loop as long as any of its lanes needs
+// it, and lanes whose ray has escaped (kernel.py:97-98; room.stl K2: 26% of rays at bounce 1, 30%
+// at bounce 2) idle through it.  So each block queues its live rays' (position, direction) in LDS
+// (ballot + mbcnt + one LDS atomic per wave), the first ceil(n_live / 64) waves of the block run
+// the environment query over the queue, and each ray picks its (t, face) back up.  Two block
+// barriers per bounce; waves left without queue entries skip the loop and free their SIMD's issue
+// slots.  Only which lane computes a query changes: same query, same inputs, same bits.
+// Measured (tools/gpu_k2ab.sh, K2, 1M rays): bit-identical, but the trace kernel takes 120.1 us
+// against 115.4 us without it -- the barriers and the queue's LDS (25 KB per block: 6 blocks per
+// CU instead of 7) cost more than the 25% of bounce-1/2 waves it retires.  Off by default
+// (RT_COMPACT=1 builds it for A/B).
+#ifndef RT_COMPACT
+#define RT_COMPACT 0  // measured slower on K2: trace kernel 120.1 vs 115.4 us (profiles/r2za_k2_compaction_ab.jsonl)
+#endif
+constexpr int kQueueFloats = 6 * 256 + 2 * 2 * 256;  // (pos, dir) per slot + (t, face) per slot x 2 bounce parities
+
+template <int B>
+__device__ __forceinline__ void trace_body_compact(const TraceArgs& a) {
+  constexpr int P = B + 1;
+  extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
+  const bool use_cone = RT_CONE && a.env_nf <= kConeMaxFaces;
+  float4* cone = lds_tab + (size_t)a.env_nf * 18;
+  float* qin = reinterpret_cast<float*>(lds_tab + (size_t)a.env_nf * (use_cone ? 21 : 18));  // [6][256]
+  float* qres = qin + 6 * 256;                                                               // [2][2][256]
+  __shared__ int qcnt[2][8];
+  if (threadIdx.x < 16) (&qcnt[0][0])[threadIdx.x] = 0;
+  if (use_cone) stage_cones(a, cone);
+  stage_env<false>(a, lds_tab);  // its barrier publishes the cones and the zeroed counters
+  const int lane = threadIdx.x & 63;
+  const float qnan = __builtin_nanf("");
+  int par = 0;
+  for (int64_t chunk = blockIdx.x; chunk * 256 < a.n; chunk += gridDim.x, par ^= 1) {
+    // the other parity's counters were last read before the previous chunk's final barrier
+    if (threadIdx.x < 8) qcnt[par ^ 1][threadIdx.x] = 0;
+    const int64_t row = chunk * 256 + threadIdx.x;
+    const bool valid = row < a.n;
+    float3 dir = rt::ray_dir(a.ray_offset + (valid ? row : 0));
+    float3 pos = make_float3(a.tx[0], a.tx[1], a.tx[2]);
+    float path[P][3];
+#pragma unroll
+    for (int i = 0; i < P; ++i) path[i][0] = path[i][1] = path[i][2] = qnan;
+    path[0][0] = pos.x;
+    path[0][1] = pos.y;
+    path[0][2] = pos.z;
+    int last_rx = -1;
+    bool alive = valid;
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      int kind = 0, face = -1;
+      rt::Hit he;
+      if (b == 0) {
+        if (alive) {
+          const rt::Shear s = rt::make_shear(pos, dir);
+          he = use_cone ? query_cone(lds_tab, cone, a.env_nf, s, dir) : query_faces(lds_tab, a.env_nf, s);
+        }
+      } else {
+        const uint64_t m = __ballot(alive);
+        int base = 0;
+        if (m) {  // wave-uniform
+          if (lane == 0) base = atomicAdd(&qcnt[par][b], (int)__popcll(m));
+          base = __shfl(base, 0, 64);
+        }
+        const int slot = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if (alive) {
+          qin[0 * 256 + slot] = pos.x;
+          qin[1 * 256 + slot] = pos.y;
+          qin[2 * 256 + slot] = pos.z;
+          qin[3 * 256 + slot] = dir.x;
+          qin[4 * 256 + slot] = dir.y;
+          qin[5 * 256 + slot] = dir.z;
+        }
+        __syncthreads();
+        const int nq = qcnt[par][b];
+        float* res = qres + (b & 1) * 512;
+        if ((int)threadIdx.x < nq) {
+          const int j = threadIdx.x;
+          const float3 qp = make_float3(qin[j], qin[256 + j], qin[512 + j]);
+          const float3 qd = make_float3(qin[768 + j], qin[1024 + j], qin[1280 + j]);
+          const rt::Hit h = query_faces(lds_tab, a.env_nf, rt::make_shear(qp, qd));
+          res[j] = h.t;
+          res[256 + j] = __int_as_float(h.face);
+        }
+        __syncthreads();
+        if (alive) {
+          he.t = res[slot];
+          he.face = __float_as_int(res[256 + slot]);
+        }
+      }
+      if (alive) {
+        const bool env_hit = he.face >= 0;
+        rt::Hit hr;
+        rt::hit_init(hr);
+        if (a.rx_nf > 0 && rx_maybe(a, pos, dir, env_hit ? he.t : RT_MAX_T))
+          hr = query_faces(a.rx_perm, a.rx_nf, rt::make_shear(pos, dir));
+        const bool rx_hit = hr.face >= 0;
+        if (rx_hit && (!env_hit || he.t > hr.t)) {  // kernel.py:85
+          pos.x = fmaf(dir.x, hr.t, pos.x);
+          pos.y = fmaf(dir.y, hr.t, pos.y);
+          pos.z = fmaf(dir.z, hr.t, pos.z);
+          path[b + 1][0] = pos.x;
+          path[b + 1][1] = pos.y;
+          path[b + 1][2] = pos.z;
+          last_rx = b + 1;
+          kind = 2;
+          face = hr.face;
+        } else if (env_hit) {  // kernel.py:93-96
+          pos.x = fmaf(dir.x, he.t, pos.x);
+          pos.y = fmaf(dir.y, he.t, pos.y);
+          pos.z = fmaf(dir.z, he.t, pos.z);
+          path[b + 1][0] = pos.x;
+          path[b + 1][1] = pos.y;
+          path[b + 1][2] = pos.z;
+          const float4 n4 = a.env_nrm[he.face];
+          const float3 n = make_float3(n4.x, n4.y, n4.z);
+          const float sc = 2.0f * rt::dot3(dir, n);
+          dir.x = fmaf(-sc, n.x, dir.x);
+          dir.y = fmaf(-sc, n.y, dir.y);
+          dir.z = fmaf(-sc, n.z, dir.z);
+          kind = 1;
+          face = he.face;
+        } else {
+          alive = false;  // kernel.py:97-98: every later iteration repeats this miss
+        }
+      }
+      if (valid && a.hit_kind) a.hit_kind[row * B + b] = kind;
+      if (valid && a.hit_face) a.hit_face[row * B + b] = face;
+    }
+    if (valid) {
+      if (a.traced) store_row_fixed<P>(a.traced + row * (P * 3), path);
+      if (a.received) {
+        float rec[P][3];
+#pragma unroll
+        for (int i = 0; i < P; ++i) {
+          const bool keep = i <= last_rx;
+          rec[i][0] = keep ? path[i][0] : qnan;
+          rec[i][1] = keep ? path[i][1] : qnan;
+          rec[i][2] = keep ? path[i][2] : qnan;
+        }
+        store_row_fixed<P>(a.received + row * (P * 3), rec);
+      }
+      if (a.mask) {
+#if RT_NT_ROWS
+        __builtin_nontemporal_store(last_rx >= 0 ? 1u : 0u, a.mask + row);
+#else
+        a.mask[row] = last_rx >= 0 ? 1u : 0u;
+#endif
+      }
+    }
+    if (a.fused) {
+      const uint64_t m = __ballot(last_rx >= 0);
+      if (m && lane == 0) {  // wave-uniform: list this wave's received rows (bits of the chunk's row mask)
+        atomicAdd(a.fz.counts + chunk, (int32_t)__popcll(m));
+        atomicAdd(a.fz.gcounts + (chunk >> 6), (int32_t)__popcll(m));
+        atomicOr((unsigned long long*)a.fz.masks + chunk * 4 + (threadIdx.x >> 6), (unsigned long long)m);
+      }
+    }
+  }
+}
+
 // brute-force kernels up to B = 3 are built for 7 waves per SIMD (72 VGPRs): with the face loop
 // unrolled by two (RT_FACE_UNROLL) the K2 kernel took 73 VGPRs (6 waves); bounded, 164 vs 170 us per
 // launch, bit-identical.  Longer paths keep their registers (their path points would spill).
@@ -447,7 +608,10 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
 #endif
 template <int B, bool USE_BVH>
 __global__ __launch_bounds__(256, (B <= 3 ? RT_BF_WAVES : 1)) void k_trace_bf(TraceArgs a) {
-  trace_body<B, USE_BVH>(a);
+  if constexpr (RT_COMPACT && !USE_BVH && B >= 2)
+    trace_body_compact<B>(a);
+  else
+    trace_body<B, USE_BVH>(a);
 }
 // BVH meshes: traversal is latency-bound (dependent node fetches), so the kernel is built for
 // RT_BVH_WAVES waves per SIMD.  4 (128 VGPRs, no spills beyond the walk stack) beat 6 (80 VGPRs,
@@ -645,7 +809,10 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
   if (a.fused) a.fz = *fused;
   if (fused_done) *fused_done = a.fused;
   // brute force: the face table, then the bounce-0 cone normals (3 float4 per face, <= 64 faces)
-  const size_t lds = bvh ? 0 : (size_t)env->nf * (env->nf <= kConeMaxFaces ? 21 : 18) * sizeof(float4);
+  // and (RT_COMPACT, B >= 2) the block's ray queue
+  const size_t lds = bvh ? 0
+                         : (size_t)env->nf * (env->nf <= kConeMaxFaces ? 21 : 18) * sizeof(float4) +
+                               (RT_COMPACT && B >= 2 && B <= 8 ? kQueueFloats * sizeof(float) : 0);
   int dev_cu = 256;
   const int64_t want = (n + 255) / 256;
   const int64_t cap = (int64_t)dev_cu * 16;
@@ -680,10 +847,16 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
     else hipLaunchKernelGGL(K, dim3(grid), blk, lds, stream, __VA_ARGS__);                              \
   } while (0)
   switch (B) {
-#define RT_CASE(BB)                                         \
-  case BB:                                                  \
-    if (bvh) RT_LAUNCH((k_trace_bvh<BB>), a);               \
-    else RT_LAUNCH((k_trace_bf<BB, false>), a);             \
+#define RT_CASE(BB)                                                                                  \
+  case BB:                                                                                           \
+    if (bvh) {                                                                                       \
+      RT_LAUNCH((k_trace_bvh<BB>), a);                                                               \
+    } else {                                                                                         \
+      if (lds > 48 * 1024) /* up to 192 faces + the ray queue: above the 64 KB default */             \
+        RT_HIP(hipFuncSetAttribute((const void*)k_trace_bf<BB, false>,                              \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));           \
+      RT_LAUNCH((k_trace_bf<BB, false>), a);                                                         \
+    }                                                                                                \
     break;
     RT_CASE(1) RT_CASE(2) RT_CASE(3) RT_CASE(4) RT_CASE(5) RT_CASE(6) RT_CASE(7) RT_CASE(8)
 #undef RT_CASE
