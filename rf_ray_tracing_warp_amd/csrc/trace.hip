@@ -61,7 +61,7 @@ __device__ __forceinline__ rt::Hit query_faces(Ptr tab, int nf, const rt::Shear&
 #endif
   const int off = s.kcase * 3;
 #ifndef RT_FACE_UNROLL
-#define RT_FACE_UNROLL 2  // fewer loop branches / SALU per face (K2 170 -> 164 us with RT_BF_WAVES)
+#define RT_FACE_UNROLL 4  // fewer loop branches / SALU per face (K2 170 -> 164 us at 2 with RT_BF_WAVES; 4: 115.1 -> 114.0 us, r2zc)
 #endif
 #pragma unroll RT_FACE_UNROLL
   for (int f = 0; f < nf; ++f) {
