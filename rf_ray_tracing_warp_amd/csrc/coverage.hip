@@ -888,10 +888,11 @@ __device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab
 // replayed in a coherent order by k_replay.  (Replaying inside this kernel on brute-force scenes
 // measured 37% slower on K3, 10.1 vs 7.4 ms per map: the replay's divergent tail and registers
 // held every candidate's wave.)
-__global__ __launch_bounds__(256) void k_win(CovParams p, const uint64_t* keys, int64_t nkeys, uint8_t* first_flag,
-                                             float* trx) {
+__global__ __launch_bounds__(256) void k_win(CovParams p, const uint64_t* keys, const unsigned long long* nkeys_dev,
+                                             int64_t cap, uint8_t* first_flag, float* trx) {
   __shared__ RxLds L;
   stage_rx(L, p.r_rx);
+  const int64_t nkeys = min((int64_t)*nkeys_dev, cap);  // the candidate count, capped as k_cells stored it
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nkeys; i += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t key = keys[i];
     const int64_t cell = (int64_t)(key >> 28), r = (int64_t)((key >> 4) & 0xFFFFFF);
@@ -921,6 +922,55 @@ __global__ __launch_bounds__(256) void k_win(CovParams p, const uint64_t* keys, 
     }
     first_flag[i] = first ? 1 : 0;
     trx[i] = tr;
+  }
+}
+
+// The first wins' candidate indices in candidate order (as hipCUB's DeviceSelect::Flagged, which
+// needs the candidate count on the host), with the count read on the device: G blocks, each over
+// one contiguous tile.  k_sel_count counts a tile's flags; k_sel_scatter adds the counts of the
+// tiles before it (<= G values from L2) and writes its indices in order.  (One atomic per wave on
+// a single counter instead measured 1.4 ms on K3: 123k contended atomics.)
+__device__ __forceinline__ int64_t sel_tile(int64_t n, int G) { return ((n + G - 1) / G + 255) / 256 * 256; }
+__device__ __forceinline__ int block_sum(int v, int* s4) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) s4[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return s4[0] + s4[1] + s4[2] + s4[3];
+}
+__global__ __launch_bounds__(256) void k_sel_count(const uint8_t* flag, const unsigned long long* n_dev, int64_t cap,
+                                                   int32_t* counts) {
+  __shared__ int s4[4];
+  const int64_t n = min((int64_t)*n_dev, cap), tile = sel_tile(n, gridDim.x);
+  const int64_t lo = (int64_t)blockIdx.x * tile, hi = min(lo + tile, n);
+  int c = 0;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) c += flag[i] != 0;
+  c = block_sum(c, s4);
+  if (threadIdx.x == 0) counts[blockIdx.x] = c;
+}
+__global__ __launch_bounds__(256) void k_sel_scatter(const uint8_t* flag, const unsigned long long* n_dev, int64_t cap,
+                                                     const int32_t* counts, int64_t* list, unsigned long long* nlist) {
+  __shared__ int s4[4];
+  __shared__ int w4[4];
+  const int64_t n = min((int64_t)*n_dev, cap), tile = sel_tile(n, gridDim.x);
+  const int64_t lo = (int64_t)blockIdx.x * tile, hi = min(lo + tile, n);
+  int before = 0;
+  for (int j = threadIdx.x; j < (int)blockIdx.x; j += blockDim.x) before += counts[j];
+  int64_t base = block_sum(before, s4);
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *nlist = (unsigned long long)(base + counts[blockIdx.x]);
+  const int wave = threadIdx.x >> 6;
+  for (int64_t i0 = lo; i0 < hi; i0 += blockDim.x) {  // block-uniform
+    const int64_t i = i0 + threadIdx.x;
+    const bool f = i < hi && flag[i] != 0;
+    const uint64_t m = __ballot(f);
+    if ((threadIdx.x & 63) == 0) w4[wave] = __popcll(m);
+    __syncthreads();
+    int off = 0;
+    for (int w = 0; w < wave; ++w) off += w4[w];
+    const int step = w4[0] + w4[1] + w4[2] + w4[3];
+    if (f) list[base + off + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = i;
+    base += step;
+    __syncthreads();  // w4 is rewritten by the next step
   }
 }
 
@@ -2012,8 +2062,17 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
     RT_HIP(hipMemsetAsync(c->work, 0, 16, s));
     hipLaunchKernelGGL(k_count_segments, dim3(1024), dim3(256), 0, s, c->nseg, c->n, c->work);
   }
-  // candidates: column items (pass A) then cells (pass B); grow and retry on overflow
-  int64_t ncand = 0;
+  // candidates: column items (pass A) then cells (pass B), the exact receiver tests and the
+  // first-win list, with one host synchronize for all three counts (k_win and k_sel_* read the
+  // candidate count on the device); grow and retry on overflow
+  const KeyBits kb = key_bits(c, n_bins);
+  if (kb.total() > 62) {
+    rt::set_error("rt_coverage_run: rays x cells x bins x ranks exceed the 63-bit record key");
+    return RT_EINVAL;
+  }
+  p.bin_bits = kb.bin;
+  p.cell_bits = kb.cell;
+  int64_t ncand = 0, nrec = 0, nlist = 0;
   const unsigned grid_items = 4096;
   for (int attempt = 0;; ++attempt) {
     p.items = c->items;
@@ -2023,12 +2082,26 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
     RT_HIP(hipMemsetAsync(c->counters, 0, 32, s));
     hipLaunchKernelGGL(k_cols, dim3(grid_rays), dim3(256), 0, s, p);
     hipLaunchKernelGGL(k_cells, dim3(grid_items), dim3(256), 0, s, p);
+    const unsigned grid_c = (unsigned)std::min<int64_t>((c->cap + 255) / 256, 8192);
+    prof_mark(c, 2, s);
+    hipLaunchKernelGGL(k_win, dim3(grid_c), dim3(256), 0, s, p, c->keys, (const unsigned long long*)c->counters,
+                       c->cap, c->first_flag, c->trx);
+    prof_mark(c, 3, s);
+    {  // ordered first-win list; tile counts in c->tcos (free until the run sums)
+      const unsigned G = (unsigned)std::max<int64_t>(1, std::min<int64_t>(1024, c->cap / 2048));
+      int32_t* tiles = reinterpret_cast<int32_t*>(c->tcos);
+      hipLaunchKernelGGL(k_sel_count, dim3(G), dim3(256), 0, s, c->first_flag, (const unsigned long long*)c->counters,
+                         c->cap, tiles);
+      hipLaunchKernelGGL(k_sel_scatter, dim3(G), dim3(256), 0, s, c->first_flag,
+                         (const unsigned long long*)c->counters, c->cap, tiles, c->list, c->counters + 2);
+    }
     RT_HIP(hipGetLastError());
-    unsigned long long h[2] = {0, 0};
-    RT_HIP(hipMemcpyAsync(h, c->counters, 16, hipMemcpyDeviceToHost, s));
+    unsigned long long h[3] = {0, 0, 0};
+    RT_HIP(hipMemcpyAsync(h, c->counters, 24, hipMemcpyDeviceToHost, s));
     RT_HIP(hipStreamSynchronize(s));
     ncand = (int64_t)h[0];
     const int64_t nitems = (int64_t)h[1];
+    nlist = (int64_t)h[2];
     if (ncand <= c->cap && nitems <= c->item_cap) break;
     if (attempt >= 3) {
       rt::set_error("rt_coverage_run: candidate buffers keep overflowing");
@@ -2048,24 +2121,7 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
   }
   c->last_candidates = ncand;
   *ncand_out = ncand;
-  const KeyBits kb = key_bits(c, n_bins);
-  if (kb.total() > 62) {
-    rt::set_error("rt_coverage_run: rays x cells x bins x ranks exceed the 63-bit record key");
-    return RT_EINVAL;
-  }
-  p.bin_bits = kb.bin;
-  p.cell_bits = kb.cell;
-  int64_t nrec = 0, nlist = 0;
   if (ncand > 0) {
-    const unsigned grid_c = (unsigned)std::min<int64_t>((ncand + 255) / 256, 8192);
-    prof_mark(c, 2, s);
-    hipLaunchKernelGGL(k_win, dim3(grid_c), dim3(256), 0, s, p, c->keys, ncand, c->first_flag, c->trx);
-    prof_mark(c, 3, s);
-    size_t tb = c->tmp_bytes;
-    RT_HIP(hipcub::DeviceSelect::Flagged(c->tmp, tb, hipcub::CountingInputIterator<int64_t>(0), c->first_flag,
-                                         c->list, (int64_t*)(c->counters + 2), (int)ncand, s));
-    RT_HIP(hipMemcpyAsync(&nlist, c->counters + 2, 8, hipMemcpyDeviceToHost, s));
-    RT_HIP(hipStreamSynchronize(s));
     if (nlist > 0) {
       // coherent processing order (16-bit keys through hipCUB, workspace stream-ordered)
       const unsigned grid_l = (unsigned)std::min<int64_t>((nlist + 255) / 256, 8192);
