@@ -14,7 +14,7 @@
 //             many lanes): ball test of the few cells of the column -> keys (cell, ray, k)
 //   k_win     exact receiver test of each candidate (the cell's icosphere, 80 faces, unrolled) and
 //             the first-win check (earlier bounces of the same (cell, ray) re-tested where their
-//             segment reaches the cell's ball) -> flags, compacted in order (DeviceSelect)
+//             segment reaches the cell's ball) -> flags, compacted in order (k_sel_count + k_sel_scatter)
 //   k_replay  replay from (p_k, d_k) with the full per-cell semantics of kernel.py:57-98, then the
 //             CIR body of tracer.py:101-117 -> record (owner | cell | bin | ray key, amp), in a
 //             coherent order (direction x coarse position keys)
@@ -1848,7 +1848,7 @@ int alloc_cands(rt_coverage* c, int64_t cap) {
   RT_HIP(hipMalloc(&c->trx, cap * 4));
   RT_HIP(hipMalloc(&c->list, cap * 8));
   RT_HIP(hipMalloc(&c->runs, (cap * 3 + 64) * 4));  // run flags, their scan, run starts, long-run list
-  size_t b1 = 0, b2 = 0, b3 = 0, b4 = 0;
+  size_t b1 = 0, b2 = 0, b3 = 0;
   RT_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, b1, c->keys, c->keys_sorted, (int)cap, 0, 64));
   size_t b2m = 0;  // both sort_records paths: Onesweep at cap, the merge sort below its threshold
   RT_HIP(sort_records(nullptr, b2, c->okeys, c->okeys_sorted, c->oamps, c->oamps_sorted, cap, 64, 0));
@@ -1860,9 +1860,7 @@ int alloc_cands(rt_coverage* c, int64_t cap) {
                       64, 0));
   RT_HIP(scan_flags(nullptr, b3, c->runs, c->runs, cap, 0));
   b3 = std::max(b3, b2i);
-  RT_HIP(hipcub::DeviceSelect::Flagged(nullptr, b4, hipcub::CountingInputIterator<int64_t>(0), c->first_flag, c->list,
-                                       (int64_t*)(c->counters + 2), (int)cap));
-  c->tmp_bytes = std::max(std::max(b1, b2), std::max(b3, b4));
+  c->tmp_bytes = std::max(std::max(b1, b2), b3);
   RT_HIP(hipMalloc(&c->tmp, c->tmp_bytes));
   // replay-order sort workspace for up to cap records (one allocation per growth, not per run)
   size_t b5 = 0;
