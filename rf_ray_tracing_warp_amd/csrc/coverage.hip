@@ -704,7 +704,10 @@ __device__ __forceinline__ unsigned column_cells(const CovParams& p, uint64_t it
 
 // One pass: an item's keys are kept in the thread's LDS slots while the block reserves its
 // output range; only items with more than kCellBuf candidates run the geometry a second time.
-constexpr int kCellBuf = 16;
+#ifndef RT_CELL_BUF
+#define RT_CELL_BUF 8  // 16 KB of LDS per block instead of 32 (r2zj: candidates stage 0.640 -> 0.636 ms on K3, 0.49 -> 0.48 on K5)
+#endif
+constexpr int kCellBuf = RT_CELL_BUF;
 
 __global__ __launch_bounds__(256) void k_cells(CovParams p) {
   __shared__ uint64_t sbuf[kCellBuf][256];
@@ -903,7 +906,10 @@ __device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab
 // replayed in a coherent order by k_replay.  (Replaying inside this kernel on brute-force scenes
 // measured 37% slower on K3, 10.1 vs 7.4 ms per map: the replay's divergent tail and registers
 // held every candidate's wave.)
-__global__ __launch_bounds__(256) void k_win(CovParams p, const uint64_t* keys, const unsigned long long* nkeys_dev,
+#ifndef RT_WIN_WAVES
+#define RT_WIN_WAVES 5  // 96 VGPRs (60 B scratch) instead of 127: K3 k_win 1.03 -> 0.98 ms, K5 0.92 -> 0.875 ms (r2zj; 6 waves: 1.01 / 0.91)
+#endif
+__global__ __launch_bounds__(256, RT_WIN_WAVES) void k_win(CovParams p, const uint64_t* keys, const unsigned long long* nkeys_dev,
                                              int64_t cap, uint8_t* first_flag, float* trx) {
   __shared__ RxLds L;
   stage_rx(L, p.r_rx);
