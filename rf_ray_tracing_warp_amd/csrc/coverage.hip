@@ -412,7 +412,8 @@ __device__ __forceinline__ rt::Hit rx_query_v(const RxLds& L, const rt_grid& g, 
 // Unbounded, k_traj<true> took 98 VGPRs (4 waves) and k_replay 201 (2 waves); 5 and 3 (96 and 168
 // VGPRs, ~100 B more spills in the replay) measured K5 6.06 -> 5.59 ms and K3 6.01 -> 5.60 ms per
 // map (k_replay<true> 2.50 -> 2.08 ms, k_replay<false> 3.03 -> 2.53 ms); 4 for the replay
-// (128 VGPRs, 200 B more spills) was no better.
+// (128 VGPRs, 200 B more spills) was no better; re-measured at the round-2 end (r2zk, K3 / K5 replay
+// ms): 3 waves 2.33 / 1.96, 4 waves 2.39 / 2.20, 2 waves (no spills in the LDS replay) 2.86 / 2.30.
 #ifndef RT_COV_TRAJ_WAVES
 #define RT_COV_TRAJ_WAVES 5
 #endif
