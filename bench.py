@@ -12,12 +12,13 @@ rt_trace_cir call (one launch on room.stl's brute-force mesh):
 Rays are sharded by global ray id (rank r traces ids [r*N, (r+1)*N)): per-GPU work is fixed as
 GPUs are added ("weak").  Inputs (mesh tables) are resident in HBM before the timed region.
 
-Side legs (each its own JSON object in the line): K3 coverage (room, 256^2 cells), K4 (terrain
+Side legs (each its own JSON object in the line): K1 (almost_empty.stl, 10k rays, 1 bounce: the
+reference's CPU plumbing config), K3 coverage (room, 256^2 cells), K4 (terrain
 stand-in, 5 bounces, ray shards) and K5 coverage (terrain, 1024^2 cells), each with the roofline of
 its dominant kernel from HIP events recorded by the library (rt_coverage_profile / rt_profile), and
 CPU baselines (the oracle, -O3 -march=native, built and timed on this host).
 
-    python bench.py [--gpus N --steps K --warmup W] [--legs k2,k3,k4,k5]
+    python bench.py [--gpus N --steps K --warmup W] [--legs k1,k2,k3,k4,k5]
     torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL)
 
 Prints ONE JSON line on rank 0.
@@ -58,7 +59,7 @@ def parse():
     ap.add_argument("--profile-every", type=int, default=8,
                     help="K2: every k-th launch of the timed loop carries the start/stop events the kernel "
                          "time comes from (each such launch costs the stream a few us; 1 = all)")
-    ap.add_argument("--legs", default="k2,k3,k4,k5", help="comma list of k2 (always run), k3, k4, k5")
+    ap.add_argument("--legs", default="k1,k2,k3,k4,k5", help="comma list of k1, k2 (always run), k3, k4, k5")
     ap.add_argument("--rays", type=int, default=1_000_000, help="rays per GPU per step (K2: 1M)")
     ap.add_argument("--bounces", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -115,6 +116,17 @@ def native_oracle():
     except (OSError, subprocess.CalledProcessError):
         orc.load(os.path.join(REPO, "oracle", "_build", "librt_oracle.so"))
         return "gcc -O3 -march=x86-64-v3 -ffp-contract=off -fopenmp (prebuilt; native build failed)"
+
+
+_CPU = {}
+
+
+def cpu_setup():
+    """(host info, oracle build description), built once per process (rank 0, N=1 only)."""
+    if not _CPU:
+        _CPU["info"] = host_info()
+        _CPU["build"] = native_oracle()
+    return _CPU["info"], _CPU["build"]
 
 
 def _median_runs(fn, runs):
@@ -182,6 +194,87 @@ def cpu_baseline_k3(args, info):
                       f"loop body: {N}-ray trace with its icosphere + host CIR + np.convolve power; median of "
                       f"{len(ts)} runs ({', '.join(f'{t:.2f}' for t in ts)} s)",
             "np_convolve_power_ms_per_cell": conv * 1e3, "host": info}
+
+
+def cpu_baseline_k1(args, info, build):
+    """K1 (BASELINE.json configs[0], the reference's CPU-only plumbing case): almost_empty.stl,
+    tx (1,0,1), rx (41,0,1) r=0.1 (main.py:25-27), 10k rays, 1 bounce, 20000 bins (main.py:15-17):
+    trace + host CIR per burst.  A burst is ~1 ms of CPU work, so one timed run repeats it."""
+    from oracle import oracle as orc
+    from rf_ray_tracing_warp_amd.mesh import load_stl, sphere
+
+    env = load_stl(os.path.join(REPO, "models", "almost_empty.stl"))
+    rxm = sphere((41.0, 0.0, 1.0), 0.1, 1)
+    E, R = orc.Mesh(env.vertices, env.faces), orc.Mesh(rxm.vertices, rxm.faces)
+    n, B, reps = 10_000, 1, 50
+    out = {}
+    for label, threads in (("all", info["threads_used"]), ("1thread", 1)):
+        def run():
+            for _ in range(reps):
+                o = orc.trace(E, R, (1.0, 0.0, 1.0), B, 0, n, want_traced=True, nthreads=threads)
+                orc.cir_from_paths(orc.clean_paths(o["received"], o["mask"]), 1, n, 2.998e8, 100e9, 200e-9)
+        med, ts = _median_runs(run, args.cpu_runs)
+        out[label] = {"value": reps * n * B / med, "unit": "ray-bounces/s", "cores": threads, "kind": "port",
+                      "sample": f"{reps} K1 bursts (ray ids 0..{n - 1}, {B} bounce, almost_empty.stl): trace "
+                                f"(traced + received + row_mask) + host CIR each, oracle/rt_oracle.c, median of "
+                                f"{args.cpu_runs} runs after 1 warm-up ({', '.join(f'{t:.3f}' for t in ts)} s)",
+                      "build": build, "host": info}
+    return out
+
+
+def cpu_baseline_k4(args, terr, info, build):
+    """K4 on the host: the oracle's BVH path (its own median-split tree over the 2.09M-face terrain)
+    for a contiguous sample of the burst's ray ids, trace + host CIR; extrapolated as ray-bounces/s."""
+    from oracle import oracle as orc
+    from rf_ray_tracing_warp_amd.mesh import sphere
+
+    t0 = time.perf_counter()
+    E = orc.Mesh(terr.vertices, terr.faces)
+    t_tree = time.perf_counter() - t0
+    rxm = sphere((-10.125, 0.0, 4.8), 0.1, 1)
+    R = orc.Mesh(rxm.vertices, rxm.faces)
+    B = 5
+    out = {}
+    for label, threads, rays in (("all", info["threads_used"], 1_000_000), ("1thread", 1, 50_000)):
+        def run():
+            o = orc.trace(E, R, (10.0, 0.0, 4.5), B, 0, rays, want_traced=True, nthreads=threads)
+            orc.cir_from_paths(orc.clean_paths(o["received"], o["mask"]), 1, rays, 2.998e8, 100e9, 200e-9)
+        med, ts = _median_runs(run, args.cpu_runs)
+        out[label] = {"value": rays * B / med, "unit": "ray-bounces/s", "cores": threads, "kind": "port",
+                      "sample": f"ray ids 0..{rays - 1} of the K4 burst ({rays} of 16,777,216 rays x {B} bounces) "
+                                f"on the terrain stand-in: trace (traced + received + row_mask) + host CIR, "
+                                f"oracle/rt_oracle.c BVH path (tree built once, {t_tree:.2f} s, not timed), median "
+                                f"of {args.cpu_runs} runs after 1 warm-up ({', '.join(f'{t:.2f}' for t in ts)} s)",
+                      "build": build, "host": info}
+    return out
+
+
+def cpu_baseline_k5(args, terr, info, cells=3):
+    """coverage.py:38-57 literally on the host for seeded K5 cells of the terrain map: per cell a
+    1M-ray trace with its icosphere (oracle BVH path), host CIR, np.convolve power."""
+    from oracle import oracle as orc
+    from rf_ray_tracing_warp_amd.coverage import CoverageGrid
+    from rf_ray_tracing_warp_amd.mesh import sphere
+
+    E = orc.Mesh(terr.vertices, terr.faces)
+    grid = CoverageGrid.square(args.k5_grid, 50.0, 2.0)
+    ids = np.random.default_rng(5).choice(grid.num_cells, cells, replace=False)
+    cen = grid.centers().reshape(-1, 3)[ids]
+    N, B, tx = args.k5_rays, 3, (10.0, 0.0, 4.5)
+
+    def run():
+        for c in cen:
+            rxm = sphere(c, 0.1, 1)
+            o = orc.trace(E, orc.Mesh(rxm.vertices, rxm.faces), tx, B, 0, N, want_traced=False,
+                          nthreads=info["threads_used"])
+            ir = orc.cir_from_paths(orc.clean_paths(o["received"], o["mask"]), 1, N, 2.998e8, 100e9, 200e-9)
+            orc.signal_power(ir, 200e-9)
+    med, ts = _median_runs(run, max(1, args.cpu_runs // 2))
+    return {"value": len(ids) / med, "unit": "cells/s", "cores": info["threads_used"], "kind": "port",
+            "sample": f"{len(ids)} seeded K5 cells ({', '.join(str(int(c)) for c in ids)}), each the reference loop "
+                      f"body: {N}-ray trace over the terrain stand-in with its icosphere (oracle BVH path) + host "
+                      f"CIR + np.convolve power; median of {len(ts)} runs ({', '.join(f'{t:.2f}' for t in ts)} s)",
+            "host": info}
 
 
 # ------------------------------------------------------------------ coverage legs
@@ -255,6 +348,9 @@ def coverage_block(name, cov, grid, dt, pm, prof, B, workload, world, mode, bvh,
     traj = _roofline(f"k_traj<{t}>", prof["traj_ms"], prof["traced_ray_bounces"], B,
                      "trajectory pass, D4 bytes over the actually traced ray-bounces (rays x segments)",
                      default_size and world == 1)
+    if traj:
+        traj["active_ray_bounces"] = int(prof["traced_ray_bounces"])
+        traj["nominal_ray_bounces"] = int(cov.ray_count) * B
     rep = _roofline(f"k_replay<{t}>", prof["replay_ms"], prof["replayed_ray_bounces"], B,
                     "first-win replay, D4 bytes over its ray-bounces (sum of B - k0 over first-win records)",
                     default_size and world == 1)
@@ -283,6 +379,62 @@ def coverage_leg(args, env_m, env, local, rank, world, dist):
                           f"tx (10,0,5), {args.coverage_rays} rays per cell, {args.bounces} bounces, 10000 bins, "
                           f"signal power per cell", world, mode, False,
                           args.coverage_grid == 256 and args.coverage_rays == 1_000_000 and args.bounces == 3)
+
+
+def k1_leg(args, local, rank, world, dist):
+    """K1 (BASELINE.json configs[0]): almost_empty.stl, tx (1,0,1), rx (41,0,1) r=0.1 (main.py:25-27),
+    10k rays, 1 bounce, 20000 bins -- the reference's CPU-only plumbing case, run here as one
+    rt_trace_cir per step on the GPU (launch-latency bound: a 10k-ray burst is 40 waves)."""
+    import torch
+    from rf_ray_tracing_warp_amd._lib import DeviceMesh, check, lib, ptr
+    from rf_ray_tracing_warp_amd.mesh import load_stl, sphere
+    from rf_ray_tracing_warp_amd.tracer import cir_flags
+
+    dev = f"cuda:{local}"
+    N, B, nb = 10_000, 1, 20_000
+    m = load_stl(os.path.join(REPO, "models", "almost_empty.stl"))
+    env = DeviceMesh(m.vertices, m.faces, local)
+    rxm = sphere((41.0, 0.0, 1.0), 0.1, 1)
+    rx = DeviceMesh(rxm.vertices, rxm.faces, local)
+    tx = np.asarray((1.0, 0.0, 1.0), np.float32)
+    traced = torch.empty((N, B + 1, 3), dtype=torch.float32, device=dev)
+    received = torch.empty_like(traced)
+    mask = torch.empty(N, dtype=torch.int32, device=dev)
+    index = torch.empty(N, dtype=torch.int64, device=dev)
+    count = torch.empty(1, dtype=torch.int64, device=dev)
+    ir = torch.empty(nb, dtype=torch.float64, device=dev)
+    L = lib()
+    ws = torch.zeros(int(L.rt_trace_cir_workspace_bytes(N)), dtype=torch.uint8, device=dev)
+    sh = torch.cuda.current_stream().cuda_stream
+    flags = cir_flags(2.998e8, 100e9)
+
+    def step():
+        check(L.rt_trace_cir(env.handle, tx.ctypes.data, rx.handle, B, rank * N, N, ptr(traced), ptr(received),
+                             ptr(mask), 1.0 / (N * world), 2.998e8, 100e9, flags, nb, ptr(ir), ptr(index), ptr(count),
+                             ptr(ws), ws.numel(), sh), "rt_trace_cir")
+
+    for _ in range(50):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    steps = 500
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt[0])
+    rows = int(count.item())
+    env.close()
+    rx.close()
+    return {"metric": "ray-bounces/sec", "value": world * N * B / dt, "unit": "ray-bounces/s", "ms_per_step": dt * 1e3,
+            "workload": f"K1 (BASELINE configs[0]): almost_empty.stl, tx (1,0,1), rx (41,0,1) r=0.1, {N} rays/GPU x "
+                        f"{world}, {B} bounce, {nb} bins, rt_trace_cir per step ({steps} steps)",
+            "scaling": "weak", "received_rows_last_step": rows}
 
 
 def terrain_legs(args, local, rank, world, dist):
@@ -368,6 +520,13 @@ def terrain_legs(args, local, rank, world, dist):
                             f"tx (10,0,4.5), {args.k5_rays} rays per cell, 3 bounces, 20000 bins", world, mode,
                             True, args.k5_grid == 1024 and args.k5_rays == 1_000_000)
     env.close()
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        info, build = cpu_setup()
+        if k4 is not None:
+            cb = cpu_baseline_k4(args, terr, info, build)
+            k4["cpu_baseline"], k4["cpu_baseline_1thread"] = cb["all"], cb["1thread"]
+        if k5 is not None:
+            k5["cpu_baseline"] = cpu_baseline_k5(args, terr, info)
     return k4, k5
 
 
@@ -480,8 +639,15 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
     received_rows = int(count.item())
-    del traced, received
+    # active ray-bounces: the bounce iterations that issue a query -- every env / RX
+    # hit plus each ray's first miss (later iterations of a missed ray repeat it, kernel.py:57-98)
+    kind = torch.empty((N, B), dtype=torch.int32, device=dev)
+    check(L.rt_trace(env.handle, tx32.ctypes.data, rxd.handle, B, ray_offset, N, ptr(traced), ptr(received), ptr(mask),
+                     ptr(kind), None, sh), "rt_trace")
+    active = int((kind != 0).sum().item()) + int((kind == 0).any(dim=1).sum().item())
+    del traced, received, kind
 
+    k1_out = k1_leg(args, local, rank, world, dist) if "k1" in args.legs else None
     cov_out = coverage_leg(args, env_m, env, local, rank, world, dist) if "k3" in args.legs else None
     k4_out = k5_out = None
     if args.legs & {"k4", "k5"}:
@@ -538,7 +704,8 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": f"k_trace_bf<{B}>", "kernel_ms": kern_ms,
                          "launches_timed": int(pst[0]), "launch_sampling": f"every {args.profile_every}",
-                         "algorithmic_bytes_per_launch": bytes_per_launch},
+                         "algorithmic_bytes_per_launch": bytes_per_launch, "ray_bounces": N * B,
+                         "active_ray_bounces": active},
             "compute_roofline": valu,
             "received_rows_last_step": received_rows,
         }
@@ -548,15 +715,19 @@ def main():
             out["k4_terrain"] = k4_out
         if k5_out is not None:
             out["k5_terrain_coverage"] = k5_out
+        if k1_out is not None:
+            out["k1_plumbing"] = k1_out
         if world == 1 and not args.no_cpu_baseline:
-            info = host_info()
-            build = native_oracle()
+            info, build = cpu_setup()
             cb = cpu_baseline_k2(args, B, tx, rx, info, build)
             out["cpu_baseline"] = cb["all"]
             # Warp's CPU launch is serial: the same restatement on one thread
             out["cpu_baseline_1thread"] = cb["1thread"]
             if cov_out is not None:
                 out["coverage"]["cpu_baseline"] = cpu_baseline_k3(args, info)
+            if k1_out is not None:
+                cb1 = cpu_baseline_k1(args, info, build)
+                k1_out["cpu_baseline"], k1_out["cpu_baseline_1thread"] = cb1["all"], cb1["1thread"]
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

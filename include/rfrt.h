@@ -189,6 +189,9 @@ int rt_coverage_last_profile(rt_coverage* cov, double* out, int n);
 int rt_debug_poison(int byte);
 int rt_selftest_math(const float* x, int64_t n, float* out, int op, void* stream);
 int rt_ray_dirs(int64_t ray_offset, int64_t n, float* out, void* stream);
+/* Exact fixed point of the coverage sums, on the host: op 0 converts n (w0, w1, w2) uint64 triples
+ * in w to the nearest doubles in a; op 1 converts the n doubles in a to triples in w. */
+int rt_selftest_fx(uint64_t* w, double* a, int64_t n, int op);
 int rt_query(const rt_mesh* mesh, const float* origins, const float* dirs, int64_t n, float* t, int32_t* face,
              void* stream);
 

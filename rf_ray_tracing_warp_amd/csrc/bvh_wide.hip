@@ -1,7 +1,8 @@
 // bvh_wide.hip -- collapse the binary BVH (either builder, after pack_leaf_refs) into 4-wide
 // nodes for rt::Walk4 (rt_bvh.h).  Host pass over the device tree: every wide node takes the
 // children of one binary node and keeps opening its largest inner child (surface area) until it
-// has four; nodes are numbered breadth first, so the top levels are contiguous from node 0.
+// has four, or until opening more would let the walk's stack bound exceed RT_BVH_STACK; nodes are
+// numbered breadth first, so the top levels are contiguous from node 0.
 // The child boxes and leaf references are copied bit for bit from the binary nodes, so culling
 // is exactly as conservative as the binary traversal's.
 #include <math.h>
@@ -49,11 +50,54 @@ int build_wide(rt_mesh* m) {
       c.id = ref >= 0 ? ref : pk;
     }
   };
+  // height of every binary node (0: no inner child), iteratively: the builders number their
+  // nodes in different orders, so no index order is bottom-up
+  std::vector<int> height((size_t)m->nnodes, -1);
+  {
+    std::vector<int> st{0};
+    while (!st.empty()) {
+      const int n = st.back();
+      Child two[2];
+      children(n, two);
+      int h = 0;
+      bool ready = true;
+      for (const Child& c : two)
+        if (c.inner) {
+          if (height[c.id] < 0) {
+            st.push_back(c.id);
+            ready = false;
+          } else {
+            h = std::max(h, height[c.id] + 1);
+          }
+        }
+      if (ready) {
+        height[n] = h;
+        st.pop_back();
+      }
+    }
+  }
+  // Stack budget: a wide node w with occ[w] entries pending above it and binary height h(w) never
+  // needs more than occ[w] + h(w) entries below it if nothing under it is opened (each binary
+  // level pushes <= 1).  A child is opened only while every resulting inner child c keeps
+  // occ(c) + h(c) <= budget, so the 4-wide walk can never overflow its stack: a deep or skewed
+  // tree degrades towards binary-like nodes instead of being rejected.
+  const int budget = RT_BVH_STACK - 1;
+  if (height[0] > budget) {
+    set_error("rt_mesh_create: BVH deeper than the traversal stack");
+    return RT_EINVAL;
+  }
   std::vector<int> order{0};  // binary node of every wide node, breadth first
   std::vector<int> occ{0};    // stack entries pending above a node: parents' extra inner children
   int max_occ = 0;
   std::vector<float> wide;
   wide.reserve((size_t)m->nnodes / 2 * 32);
+  auto fits = [&](const Child* ch, int k, int o) {
+    int inner = 0;
+    for (int c = 0; c < k; ++c) inner += ch[c].inner;
+    for (int c = 0; c < k; ++c)
+      if (ch[c].inner && o + inner - 1 + height[ch[c].id] > budget) return false;
+    return true;
+  };
   for (size_t w = 0; w < order.size(); ++w) {
     Child ch[4];
     children(order[w], ch);
@@ -67,10 +111,15 @@ int build_wide(rt_mesh* m) {
           j = c;
         }
       if (j < 0) break;
-      Child two[2];
+      Child two[2], keep = ch[j];
       children(ch[j].id, two);
       ch[j] = two[0];
-      ch[k++] = two[1];
+      ch[k] = two[1];
+      if (!fits(ch, k + 1, occ[w])) {  // opening would let a subtree outgrow the stack
+        ch[j] = keep;
+        break;
+      }
+      ++k;
     }
     float node[32];
     int inner = 0;
@@ -101,8 +150,8 @@ int build_wide(rt_mesh* m) {
     }
     wide.insert(wide.end(), node, node + 32);
   }
-  if (max_occ + 1 > RT_BVH_STACK) {  // bvh4_query pushes <= inner - 1 entries per visited node
-    set_error("rt_mesh_create: BVH too deep for the 4-wide traversal stack");
+  if (max_occ + 1 > RT_BVH_STACK) {  // cannot happen: the budget above bounds every occ
+    set_error("rt_mesh_create: internal error, 4-wide stack bound exceeded");
     return RT_EINVAL;
   }
   m->wide_stack = max_occ;

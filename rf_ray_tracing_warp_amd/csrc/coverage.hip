@@ -1617,14 +1617,16 @@ __host__ __device__ __forceinline__ double fx_to_double(const Fx192& x) {
   if (sh < 64) {
     win = (x.w0 >> sh) | (x.w1 << (64 - sh));
     sticky = x.w0 & ((1ull << sh) - 1);
-    if (top >= 128) win = (x.w1 >> sh) | (x.w2 << (64 - sh)), sticky = x.w0 | (x.w1 & ((1ull << sh) - 1));
   } else if (sh == 64) {
     win = x.w1;
     sticky = x.w0;
-  } else {
+  } else if (sh < 128) {
     const int b = sh - 64;
     win = (x.w1 >> b) | (x.w2 << (64 - b));
     sticky = x.w0 | (x.w1 & ((1ull << b) - 1));
+  } else {  // top bit of w2 set (a saturated value): the window is w2 itself
+    win = x.w2;
+    sticky = x.w0 | x.w1;
   }
   return ldexp((double)(win | (sticky ? 1ull : 0ull)), sh - 136);
 }
@@ -2582,6 +2584,26 @@ int rt_coverage_received(rt_coverage* c, uint64_t* keys_out, double* amps_out, i
   const int64_t m = std::min(nu, max_out);
   if (m > 0 && keys_out) RT_HIP(hipMemcpyAsync(keys_out, c->ukeys, m * 8, hipMemcpyDeviceToDevice, s));
   if (m > 0 && amps_out) RT_HIP(hipMemcpyAsync(amps_out, c->uamps, m * 8, hipMemcpyDeviceToDevice, s));
+  return RT_OK;
+}
+
+// host self-test of the exact fixed point (tests/test_abi_host.py): op 0 = fx_to_double of n
+// (w0, w1, w2) triples in w, op 1 = fx_from_double of the n doubles in a into w
+int rt_selftest_fx(uint64_t* w, double* a, int64_t n, int op) {
+  if (n < 0 || (n > 0 && (!w || !a)) || (op != 0 && op != 1)) {
+    rt::set_error("rt_selftest_fx: invalid arguments");
+    return RT_EINVAL;
+  }
+  for (int64_t i = 0; i < n; ++i) {
+    if (op == 0) {
+      a[i] = fx_to_double(Fx192{w[3 * i], w[3 * i + 1], w[3 * i + 2]});
+    } else {
+      const Fx192 f = fx_from_double(a[i]);
+      w[3 * i] = f.w0;
+      w[3 * i + 1] = f.w1;
+      w[3 * i + 2] = f.w2;
+    }
+  }
   return RT_OK;
 }
 

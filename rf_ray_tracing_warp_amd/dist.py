@@ -125,8 +125,10 @@ def exchange_records(keys, vals, send_counts, group=None):
     recv_counts = [int(c) for c in rc.tolist()]
     v = vals[:n]
     is_f64 = v.dim() == 1 and v.dtype == torch.float64
-    v64 = v.contiguous().view(torch.int64).reshape(n, -1) if is_f64 else v.contiguous().reshape(n, -1).to(torch.int64)
-    width = 1 + v64.shape[1]
+    # explicit widths: reshape(0, -1) is ambiguous and raises when this rank sends nothing
+    vw = 1 if (is_f64 or v.dim() == 1) else int(v.shape[1])
+    v64 = v.contiguous().view(torch.int64).reshape(n, 1) if is_f64 else v.contiguous().reshape(n, vw).to(torch.int64)
+    width = 1 + vw
     packed = torch.cat([keys[:n].view(torch.int64).reshape(n, 1), v64], dim=1).to(wire)
     out = torch.empty((sum(recv_counts), width), dtype=torch.int64, device=wire)
     dist.all_to_all_single(out, packed, recv_counts, send_counts, group=group)

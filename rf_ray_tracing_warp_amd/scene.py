@@ -230,9 +230,10 @@ def glb_from_html(html: str) -> bytes:
 
 
 def visualize(mesh=None, tx_pos=None, rx_pos=None, paths=None, points=None, point_color_pairs=None,
-              out_path="viz/scene.html", serve=True, port=8000):
+              out_path="viz/scene.html", serve=True, port=8000, host="127.0.0.1"):
     """viz/visualization.py:6-50: the scene of a trace as ``viz/scene.html``, then an HTTP server on
-    ``port`` answering ``/`` and ``/index.html`` with it (blocks, as the reference does)."""
+    ``host:port`` answering ``/`` and ``/index.html`` with it and 404 for everything else (blocks,
+    as the reference does).  host defaults to the loopback interface; pass "" for all interfaces."""
     sc = Scene()
     if mesh is not None:
         sc.add_mesh(mesh.vertices, mesh.faces, GREY, name=getattr(mesh, "name", None))
@@ -257,15 +258,32 @@ def visualize(mesh=None, tx_pos=None, rx_pos=None, paths=None, points=None, poin
     if serve:
         import http.server
 
-        page = "/" + os.path.relpath(out_path).replace(os.sep, "/")
-
-        class Handler(http.server.SimpleHTTPRequestHandler):
-            def do_GET(self):
-                if self.path in ("/index.html", "/"):
-                    self.path = page
-                return http.server.SimpleHTTPRequestHandler.do_GET(self)
-
-        httpd = http.server.HTTPServer(("", port), Handler)
-        print(f"Serving visualization at localhost:{port}")
+        httpd = http.server.HTTPServer((host, port), _page_handler(out_path))
+        print(f"Serving visualization at {host or 'localhost'}:{port}")
         httpd.serve_forever()
     return sc
+
+
+def _page_handler(out_path):
+    """HTTP handler that answers only / and /index.html, with the page at out_path (the
+    reference's handler, viz/visualization.py:43-47, serves nothing else either); every other path
+    is a 404, so the working directory is never listed or served."""
+    import http.server
+
+    class Handler(http.server.BaseHTTPRequestHandler):
+        def do_GET(self):
+            if self.path not in ("/", "/index.html"):
+                self.send_error(404)
+                return
+            with open(out_path, "rb") as f:
+                body = f.read()
+            self.send_response(200)
+            self.send_header("Content-Type", "text/html; charset=utf-8")
+            self.send_header("Content-Length", str(len(body)))
+            self.end_headers()
+            self.wfile.write(body)
+
+        def log_message(self, *args):
+            pass
+
+    return Handler

@@ -53,6 +53,10 @@ def cir_flags(light_speed_mps, sample_rate_hz) -> int:
 class Tracer:
     """tracer.py:11 ``class Tracer`` -- same constructor arguments, plus ``device`` / ``verbose``."""
 
+    # rt_trace_cir's per-call limit (its chunk tables, include/rfrt.h); larger bursts take rt_trace +
+    # rt_compact + rt_cir, which have no cap (the reference's tracer.py has none either)
+    TRACE_CIR_MAX_RAYS = 1 << 25
+
     def __init__(self, environment_trimesh, light_speed_mps, sample_rate_hz, sample_window_s, max_bounces,
                  tx_num_rays, device: int | None = None, verbose: bool = False):
         import torch
@@ -157,6 +161,17 @@ class Tracer:
                                  self._tc_ws.numel(), _lib.stream_handle(self.device)), "rt_trace_cir")
         return index, count
 
+    def _trace_and_cir(self, tx_pos, rx_mesh, received, mask, tx_power, ir, traced=None, ray_offset=0, n=None):
+        """tracer.py:75-117 on the device for a burst of any size: the fused rt_trace_cir up to
+        TRACE_CIR_MAX_RAYS rays, else rt_trace then rt_compact + rt_cir (ir must be zero; rt_cir adds
+        the paths in ray order).  Returns (index, count) device tensors of the received rows."""
+        n = self.tx_num_rays if n is None else int(n)
+        if n <= self.TRACE_CIR_MAX_RAYS:
+            return self.trace_cir_device(tx_pos, rx_mesh, received, mask, tx_power, ir, traced=traced,
+                                         ray_offset=ray_offset, n=n)
+        self.trace_device(tx_pos, rx_mesh, received, mask, traced=traced, ray_offset=ray_offset, n=n)
+        return self.cir_device(received, mask, tx_power, ir, n=n)
+
     def n_bins(self) -> int:
         return int(self.sample_window_s * self.sample_rate_hz)  # tracer.py:101
 
@@ -175,7 +190,7 @@ class Tracer:
             traced = torch.empty((N, P, 3), dtype=torch.float32, device=dev)
         else:
             traced = None  # scratch in the reference (Q6); kept in registers here
-        index, count = self.trace_cir_device(tx_pos, rx_mesh, received, mask, tx_power, ir, traced=traced)
+        index, count = self._trace_and_cir(tx_pos, rx_mesh, received, mask, tx_power, ir, traced=traced)
         k = int(count.item())  # synchronises (tracer.py:80)
         rows = received.index_select(0, index[:k]).cpu().numpy() if k else np.zeros((0, P, 3), np.float32)
         cleaned_paths = []
@@ -224,8 +239,8 @@ class Tracer:
         k = 0
         rows = np.zeros((0, P, 3), np.float32)
         if n > 0:
-            index, count = self.trace_cir_device(tx_pos, rx_mesh, received, mask, tx_power, ir, traced=traced,
-                                                 ray_offset=lo, n=n)
+            index, count = self._trace_and_cir(tx_pos, rx_mesh, received, mask, tx_power, ir, traced=traced,
+                                               ray_offset=lo, n=n)
             k = int(count.item())
             if k:
                 rows = received.index_select(0, index[:k]).cpu().numpy()

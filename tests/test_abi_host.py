@@ -92,3 +92,45 @@ def test_nep50_cir_flags_follow_numpy_promotion(c, fs):
         assert bool(f & _lib.RT_CIR_FS_F64) == (np.asarray(val).dtype == np.float64)
     else:
         assert np.asarray(val).dtype == np.float64
+
+
+def _fx_to_double(words):
+    L = _lib.lib()
+    w = np.ascontiguousarray(np.asarray(words, dtype=np.uint64).reshape(-1, 3))
+    out = np.zeros(len(w))
+    _lib.check(L.rt_selftest_fx(w.ctypes.data, out.ctypes.data, len(w), 0), "rt_selftest_fx")
+    return out
+
+
+def _fx_exact(words):
+    from fractions import Fraction
+    w0, w1, w2 = (int(x) for x in words)
+    return Fraction(w0 + (w1 << 64) + (w2 << 128), 1 << 136)
+
+
+def test_fixed_point_to_double_is_correctly_rounded_everywhere():
+    """coverage.hip fx_to_double (the coverage bin sums, rounded once): every window position,
+    including a saturated value whose top bit is bit 191 (the shift by 64 there)."""
+    rng = np.random.default_rng(7)
+    cases = [(0, 0, 0), (1, 0, 0), (~0 & (2**64 - 1), 0, 0), (0, 1, 0), (0, 0, 1), (2**63, 2**63, 2**63),
+             (2**64 - 1, 2**64 - 1, 2**64 - 1), (1, 0, 2**63), (0, 1, 2**63), (0, 0, 2**63), (2**64 - 1, 2**64 - 1, 0)]
+    for top in range(0, 192, 3):
+        for _ in range(4):
+            v = int(rng.integers(0, 2**63)) | (1 << 63)
+            lo = int(rng.integers(0, 2**63)) * 2 + int(rng.integers(0, 2))
+            x = (lo | (v << 128)) >> (191 - top) if top < 191 else (lo | (v << 128))
+            cases.append((x & (2**64 - 1), (x >> 64) & (2**64 - 1), x >> 128))
+    got = _fx_to_double(cases)
+    for c, g in zip(cases, got):
+        assert g == float(_fx_exact(c)), (c, g)  # float(Fraction) rounds to nearest even
+
+
+def test_fixed_point_from_double_truncates_exactly():
+    L = _lib.lib()
+    a = np.array([0.0, 1e-6, 3.5e-41, 2.0**-136, 2.0**-137, 1.0, 123.456, 2.0**55, 2.0**56 * 0.75, 5e-324], np.float64)
+    w = np.zeros((len(a), 3), np.uint64)
+    _lib.check(L.rt_selftest_fx(w.ctypes.data, a.ctypes.data, len(a), 1), "rt_selftest_fx")
+    from fractions import Fraction
+    for x, ww in zip(a, w):
+        want = int(Fraction(float(x)) * (1 << 136))  # truncation below the unit 2^-136
+        assert _fx_exact(ww) * (1 << 136) == want, x

@@ -170,3 +170,35 @@ def test_gather_rows_variable_counts(world):
             assert blk.shape[0] == src * 2
             for i in range(src * 2):
                 assert (blk[i] == src * 100 + i).all()
+
+
+def _a2a_empty_worker(rank, world, port, out):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # rank 0 sends nothing at all (a ray share with no first-win record); the others send 2 per owner
+    counts = [0] * world if rank == 0 else [2] * world
+    n = sum(counts)
+    keys = torch.tensor([rank * 100 + d * 10 + i for d in range(world) for i in range(counts[d])], dtype=torch.int64)
+    sums = torch.stack([keys, keys + 1, keys + 2], dim=1) if n else torch.empty((0, 3), dtype=torch.int64)
+    amps = keys.to(torch.float64) / 3.0
+    k, s = rdist.exchange_records(keys, sums, counts)
+    k1, a1 = rdist.exchange_records(keys, amps, counts)
+    out.put((rank, k.tolist(), s.tolist(), k1.tolist(), a1.tolist()))
+    dist.destroy_process_group()
+
+
+def test_exchange_records_with_an_empty_sender():
+    """a rank whose send counts are all zero must not break the record all-to-all."""
+    world = 3
+    q = mp.get_context("spawn").Queue()
+    pc = mp.spawn(_a2a_empty_worker, args=(world, _port(), q), nprocs=world, join=False)
+    got = dict((r, rest) for r, *rest in (q.get(timeout=120) for _ in range(world)))
+    pc.join()
+    for d in range(world):
+        k, s, k1, a1 = got[d]
+        want = [r * 100 + d * 10 + i for r in range(1, world) for i in range(2)]
+        assert k == want and k1 == want
+        assert s == [[x, x + 1, x + 2] for x in want]
+        assert a1 == [float(np.float64(x) / 3.0) for x in want]

@@ -119,3 +119,18 @@ def test_trace_profile_stats_counts_kernels():
     st = np.zeros(4)
     check(L.rt_trace_profile_stats(st.ctypes.data, 4), "rt_trace_profile_stats")
     assert st[0] == 3 and 0 < st[2] <= st[1] <= st[3] < 100
+
+
+def test_compute_cir_above_the_fused_cap_takes_the_uncapped_path(monkeypatch):
+    """rt_trace_cir takes at most 2^25 rays per call; Tracer.compute_cir falls back to
+    rt_trace + rt_compact + rt_cir above that (no cap, like the reference's tracer.py).  The cap is
+    lowered here so a small burst crosses it: both paths give the same paths and impulse response."""
+    from rf_ray_tracing_warp_amd import Tracer
+    room = load_stl(os.path.join(REPO, "models", "room.stl"))
+    t = Tracer(room, C, FS, 100e-9, 3, 300_000, device=0)
+    ref_paths, ref_ir = t.compute_cir(np.array((10.0, 0.0, 5.0)), 1, np.array((8.5, 0.5, 5.0)), 1.5)
+    monkeypatch.setattr(Tracer, "TRACE_CIR_MAX_RAYS", 1000)
+    paths, ir = t.compute_cir(np.array((10.0, 0.0, 5.0)), 1, np.array((8.5, 0.5, 5.0)), 1.5)
+    assert len(paths) == len(ref_paths) > 10_000
+    assert all(np.array_equal(a, b) for a, b in zip(paths, ref_paths))
+    assert ir.tobytes() == ref_ir.tobytes()

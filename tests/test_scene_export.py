@@ -89,3 +89,34 @@ def test_visualize_writes_a_page_that_round_trips(tmp_path, golden):
     assert abs(np.linalg.norm(tx - golden["tx"], axis=1).max() - 0.25) < 1e-6
     col = _acc(js, binb, js["meshes"][-1]["primitives"][0]["attributes"]["COLOR_0"])
     assert (col == [0, 0, 255, 255]).all()
+
+
+def test_page_handler_serves_only_the_page(tmp_path):
+    """the viewer answers / and /index.html only (viz/visualization.py:43-47), never
+    other files of the working directory."""
+    import http.client
+    import http.server
+    import threading
+
+    from rf_ray_tracing_warp_amd.scene import _page_handler
+    page = tmp_path / "scene.html"
+    page.write_text("<html>scene</html>")
+    (tmp_path / "secret.txt").write_text("no")
+    httpd = http.server.HTTPServer(("127.0.0.1", 0), _page_handler(str(page)))
+    th = threading.Thread(target=httpd.serve_forever, daemon=True)
+    th.start()
+    try:
+        port = httpd.server_address[1]
+        got = {}
+        for path in ("/", "/index.html", "/secret.txt", "/scene.html", "/../", "/tests/"):
+            c = http.client.HTTPConnection("127.0.0.1", port, timeout=10)
+            c.request("GET", path)
+            r = c.getresponse()
+            got[path] = (r.status, r.read())
+            c.close()
+        assert got["/"] == (200, b"<html>scene</html>") and got["/index.html"] == got["/"]
+        for path in ("/secret.txt", "/scene.html", "/../", "/tests/"):
+            assert got[path][0] == 404
+    finally:
+        httpd.shutdown()
+        httpd.server_close()

@@ -1,6 +1,9 @@
-"""Per-kernel resource usage of librfrt's own kernels (VGPRs, scratch, dynamic stack, occupancy).
+"""Per-kernel resource usage of librfrt's own kernels (VGPRs, SGPRs, scratch, dynamic stack, LDS,
+occupancy), from the compiler's resource-usage remarks for the code objects the library is built from.
 
-    python tools/kernel_resources.py [source.hip ...]
+    python tools/kernel_resources.py [--out profiles/rNN_kernel_resources] [source.hip ...]
+
+With --out, also writes <out>.json (every remark field per kernel) and <out>.md (the table).
 
 Compiles each source with the library's flags plus -Rpass-analysis=kernel-resource-usage and
 prints one line per kernel of ours (library kernels from rocPRIM/hipCUB are skipped).  A kernel
@@ -38,14 +41,50 @@ def resources(src):
     return rows
 
 
+def demangle(names):
+    try:
+        r = subprocess.run(["c++filt"], input="\n".join(names), capture_output=True,
+                           text=True, timeout=60)
+        out = r.stdout.splitlines()
+        if len(out) == len(names):
+            return out
+    except (OSError, subprocess.SubprocessError):
+        pass
+    return names
+
+
 def main(argv):
+    import json
+    out = None
+    if argv[:1] == ["--out"]:
+        out, argv = argv[1], argv[2:]
     srcs = argv or sorted(glob.glob(os.path.join(B.CSRC, "*.hip")))
+    table = []
     for src in srcs:
-        for r in resources(src):
-            print(f"{os.path.basename(src):14s} VGPR {r.get('VGPRs', '?'):>4s} AGPR {r.get('AGPRs', '?'):>3s} "
+        rows = resources(src)
+        for r, d in zip(rows, demangle([r["name"] for r in rows])):
+            r["source"] = os.path.basename(src)
+            r["demangled"] = d
+            table.append(r)
+            print(f"{r['source']:14s} VGPR {r.get('VGPRs', '?'):>4s} SGPR {r.get('TotalSGPRs', '?'):>3s} "
+                  f"spill {r.get('VGPRs Spill', '?'):>3s} "
                   f"scratch {r.get('ScratchSize [bytes/lane]', '?'):>5s} dynstack {r.get('Dynamic Stack', '?'):5s} "
                   f"occ {r.get('Occupancy [waves/SIMD]', '?'):>2s} LDS {r.get('LDS Size [bytes/block]', '?'):>6s}  "
-                  f"{r['name'][:90]}")
+                  f"{d[:100]}")
+    if out:
+        with open(out + ".json", "w") as f:
+            json.dump({"cflags": B.CFLAGS, "kernels": table}, f, indent=1)
+        with open(out + ".md", "w") as f:
+            f.write("# Kernel resources (compiler remarks, `python tools/kernel_resources.py --out ...`)\n\n")
+            f.write("Flags: `" + " ".join(B.CFLAGS) + "`\n\n")
+            f.write("| source | kernel | VGPRs | VGPR spills | AGPRs | SGPRs | scratch B/lane | dyn. stack | LDS B/block "
+                    "| waves/SIMD |\n")
+            f.write("|---|---|---|---|---|---|---|---|---|---|\n")
+            for r in table:
+                f.write(f"| {r['source']} | `{r['demangled'][:120]}` | {r.get('VGPRs', '?')} | {r.get('VGPRs Spill', '?')} | "
+                        f"{r.get('AGPRs', '?')} | {r.get('TotalSGPRs', '?')} | {r.get('ScratchSize [bytes/lane]', '?')} | "
+                        f"{r.get('Dynamic Stack', '?')} | {r.get('LDS Size [bytes/block]', '?')} | "
+                        f"{r.get('Occupancy [waves/SIMD]', '?')} |\n")
 
 
 if __name__ == "__main__":
