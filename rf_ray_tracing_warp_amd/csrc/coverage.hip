@@ -479,7 +479,7 @@ __global__ __launch_bounds__(256, RT_COV_TRAJ_WAVES) void k_traj_split(CovParams
     for (int k = 0; k < p.B; ++k) {
       const rt::Shear s = rt::make_shear(pos, dir);
       rt::Walk4 w;
-      rt::WalkStack st;
+      rt::WalkStack st = rt::make_stack();
       bool active = false;
       if (alive) {
         rt::split_init<G>(w, st, p.env_bvh, s, pos, dir, j);

@@ -115,10 +115,55 @@ __device__ __forceinline__ float cull_limit(const Hit& h, float tc) { return fmi
 // The (node, entry t) stack, kept apart from the walk's scalar state: inside one aggregate with
 // the dynamically indexed arrays, the scalars went to scratch too (k_traj<true> 92 -> 102 VGPRs
 // and +40 B scratch: cur, sp, the best hit and the ray box reloaded every step).
+//
+// RT_BVH_LDS_STACK = K > 0 keeps the K entries nearest the bottom of every lane's stack in LDS
+// (a [K][256] column per thread of the 256-thread block: lanes of a wave always hit distinct banks,
+// whatever their stack pointers) and only deeper entries in the private array, so a walk that stays
+// within K pending entries never touches scratch memory.
+#ifndef RT_BVH_LDS_STACK
+#define RT_BVH_LDS_STACK 0
+#endif
+#if RT_BVH_LDS_STACK
+constexpr int kLdsStack = RT_BVH_LDS_STACK;
+struct WalkStack {
+  int* ln;    // this thread's LDS column: entry i at ln[256 * i]
+  float* lt;
+  int node[RT_BVH_STACK - kLdsStack];
+  float t[RT_BVH_STACK - kLdsStack];
+  __device__ __forceinline__ void set(int i, int c, float tt) {
+    if (i < kLdsStack) {
+      ln[256 * i] = c;
+      lt[256 * i] = tt;
+    } else {
+      node[i - kLdsStack] = c;
+      t[i - kLdsStack] = tt;
+    }
+  }
+  __device__ __forceinline__ int get_node(int i) const { return i < kLdsStack ? ln[256 * i] : node[i - kLdsStack]; }
+  __device__ __forceinline__ float get_t(int i) const { return i < kLdsStack ? lt[256 * i] : t[i - kLdsStack]; }
+};
+// every kernel that walks gets one [K][256] block of LDS (blocks of at most 256 threads)
+__device__ __forceinline__ WalkStack make_stack() {
+  __shared__ int s_node[kLdsStack * 256];
+  __shared__ float s_t[kLdsStack * 256];
+  WalkStack st;
+  st.ln = s_node + threadIdx.x;
+  st.lt = s_t + threadIdx.x;
+  return st;
+}
+#else
 struct WalkStack {
   int node[RT_BVH_STACK];
   float t[RT_BVH_STACK];
+  __device__ __forceinline__ void set(int i, int c, float tt) {
+    node[i] = c;
+    t[i] = tt;
+  }
+  __device__ __forceinline__ int get_node(int i) const { return node[i]; }
+  __device__ __forceinline__ float get_t(int i) const { return t[i]; }
 };
+__device__ __forceinline__ WalkStack make_stack() { return WalkStack(); }
+#endif
 
 // binary nodes: near child first, far child pushed
 struct Walk2 {
@@ -139,7 +184,7 @@ struct Walk2 {
     if (cur < 0) {  // pop
       if (sp == 0) return false;
       --sp;
-      if (st.t[sp] <= cull_limit(h, tc)) cur = st.node[sp];
+      if (st.get_t(sp) <= cull_limit(h, tc)) cur = st.get_node(sp);
       else visit = false;
     }
     if (visit) {
@@ -165,8 +210,7 @@ struct Walk2 {
     if (h0 && h1) {
       const bool first0 = t0 <= t1;
       if (sp < RT_BVH_STACK) {  // cannot overflow: tree depth <= RT_BVH_STACK - 4 (bvh.hip)
-        st.node[sp] = first0 ? c1 : c0;
-        st.t[sp] = first0 ? t1 : t0;
+        st.set(sp, first0 ? c1 : c0, first0 ? t1 : t0);
         ++sp;
       }
       cur = first0 ? c0 : c1;
@@ -213,8 +257,7 @@ struct Walk4 {
   }
   __device__ __forceinline__ void push(WalkStack& st, int c, float t) {
     if (sp < RT_BVH_STACK) {  // cannot overflow: bound checked on the host (build_wide)
-      st.node[sp] = c;
-      st.t[sp] = t;
+      st.set(sp, c, t);
       ++sp;
     }
   }
@@ -223,7 +266,7 @@ struct Walk4 {
     if (cur < 0) {  // pop
       if (sp == 0) return false;
       --sp;
-      if (st.t[sp] <= cull_limit(h, tc)) cur = st.node[sp];
+      if (st.get_t(sp) <= cull_limit(h, tc)) cur = st.get_node(sp);
       else visit = false;
     }
     if (visit) {
@@ -357,7 +400,7 @@ using Walk = Walk2;
 __device__ __forceinline__ Hit bvh_query(const BvhView& b, const Shear& s, float3 o, float3 d,
                                          float tcull = RT_MAX_T) {
   Walk w;
-  WalkStack st;
+  WalkStack st = make_stack();
   w.init(o, d, tcull);
   bool active = true;
   while (active) active = w.step(b, s, st);

@@ -101,6 +101,9 @@ __device__ __forceinline__ bool rx_maybe(const TraceArgs& a, float3 o, float3 d,
 #ifndef RT_NT_ROWS
 #define RT_NT_ROWS 1
 #endif
+#ifndef RT_ROW_X2
+#define RT_ROW_X2 0  // 8-byte stores for rows of P = 2, 6 points (A/B builds)
+#endif
 template <int P>
 __device__ __forceinline__ void store_row_fixed(float* dst, const float (*pts)[3]) {
   if constexpr ((P * 3) % 4 == 0) {  // 16-B aligned rows (P = 4, 8): 16-byte stores
@@ -115,6 +118,19 @@ __device__ __forceinline__ void store_row_fixed(float* dst, const float (*pts)[3
       __builtin_nontemporal_store(v, d4 + j);
 #else
       d4[j] = v;
+#endif
+    }
+  } else if constexpr (RT_ROW_X2 && (P * 3) % 2 == 0) {  // 8-B aligned rows (P = 2, 6): 8-byte stores
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    f2v* d2 = reinterpret_cast<f2v*>(dst);
+#pragma unroll
+    for (int j = 0; j < P * 3 / 2; ++j) {
+      const int i = 2 * j;
+      const f2v v = {pts[i / 3][i % 3], pts[(i + 1) / 3][(i + 1) % 3]};
+#if RT_NT_ROWS
+      __builtin_nontemporal_store(v, d2 + j);
+#else
+      d2[j] = v;
 #endif
     }
   } else {

@@ -20,6 +20,7 @@
 #   covvar    tools/cov_variants.py over LIBS (A/B, hashed)                  -> ${TAG}_cov.jsonl
 #   tracevar  tools/trace_variants.py over LIBS (SCENE=room|terrain)         -> ${TAG}_trace.jsonl
 #   k2var     tools/k2_fused_variants.py over LIBS                           -> ${TAG}_k2.jsonl
+#   k4write   rocprofv3 --pmc WRITE_SIZE / FETCH_SIZE over tools/k4_write_ab.py, per library in LIBS
 #   rehearse  bench.py N=2,4 on this one GPU (gloo, RFRT_BENCH_ONE_GPU=1)    -> ${TAG}_rehearse_<n>.log
 #   full      = tests smoke bench
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
@@ -85,6 +86,17 @@ run_task() {
     k2var)
       LIBS="$LIBS" timeout -k 10 ${T_VAR:-300} python -u tools/k2_fused_variants.py > ${O}_k2.jsonl 2>&1
       rc=$?; cat ${O}_k2.jsonl | cut -c1-300; step_rc $rc k2var ;;
+    k4write)
+      # WRITE_SIZE / FETCH_SIZE of k_trace_bvh<5> per output set, for every library in LIBS
+      mkdir -p gpurun_out/prof_${TAG}
+      for lib in $LIBS; do
+        b=$(basename $lib .so)
+        for c in WRITE_SIZE FETCH_SIZE; do
+          RFRT_LIB_PATH=$lib timeout -s KILL ${T_PMC:-180} rocprofv3 --pmc $c --kernel-trace --output-format csv \
+            -d gpurun_out/prof_${TAG}/k4w_${b}_$c -o k -- python3 tools/k4_write_ab.py > gpurun_out/prof_${TAG}/k4w_${b}_$c.log 2>&1
+          rc=$?; echo "k4write $b $c rc=$rc"; tail -1 gpurun_out/prof_${TAG}/k4w_${b}_$c.log | cut -c1-300; step_rc $rc "k4write $b"
+        done
+      done ;;
     rehearse)
       for n in 2 4; do
         RFRT_BENCH_ONE_GPU=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
