@@ -44,6 +44,8 @@ struct TraceArgs {
   int32_t* hit_kind;  // (n, B) or null
   int32_t* hit_face;  // (n, B) or null
   const int32_t* order;  // processing order of the rows (null = identity), see launch_trace
+  int win_chunks;        // > 0: order is sorted within windows of win_chunks 256-row chunks, and every
+                         // window's chunks run on one XCD (xcd_chunk)
   bool fused;             // brute-force kernels under rt_trace_cir: list received rows, per-path CIR
   rt::TraceCirFused fz;
 };
@@ -348,6 +350,21 @@ __global__ __launch_bounds__(512) void k_trace_cir_tail(rt::TraceCirFused fz, in
   if (wave == 0 && fz.ir) rt::ir_accumulate_wave(fz.cbin, fz.camp, total, fz.k.n_bins, fz.ir, false);
 }
 
+// XCD-affine chunk order for window-sorted bursts.  Blocks are dispatched round-robin over the 8
+// XCDs (block b on XCD b % 8), and every XCD has its own L2.  Window w (win_chunks consecutive
+// 256-row chunks, its rows sorted by direction inside the window, dir_order_windows) is traced by
+// the blocks of XCD w % 8 only, so the partial 128-B lines its scattered rows leave in that XCD's
+// L2 are completed there before they are written back (a globally sorted burst scatters each row
+// over the whole output: 3x write traffic, profiles/r3b_k4_write_split.json).  Iteration `it` of
+// block b = (xcd, q) takes item q + it * nq of its XCD's (window, chunk) items; -1 when done.
+__device__ __forceinline__ int64_t xcd_chunk(int win_chunks, int64_t nchunks, int64_t it) {
+  const int64_t x = blockIdx.x & 7, q = blockIdx.x >> 3, nq = (int64_t)gridDim.x >> 3;
+  const int64_t t = q + it * nq;
+  const int64_t w = x + 8 * (t / win_chunks);
+  const int64_t chunk = w * win_chunks + t % win_chunks;
+  return w * win_chunks < nchunks ? chunk : -1;
+}
+
 template <int B, bool USE_BVH>
 __device__ __forceinline__ void trace_body(const TraceArgs& a) {
   constexpr int P = B + 1;
@@ -360,7 +377,10 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
   const float qnan = __builtin_nanf("");
   // block-uniform loop over 256-row chunks (the same rows per thread as a grid-stride loop), so a
   // wave can list its part of a chunk's received rows for rt_trace_cir
-  for (int64_t chunk = blockIdx.x; chunk * 256 < a.n; chunk += gridDim.x) {
+  const int64_t nchunks = (a.n + 255) / 256;
+  for (int64_t it = 0;; ++it) {
+    const int64_t chunk = a.win_chunks > 0 ? xcd_chunk(a.win_chunks, nchunks, it) : blockIdx.x + it * gridDim.x;
+    if (chunk < 0 || chunk >= nchunks) break;
     const int64_t irow = chunk * 256 + threadIdx.x;
     bool got = false;
     if (irow < a.n) {
@@ -715,10 +735,8 @@ __global__ __launch_bounds__(256) void k_trace_bf_generic(TraceArgs a, int B) {
 // Sort key of a ray: the cell of its initial direction on a 256x256 octahedral map, in Morton
 // order, so that rays traced by one wave start in nearly the same direction.  Only the order in
 // which rows are processed changes; every row is computed exactly as before.
-__global__ __launch_bounds__(256) void k_dir_keys(int64_t ray_offset, int64_t n, uint16_t* keys, int32_t* rows) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const float3 d = rt::ray_dir(ray_offset + i);
+__device__ __forceinline__ uint16_t dir_cell(int64_t gid) {
+  const float3 d = rt::ray_dir(gid);
   const float s = fabsf(d.x) + fabsf(d.y) + fabsf(d.z);
   float x = d.x / s, y = d.y / s;
   if (d.z < 0.0f) {
@@ -731,8 +749,39 @@ __global__ __launch_bounds__(256) void k_dir_keys(int64_t ray_offset, int64_t n,
   uint32_t k = 0;
 #pragma unroll
   for (int b = 0; b < 8; ++b) k |= ((cx >> b) & 1u) << (2 * b) | ((cy >> b) & 1u) << (2 * b + 1);
-  keys[i] = (uint16_t)k;
+  return (uint16_t)k;
+}
+__global__ __launch_bounds__(256) void k_dir_keys(int64_t ray_offset, int64_t n, uint16_t* keys, int32_t* rows) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  keys[i] = dir_cell(ray_offset + i);
   rows[i] = (int32_t)i;
+}
+
+// Window-sorted order (xcd_chunk): window w = rows [w W, (w + 1) W), W = 1024 * RT_DIR_WIN_ITEMS,
+// sorted by direction cell inside the window by one 1024-thread block in LDS (stable: a key's rows
+// stay ascending), so one launch replaces the device-wide radix sort's passes.  Rows past n get the
+// largest key and, being last in the input, sort after every valid row of the window.
+#ifndef RT_DIR_WIN_ITEMS
+#define RT_DIR_WIN_ITEMS 8
+#endif
+constexpr int kDirWinRows = 1024 * RT_DIR_WIN_ITEMS;
+__global__ __launch_bounds__(1024) void k_dir_window_sort(int64_t ray_offset, int64_t n, int32_t* order) {
+  using Sort = rocprim::block_radix_sort<uint16_t, 1024, RT_DIR_WIN_ITEMS, int32_t>;
+  __shared__ typename Sort::storage_type st;
+  const int64_t base = (int64_t)blockIdx.x * kDirWinRows + (int64_t)threadIdx.x * RT_DIR_WIN_ITEMS;
+  uint16_t k[RT_DIR_WIN_ITEMS];
+  int32_t v[RT_DIR_WIN_ITEMS];
+#pragma unroll
+  for (int i = 0; i < RT_DIR_WIN_ITEMS; ++i) {
+    const int64_t row = base + i;
+    k[i] = row < n ? dir_cell(ray_offset + row) : (uint16_t)0xFFFF;
+    v[i] = (int32_t)row;
+  }
+  Sort().sort(k, v, st);
+#pragma unroll
+  for (int i = 0; i < RT_DIR_WIN_ITEMS; ++i)
+    if (base + i < n) order[base + i] = v[i];
 }
 
 }  // namespace
@@ -789,6 +838,27 @@ const int32_t* dir_order(int64_t ray_offset, int64_t n, hipStream_t stream, void
   return r_out;
 }
 
+// window-sorted order for the BVH trace kernels (xcd_chunk); nullptr on failure
+const int32_t* dir_order_windows(int64_t ray_offset, int64_t n, hipStream_t stream, void** ws) {
+  keep_pool_memory();
+  *ws = nullptr;
+  hipError_t e = hipMallocAsync(ws, ((size_t)n * 4 + 255) / 256 * 256, stream);
+  if (e != hipSuccess) {
+    hip_fail(e, "dir_order_windows workspace");
+    *ws = nullptr;
+    return nullptr;
+  }
+  hipLaunchKernelGGL(k_dir_window_sort, dim3((unsigned)((n + kDirWinRows - 1) / kDirWinRows)), dim3(1024), 0, stream,
+                     ray_offset, n, (int32_t*)*ws);
+  return (const int32_t*)*ws;
+}
+
+// RT_XCD_WINDOWS: BVH bursts of at least 64 windows are traced window by window, each window on one
+// XCD (xcd_chunk); 0 keeps the device-wide direction sort
+#ifndef RT_XCD_WINDOWS
+#define RT_XCD_WINDOWS 1
+#endif
+
 void trace_mark(int i, hipStream_t s);
 void trace_events(hipEvent_t* e0, hipEvent_t* e1);
 
@@ -832,7 +902,7 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
   int dev_cu = 256;
   const int64_t want = (n + 255) / 256;
   const int64_t cap = (int64_t)dev_cu * 16;
-  const int grid = (int)(want < cap ? want : cap);
+  const int grid0 = (int)(want < cap ? want : cap);
   const dim3 blk(256);
   // a generic (non-generic-Warp) B>8 falls back to the row-resident kernel
   if (traced == nullptr && B > 8) {
@@ -847,12 +917,16 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
     if (rc) return rc;
   }
   const bool sort = bvh && n >= kSortMinRays && n <= INT32_MAX;
+  const bool windows = sort && RT_XCD_WINDOWS && n >= 64 * (int64_t)kDirWinRows;
   if (sort) trace_mark(0, stream);
   if (sort) {
-    a.order = dir_order(ray_offset, n, stream, &sort_ws);
+    a.order = windows ? dir_order_windows(ray_offset, n, stream, &sort_ws) : dir_order(ray_offset, n, stream, &sort_ws);
     if (!a.order) return -1;
+    a.win_chunks = windows ? kDirWinRows / 256 : 0;
     trace_mark(1, stream);
   }
+  // xcd_chunk needs whole groups of 8 blocks (one per XCD)
+  const int grid = windows ? (grid0 + 7) / 8 * 8 : grid0;
   // profiling: the kernel's own dispatch packet carries the start/stop timestamps
   // (hipExtLaunchKernelGGL), so timing adds no marker packets -- and no gaps -- to the stream
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
