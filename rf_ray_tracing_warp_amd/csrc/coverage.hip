@@ -1006,10 +1006,8 @@ __global__ __launch_bounds__(256) void k_sel_scatter(const uint8_t* flag, const 
 #define RT_COV_BVH_DIRKEY 0
 #endif
 template <bool USE_BVH>
-__global__ __launch_bounds__(256) void k_replay_keys(CovParams p, const uint64_t* keys, const int64_t* list, int64_t nl,
-                                                     uint16_t* okey, int32_t* oval) {
-  for (int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; li < nl; li += (int64_t)gridDim.x * blockDim.x) {
-    const uint64_t key = keys[list[li]];
+__device__ __forceinline__ uint16_t replay_key(const CovParams& p, uint64_t key) {
+  {
     const int64_t cell = (int64_t)(key >> 28), r = (int64_t)((key >> 4) & 0xFFFFFF);
     const int k0 = (int)(key & 15);
     const float4 d = traj_d(p, r, k0);
@@ -1027,14 +1025,50 @@ __global__ __launch_bounds__(256) void k_replay_keys(CovParams p, const uint64_t
     uint32_t mz = 0;
 #pragma unroll
     for (int b = 0; b < 5; ++b) mz |= ((cx >> b) & 1u) << (2 * b) | ((cy >> b) & 1u) << (2 * b + 1);
-    if (USE_BVH && RT_COV_BVH_DIRKEY) {
-      okey[li] = (uint16_t)((dy * 8 + dx) << 10 | mz);
-    } else {
-      const uint32_t rem = (uint32_t)min(max(p.B - 1 - k0, 0), 3);
-      okey[li] = (uint16_t)(rem << 14 | (dy * 8 + dx) << 8 | mz >> 2);
-    }
+    if (USE_BVH && RT_COV_BVH_DIRKEY) return (uint16_t)((dy * 8 + dx) << 10 | mz);
+    const uint32_t rem = (uint32_t)min(max(p.B - 1 - k0, 0), 3);
+    return (uint16_t)(rem << 14 | (dy * 8 + dx) << 8 | mz >> 2);
+  }
+}
+template <bool USE_BVH>
+__global__ __launch_bounds__(256) void k_replay_keys(CovParams p, const uint64_t* keys, const int64_t* list, int64_t nl,
+                                                     uint16_t* okey, int32_t* oval) {
+  for (int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; li < nl; li += (int64_t)gridDim.x * blockDim.x) {
+    okey[li] = replay_key<USE_BVH>(p, keys[list[li]]);
     oval[li] = (int32_t)li;
   }
+}
+
+// The replay order by windows (RT_REPLAY_WINDOW): list entries [w W, (w + 1) W), W = 1024 *
+// RT_REPLAY_WIN_ITEMS, sorted by replay_key inside the window by one 1024-thread block in LDS --
+// one launch instead of k_replay_keys and a device-wide radix sort (hipCUB: ~8 launches and fills,
+// ~100 us per K3 rank of 8, profiles/r3b_k3.timeline.txt).  A wave still gets lanes with the same
+// bounces left and nearby directions and cells, from its window instead of from the whole list.
+#ifndef RT_REPLAY_WINDOW
+#define RT_REPLAY_WINDOW 1
+#endif
+#ifndef RT_REPLAY_WIN_ITEMS
+#define RT_REPLAY_WIN_ITEMS 8
+#endif
+constexpr int kReplayWin = 1024 * RT_REPLAY_WIN_ITEMS;
+template <bool USE_BVH>
+__global__ __launch_bounds__(1024) void k_replay_order(CovParams p, const uint64_t* keys, const int64_t* list,
+                                                       int64_t nl, int32_t* order) {
+  using Sort = rocprim::block_radix_sort<uint16_t, 1024, RT_REPLAY_WIN_ITEMS, int32_t>;
+  __shared__ typename Sort::storage_type st;
+  const int64_t base = (int64_t)blockIdx.x * kReplayWin + (int64_t)threadIdx.x * RT_REPLAY_WIN_ITEMS;
+  uint16_t k[RT_REPLAY_WIN_ITEMS];
+  int32_t v[RT_REPLAY_WIN_ITEMS];
+#pragma unroll
+  for (int i = 0; i < RT_REPLAY_WIN_ITEMS; ++i) {
+    const int64_t li = base + i;
+    k[i] = li < nl ? replay_key<USE_BVH>(p, keys[list[li]]) : (uint16_t)0xFFFF;
+    v[i] = (int32_t)li;
+  }
+  Sort().sort(k, v, st);
+#pragma unroll
+  for (int i = 0; i < RT_REPLAY_WIN_ITEMS; ++i)
+    if (base + i < nl) order[base + i] = v[i];
 }
 
 template <bool USE_BVH, bool RX_FIRST>
@@ -2154,12 +2188,21 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
       uint16_t* k_out = (uint16_t*)((char*)ws + kbs);
       int32_t* v_in = (int32_t*)((char*)ws + 2 * kbs);
       int32_t* v_out = (int32_t*)((char*)ws + 2 * kbs + rbs);
-      if (bvh)
-        hipLaunchKernelGGL(k_replay_keys<true>, dim3(grid_l), dim3(256), 0, s, p, c->keys, c->list, nlist, k_in, v_in);
-      else
-        hipLaunchKernelGGL(k_replay_keys<false>, dim3(grid_l), dim3(256), 0, s, p, c->keys, c->list, nlist, k_in, v_in);
-      RT_HIP(hipcub::DeviceRadixSort::SortPairs((char*)ws + 2 * kbs + 2 * rbs, cub_bytes, k_in, k_out, v_in, v_out,
-                                                (int)nlist, 0, 16, s));
+      if (RT_REPLAY_WINDOW) {
+        const unsigned grid_w = (unsigned)((nlist + kReplayWin - 1) / kReplayWin);
+        if (bvh)
+          hipLaunchKernelGGL(k_replay_order<true>, dim3(grid_w), dim3(1024), 0, s, p, c->keys, c->list, nlist, v_out);
+        else
+          hipLaunchKernelGGL(k_replay_order<false>, dim3(grid_w), dim3(1024), 0, s, p, c->keys, c->list, nlist, v_out);
+      } else {
+        if (bvh)
+          hipLaunchKernelGGL(k_replay_keys<true>, dim3(grid_l), dim3(256), 0, s, p, c->keys, c->list, nlist, k_in, v_in);
+        else
+          hipLaunchKernelGGL(k_replay_keys<false>, dim3(grid_l), dim3(256), 0, s, p, c->keys, c->list, nlist, k_in,
+                             v_in);
+        RT_HIP(hipcub::DeviceRadixSort::SortPairs((char*)ws + 2 * kbs + 2 * rbs, cub_bytes, k_in, k_out, v_in, v_out,
+                                                  (int)nlist, 0, 16, s));
+      }
       prof_mark(c, 4, s);
       // BVH scenes: receiver first, the traversal culled at its t (K5 replay 3.47 -> 2.7 ms); the
       // LDS brute force tests every face anyway (a plane-culled variant measured 5% slower on K3,

@@ -856,7 +856,7 @@ const int32_t* dir_order_windows(int64_t ray_offset, int64_t n, hipStream_t stre
 // RT_XCD_WINDOWS: BVH bursts of at least 64 windows are traced window by window, each window on one
 // XCD (xcd_chunk); 0 keeps the device-wide direction sort
 #ifndef RT_XCD_WINDOWS
-#define RT_XCD_WINDOWS 1
+#define RT_XCD_WINDOWS 0  // measured: no less write traffic (1.02 GB either way), 5x the node fetches, K4 1347 -> 1441 us (profiles/r3c_*)
 #endif
 
 void trace_mark(int i, hipStream_t s);
