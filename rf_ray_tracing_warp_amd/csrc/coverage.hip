@@ -804,9 +804,18 @@ struct PathAcc {
 // Record key (compact): [owner | cell | bin] with the field widths of CovParams.  Sorting it groups
 // the records by destination rank, then (cell, bin); the bins are summed exactly (Fx192), so the
 // order of the records within a bin -- tracer.py:116 adds them in ray order -- cannot matter.
+// With several owners the cell field is the cell's index among its owner's cells,
+// (rest * nxo + ix / own_world) with nxo = ceil(nx / own_world): bits_for(ncell / world) instead of
+// bits_for(ncell), so a K3 rank's key is 30 bits (3 radix passes) instead of 33 (4).
 __device__ __forceinline__ uint64_t record_key(const CovParams& p, int64_t cell, int64_t bin) {
-  const uint64_t own = p.own_world > 1 ? (uint64_t)((cell % p.g.nx) % p.own_world) : 0ull;
-  return (own << p.cell_bits | (uint64_t)cell) << p.bin_bits | (uint64_t)bin;
+  uint64_t own = 0, lc = (uint64_t)cell;
+  if (p.own_world > 1) {
+    const int64_t ix = cell % p.g.nx, rest = cell / p.g.nx;
+    const int64_t nxo = (p.g.nx + p.own_world - 1) / p.own_world;
+    own = (uint64_t)(ix % p.own_world);
+    lc = (uint64_t)(rest * nxo + ix / p.own_world);
+  }
+  return (own << p.cell_bits | lc) << p.bin_bits | (uint64_t)bin;
 }
 
 // Does the receiver of `cell` win bounce k of ray r (kernel.py:85: hit, and the environment missed
@@ -1051,6 +1060,14 @@ __global__ __launch_bounds__(256) void k_replay_keys(CovParams p, const uint64_t
 #define RT_REPLAY_WIN_ITEMS 8
 #endif
 constexpr int kReplayWin = 1024 * RT_REPLAY_WIN_ITEMS;
+// Larger lists (one GPU's whole map: K3 7.9M, K5 6.4M first wins) keep the device-wide sort: there
+// the windows cost more replay coherence than the sort's launches (K5 map 4.73 -> 5.21 ms with
+// windows, K3 4.94 -> 5.13 ms; a K3 rank of 8: order 105 -> 36 us, replay 310 -> 319 us;
+// profiles/r3d_*).
+#ifndef RT_REPLAY_WINDOW_MAX
+#define RT_REPLAY_WINDOW_MAX (1 << 21)
+#endif
+constexpr int64_t kReplayWindowMax = RT_REPLAY_WINDOW_MAX;
 template <bool USE_BVH>
 __global__ __launch_bounds__(1024) void k_replay_order(CovParams p, const uint64_t* keys, const int64_t* list,
                                                        int64_t nl, int32_t* order) {
@@ -1091,11 +1108,16 @@ __global__ __launch_bounds__(256, RT_COV_REPLAY_WAVES) void k_replay(CovParams p
 // compact record key -> the (owner << own_shift | cell << 32 | bin) key of the reduced records
 struct WideKey {
   int ray_bits, bin_bits, cell_bits, own_shift;
+  int64_t nx, world;  // world > 1: the cell field is owner-local (record_key)
   __host__ __device__ __forceinline__ uint64_t operator()(uint64_t k) const {
     if (k == ~0ull) return ~0ull;
     const uint64_t bin = (k >> ray_bits) & ((1ull << bin_bits) - 1);
-    const uint64_t cell = (k >> (ray_bits + bin_bits)) & ((1ull << cell_bits) - 1);
+    uint64_t cell = (k >> (ray_bits + bin_bits)) & ((1ull << cell_bits) - 1);
     const uint64_t own = k >> (ray_bits + bin_bits + cell_bits);
+    if (world > 1) {
+      const uint64_t nxo = (uint64_t)((nx + world - 1) / world);
+      cell = (cell / nxo) * (uint64_t)nx + (cell % nxo) * (uint64_t)world + own;
+    }
     return own << own_shift | cell << 32 | bin;
   }
 };
@@ -1813,6 +1835,136 @@ __global__ __launch_bounds__(256) void k_long_final(const int32_t* starts, const
   }
 }
 
+// ---- Run sums in three launches (RT_RUN_SUMS_V2, default).  The sorted records are cut into
+// ntiles <= kMaxTiles tiles of T records (T a multiple of 64); a record is a run head when its key
+// differs from the previous record's.
+//   k_tile_heads  per tile: its number of heads
+//   k_tile_sums   one wave per tile: its first unique index (sum of the earlier tiles' heads), then
+//                 64-record chunks in order -- a segmented inclusive scan of the Fx192 values by head
+//                 flags, the open run's running sum carried from chunk to chunk.  Runs that end in
+//                 the tile are written (key, exact sum, f64); the part of the tile before its first
+//                 head (headpart) and the open run at its end (tailpart) are left for k_cross_tiles
+//   k_cross_tiles one wave per tile whose last run goes on into the next tile: tailpart + the
+//                 headparts of the following tiles up to the first one with a head
+// Integer sums throughout (Fx192), so the tiling cannot change a bit.  The round-2 form took 7
+// launches and three passes over the records (flags, scan, starts, ...; ~90 us on a K3 rank of 8,
+// profiles/r3b_k3_rank_timeline.txt).
+#ifndef RT_RUN_SUMS_V2
+#define RT_RUN_SUMS_V2 1
+#endif
+constexpr int64_t kMaxTiles = 2048;
+struct TileMeta {
+  int32_t* heads;   // [ntiles]
+  int64_t* tail_u;  // [ntiles] unique index of the run open at the tile's end, -1 if it ends there
+  Fx192* headpart;  // [ntiles] sum of the records before the tile's first head (whole tile if none)
+  Fx192* tailpart;  // [ntiles] sum of the open run's records in the tile
+};
+__device__ __forceinline__ Fx192 shfl_fx(const Fx192& x, int src) {
+  return Fx192{__shfl(x.w0, src, 64), __shfl(x.w1, src, 64), __shfl(x.w2, src, 64)};
+}
+__device__ __forceinline__ Fx192 shfl_up_fx(const Fx192& x, int o) {
+  return Fx192{__shfl_up(x.w0, o, 64), __shfl_up(x.w1, o, 64), __shfl_up(x.w2, o, 64)};
+}
+__global__ __launch_bounds__(256) void k_tile_heads(const uint64_t* keys, int64_t n, int64_t T, int32_t* heads) {
+  __shared__ int s4[4];
+  const int64_t lo = (int64_t)blockIdx.x * T, hi = lo + T < n ? lo + T : n;
+  int c = 0;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) c += (i == 0 || keys[i] != keys[i - 1]) ? 1 : 0;
+  c = block_sum(c, s4);
+  if (threadIdx.x == 0) heads[blockIdx.x] = c;
+}
+template <typename Val>
+__global__ __launch_bounds__(64) void k_tile_sums(const uint64_t* keys, Val val, int64_t n, int64_t T, int64_t ntiles,
+                                                  TileMeta tm, WideKey wk, uint64_t* ukeys, Fx192* usums,
+                                                  double* uamps, int64_t* nuniq) {
+  const int lane = threadIdx.x;
+  const int64_t t = blockIdx.x;
+  const int64_t lo = t * T, hi = lo + T < n ? lo + T : n;
+  int64_t base = 0;  // unique index of the tile's first head
+  for (int64_t j = lane; j < t; j += 64) base += tm.heads[j];
+  for (int o = 32; o >= 1; o >>= 1) base += __shfl_xor(base, o, 64);
+  if (t == ntiles - 1 && lane == 0) *nuniq = base + tm.heads[t];
+  const Fx192 zero{0, 0, 0};
+  const bool first_is_head = lo == 0 || keys[lo] != keys[lo - 1];
+  Fx192 carry = zero;     // running sum of the run open at the end of the previous chunk
+  bool carry_pre = !first_is_head;  // that run began before the tile
+  int64_t u = base - 1;   // unique index of the open run
+  for (int64_t c0 = lo; c0 < hi; c0 += 64) {
+    const int64_t i = c0 + lane;
+    const bool valid = i < hi;
+    const uint64_t k = valid ? keys[i] : 0;
+    const bool head = valid && (i == 0 || k != keys[i - 1]);
+    // the record after this one starts a new run (the tile's last record: left to the tile end)
+    const bool ends = valid && i + 1 < hi && keys[i + 1] != k;
+    Fx192 v = valid ? val(i) : zero;
+    // segmented inclusive scan: v = sum of this lane's run from its start in this chunk to here
+    bool f = head;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const Fx192 y = shfl_up_fx(v, o);
+      const bool fy = __shfl_up(f ? 1 : 0, o, 64) != 0;
+      if (lane >= o && !f) v = FxPlus()(v, y);
+      if (lane >= o) f = f || fy;
+    }
+    const uint64_t hb = __ballot(head);
+    const int fh = hb ? __builtin_ctzll(hb) : 64;  // first head lane of the chunk
+    if (lane < fh) v = FxPlus()(v, carry);         // lanes of the run carried into the chunk
+    const uint64_t below = lane ? (hb & (~0ull >> (64 - lane))) : 0ull;
+    const int64_t ul = u + __popcll(below) + (head ? 1 : 0);  // this lane's run
+    if (head) ukeys[ul] = wk(k);
+    if (ends) {
+      if (lane < fh && carry_pre) {
+        tm.headpart[t] = v;  // the run that began before the tile: its part in this tile
+      } else {
+        usums[ul] = v;
+        uamps[ul] = fx_to_double(v);
+      }
+    }
+    const int nvalid = (int)(hi - c0 < 64 ? hi - c0 : 64);
+    carry = shfl_fx(v, nvalid - 1);
+    if (hb) carry_pre = false;
+    u += __popcll(hb);
+  }
+  if (lane == 0) {  // the run open at the end of the tile
+    const bool goes_on = hi < n && keys[hi] == keys[hi - 1];
+    if (first_is_head) tm.headpart[t] = zero;  // nothing before the tile's first head
+    if (carry_pre) {  // no head in the tile: all of it belongs to a run that began earlier
+      tm.headpart[t] = carry;
+      tm.tail_u[t] = -1;
+    } else if (goes_on) {
+      tm.tailpart[t] = carry;
+      tm.tail_u[t] = u;
+    } else {
+      usums[u] = carry;
+      uamps[u] = fx_to_double(carry);
+      tm.tail_u[t] = -1;
+    }
+  }
+}
+__global__ __launch_bounds__(256) void k_cross_tiles(int64_t ntiles, TileMeta tm, Fx192* usums, double* uamps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t ta = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (ta >= ntiles) return;
+  const int64_t u = tm.tail_u[ta];
+  if (u < 0) return;  // wave-uniform
+  const Fx192 zero{0, 0, 0};
+  Fx192 acc = lane == 0 ? tm.tailpart[ta] : zero;
+  for (int64_t t0 = ta + 1; t0 < ntiles; t0 += 64) {
+    const int64_t t = t0 + lane;
+    const bool in = t < ntiles;
+    const bool has_head = in && tm.heads[t] > 0;
+    const uint64_t hb = __ballot(has_head);
+    const int stop = hb ? __builtin_ctzll(hb) : 64;  // the run ends in tile t0 + stop
+    if (in && lane <= stop) acc = FxPlus()(acc, tm.headpart[t]);
+    if (hb || t0 + 64 >= ntiles) break;
+  }
+  acc = wave_fx_sum(acc);
+  if (lane == 0) {
+    usums[u] = acc;
+    uamps[u] = fx_to_double(acc);
+  }
+}
+
 hipError_t scan_flags(void* tmp, size_t& bytes, const int32_t* flags, int32_t* scan, int64_t n, hipStream_t s) {
   return rocprim::inclusive_scan(tmp, bytes, flags, scan, (size_t)n, rocprim::plus<int32_t>(), s);
 }
@@ -2044,11 +2196,28 @@ KeyBits key_bits(const rt_coverage* c, int64_t n_bins) {
   KeyBits k;
   k.ray = 0;  // bins are summed exactly (Fx192), so the order within a bin needs no ray field
   k.bin = std::max(1, bits_for((uint64_t)(n_bins - 1)));
-  k.cell = std::max(1, bits_for((uint64_t)(cov_ncell(c) - 1)));
   k.own = c->ray_mode ? bits_for((uint64_t)(c->nshard - 1)) : 0;
+  const int64_t world = c->ray_mode ? c->nshard : 1;
+  const int64_t nown = (c->grid.nx + world - 1) / world * c->grid.ny * c->grid.nz;  // cells per owner (record_key)
+  k.cell = std::max(1, bits_for((uint64_t)(nown - 1)));
   return k;
 }
-WideKey wide_key(const rt_coverage* c, const KeyBits& k) { return WideKey{k.ray, k.bin, k.cell, own_shift(c)}; }
+// Sort end bit of the replay's records.  Dropped records carry ~0 and must sort after every valid
+// key: with end_bit = total they do whenever no valid key has all `total` bits set (an all-ones
+// bin, owner-local cell or owner field is out of range), which saves the extra bit -- and, at
+// 30 bits, a whole radix pass (K3).
+int record_sort_bits(const rt_coverage* c, const KeyBits& k, int64_t n_bins) {
+  const int64_t world = c->ray_mode ? c->nshard : 1;
+  const int64_t nown = (c->grid.nx + world - 1) / world * c->grid.ny * c->grid.nz;
+  const bool safe = ((1ll << k.bin) - 1 >= n_bins) || ((1ll << k.cell) - 1 >= nown) ||
+                    (k.own > 0 && (1ll << k.own) - 1 >= world);
+  return k.total() + (safe ? 0 : 1);
+}
+// the compact keys of the sort -> wide keys; `owner_local`: the cell field is record_key's
+// owner-local index (the trace stage of a ray-sharded plan), else a global cell id
+WideKey wide_key(const rt_coverage* c, const KeyBits& k, bool owner_local = true) {
+  return WideKey{k.ray, k.bin, k.cell, own_shift(c), c->grid.nx, owner_local && c->ray_mode ? (int64_t)c->nshard : 1};
+}
 
 // Stages 1-4 (trajectories, candidates, exact receiver tests, replay): the first-win records of
 // this plan's rays as (compact record key, amplitude) in c->okeys / c->oamps, in candidate order.
@@ -2188,7 +2357,7 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
       uint16_t* k_out = (uint16_t*)((char*)ws + kbs);
       int32_t* v_in = (int32_t*)((char*)ws + 2 * kbs);
       int32_t* v_out = (int32_t*)((char*)ws + 2 * kbs + rbs);
-      if (RT_REPLAY_WINDOW) {
+      if (RT_REPLAY_WINDOW && nlist <= kReplayWindowMax) {
         const unsigned grid_w = (unsigned)((nlist + kReplayWin - 1) / kReplayWin);
         if (bvh)
           hipLaunchKernelGGL(k_replay_order<true>, dim3(grid_w), dim3(1024), 0, s, p, c->keys, c->list, nlist, v_out);
@@ -2240,6 +2409,24 @@ int grow_for(rt_coverage* c, int64_t n) {
 // c->nuniq, then their f64 values into c->uamps
 template <typename Val>
 int run_sums(rt_coverage* c, Val val, int64_t n, WideKey wk, hipStream_t s) {
+  if (RT_RUN_SUMS_V2) {
+    const int64_t T = (n + 64 * kMaxTiles - 1) / (64 * kMaxTiles) * 64 > 1024
+                          ? (n + 64 * kMaxTiles - 1) / (64 * kMaxTiles) * 64
+                          : 1024;
+    const int64_t ntiles = (n + T - 1) / T;
+    TileMeta tm;
+    tm.heads = c->runs;
+    tm.tail_u = reinterpret_cast<int64_t*>(c->runs + 2 * kMaxTiles);
+    tm.headpart = reinterpret_cast<Fx192*>(c->tcos);  // free until k_terms
+    tm.tailpart = tm.headpart + kMaxTiles;
+    hipLaunchKernelGGL(k_tile_heads, dim3((unsigned)ntiles), dim3(256), 0, s, c->okeys_sorted, n, T, tm.heads);
+    hipLaunchKernelGGL(k_tile_sums<Val>, dim3((unsigned)ntiles), dim3(64), 0, s, c->okeys_sorted, val, n, T, ntiles, tm,
+                       wk, c->ukeys, plan_sums(c), c->uamps, c->nuniq);
+    hipLaunchKernelGGL(k_cross_tiles, dim3((unsigned)((ntiles + 3) / 4)), dim3(256), 0, s, ntiles, tm, plan_sums(c),
+                       c->uamps);
+    RT_HIP(hipGetLastError());
+    return RT_OK;
+  }
   int32_t* flags = c->runs;  // then the long-run id of every run
   int32_t* scan = c->runs + c->cap;
   int32_t* starts = c->runs + 2 * c->cap;
@@ -2418,7 +2605,7 @@ int rt_coverage_run(rt_coverage* c, const float* tx_pos, double tx_power, double
   prof_mark(c, 6, s);
   if (nlist > 0) {
     const KeyBits kb = key_bits(c, n_bins);
-    rc = cov_reduce(c, c->okeys, c->oamps, nlist, kb.total() + 1, wide_key(c, kb), s);
+    rc = cov_reduce(c, c->okeys, c->oamps, nlist, record_sort_bits(c, kb, n_bins), wide_key(c, kb), s);
     if (rc) return rc;
   } else {
     RT_HIP(hipMemsetAsync(c->nuniq, 0, 8, s));
@@ -2480,7 +2667,7 @@ int rt_coverage_trace_records(rt_coverage* c, const float* tx_pos, double tx_pow
   prof_mark(c, 6, s);
   if (nlist > 0) {
     const KeyBits kb = key_bits(c, n_bins);
-    rc = cov_reduce(c, c->okeys, c->oamps, nlist, kb.total() + 1, wide_key(c, kb), s);
+    rc = cov_reduce(c, c->okeys, c->oamps, nlist, record_sort_bits(c, kb, n_bins), wide_key(c, kb), s);
     if (rc) return rc;
     hipLaunchKernelGGL(k_owner_bounds, dim3((unsigned)std::min<int64_t>((nlist + 255) / 256, 4096)), dim3(256), 0, s,
                        c->ukeys, c->nuniq, world, own_shift(c), c->bounds);
@@ -2547,10 +2734,14 @@ int rt_coverage_power_records(rt_coverage* c, const uint64_t* keys, const uint64
     KeyBits kb = key_bits(c, n_bins);
     kb.ray = 0;
     kb.own = 0;
+    kb.cell = std::max(1, bits_for((uint64_t)(cov_ncell(c) - 1)));  // received keys carry global cells
     hipLaunchKernelGGL(k_compact_keys, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 8192)), dim3(256), 0, s, keys,
                        n, kb.bin, c->keys_sorted);
     RT_HIP(hipGetLastError());
-    rc = cov_reduce_sums(c, c->keys_sorted, (const Fx192*)sums, n, kb.total() + 1, wide_key(c, kb), s);
+    // received keys are valid ones (a ~0 key, never sent, would need the extra bit to sort last)
+    const bool safe = ((1ll << kb.bin) - 1 >= n_bins) || ((1ll << kb.cell) - 1 >= cov_ncell(c));
+    rc = cov_reduce_sums(c, c->keys_sorted, (const Fx192*)sums, n, kb.total() + (safe ? 0 : 1), wide_key(c, kb, false),
+                         s);
   } else {
     RT_HIP(hipMemsetAsync(c->nuniq, 0, 8, s));
   }
