@@ -1123,10 +1123,13 @@ struct WideKey {
 };
 
 // wide (cell << 32 | bin) keys received from other ranks -> compact [cell | bin] for the sort
-__global__ __launch_bounds__(256) void k_compact_keys(const uint64_t* in, int64_t n, int bin_bits, uint64_t* out) {
+// ... and the record indices the sort carries as its payload (one launch for both)
+__global__ __launch_bounds__(256) void k_compact_keys(const uint64_t* in, int64_t n, int bin_bits, uint64_t* out,
+                                                      int64_t* idx) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t k = in[i];
     out[i] = k == ~0ull ? ~0ull : ((k >> 32) << bin_bits | (k & 0xFFFFFFFFull));
+    idx[i] = i;
   }
 }
 
@@ -1301,32 +1304,76 @@ __global__ __launch_bounds__(256) void k_terms(const uint64_t* ukeys, const doub
 // one thread per cell of ours (x columns ix % nshard == shard); other cells are left to the
 // caller's zero fill, the power map being sum-reduced across ranks
 // [start, end) of every cell's run in the sorted unique keys (cells without keys keep 0, 0)
+// [start, end) of every cell's run in the sorted unique keys, stamped with the run's epoch: a
+// cell whose stamp is not this run's has no keys (so the arrays never need a fill).  Also resets
+// *nbig for k_power_small (stream order: it runs before).
 __global__ __launch_bounds__(256) void k_cell_ranges(const uint64_t* ukeys, const int64_t* nuniq, int64_t ncell,
-                                                     int32_t* cstart, int32_t* cend) {
+                                                     int32_t* cstart, int32_t* cend, int32_t* cepoch, int32_t epoch,
+                                                     unsigned* nbig) {
   const int64_t nu = *nuniq;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *nbig = 0u;
   for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < nu; u += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t c = ukeys[u] >> 32;
     if (c >= (uint64_t)ncell) continue;  // dropped records (~0) sort last
-    if (u == 0 || (ukeys[u - 1] >> 32) != c) cstart[c] = (int32_t)u;
+    if (u == 0 || (ukeys[u - 1] >> 32) != c) {
+      cstart[c] = (int32_t)u;
+      cepoch[c] = epoch;
+    }
     if (u == nu - 1 || (ukeys[u + 1] >> 32) != c) cend[c] = (int32_t)(u + 1);
   }
 }
 
 constexpr int kPowLds = 192;  // terms per wave staged in LDS (3 per lane); larger cells read global memory
-constexpr int kPowSmall = 16;  // cells with at most this many terms: one thread each (k_power_small)
+#ifndef RT_POW_SMALL
+#define RT_POW_SMALL 16
+#endif
+constexpr int kPowSmall = RT_POW_SMALL;  // cells with at most this many terms: one thread each (k_power_small)
+// RT_POW_SMALL_LDS: k_power_small first copies each thread's terms into its LDS column (independent
+// loads, one memory latency), then sweeps them there -- instead of a chain of dependent global
+// loads per interval (~37 us for a K3 rank's 8k cells, profiles/r3e_k3.timeline.txt)
+#ifndef RT_POW_SMALL_LDS
+#define RT_POW_SMALL_LDS 1
+#endif
+struct LdsTerms {  // a thread's terms k = lo .. lo + K - 1 at column `lane` of the block's arrays
+  const int32_t (*sm)[64];
+  const double (*sc)[64];
+  const double (*ss)[64];
+  const double (*sev)[4][64];
+  int64_t lo;
+  int lane;
+  __device__ __forceinline__ int64_t m(int64_t k) const { return sm[k - lo][lane]; }
+  __device__ __forceinline__ void cs(int64_t k, double& c, double& s) const {
+    c = sc[k - lo][lane];
+    s = ss[k - lo][lane];
+  }
+  __device__ __forceinline__ void start(int64_t k, double& s, double& c) const {
+    s = sev[k - lo][0][lane];
+    c = sev[k - lo][1][lane];
+  }
+  __device__ __forceinline__ void stop(int64_t k, double& s, double& c) const {
+    s = sev[k - lo][2][lane];
+    c = sev[k - lo][3][lane];
+  }
+};
 
 // cells of ours with 0..kPowSmall terms: one thread per cell, serial sweep (most cells of a large
 // map receive a handful of bins; a wave per such cell costs more than its whole sweep)
 // Larger cells are listed (big[], count in *nbig; one atomic per wave) for k_power, which then
 // visits only them (it used to stride over every cell of the map to skip the small ones: 1M cell
 // ranges read per K5 map for a few thousand large cells).
-__global__ __launch_bounds__(256) void k_power_small(TermArrays G, const int32_t* cstart, const int32_t* cend, rt_grid g,
-                                                     int shard, int nshard, PowerParams P, double* power, int32_t* big,
+__global__ __launch_bounds__(64) void k_power_small(TermArrays G, const int32_t* cstart, const int32_t* cend,
+                                                     const int32_t* cepoch, int32_t epoch, rt_grid g, int shard,
+                                                     int nshard, PowerParams P, double* power, int32_t* big,
                                                      unsigned* nbig) {
   const int64_t nxo = g.nx > shard ? (g.nx - shard + nshard - 1) / nshard : 0;
   const int64_t nown = nxo * g.ny * g.nz;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int lane = threadIdx.x & 63;
+  if (nshard > 1) {  // other ranks' cells: 0 (the map is sum-reduced), instead of a fill
+    const int64_t ncell = g.nx * g.ny * g.nz;
+    for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < ncell; c += stride)
+      if ((c % g.nx) % nshard != shard) power[c] = 0.0;
+  }
   for (int64_t base = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); base < nown; base += stride) {
     const int64_t t = base + lane;
     bool is_big = false;
@@ -1334,9 +1381,26 @@ __global__ __launch_bounds__(256) void k_power_small(TermArrays G, const int32_t
     if (t < nown) {
       const int64_t jx = t % nxo, rest = t / nxo;
       c = rest * g.nx + shard + jx * nshard;
-      const int64_t lo = cstart[c], hi = cend[c];
-      if (hi - lo <= kPowSmall) power[c] = power_sparse(lo, hi, P, G);  // NaN when empty
-      else is_big = true;
+      const bool has = cepoch[c] == epoch;
+      const int64_t lo = has ? cstart[c] : 0, hi = has ? cend[c] : 0;
+      if (hi - lo <= kPowSmall) {
+#if RT_POW_SMALL_LDS
+        __shared__ int32_t sm[kPowSmall][64];
+        __shared__ double sc[kPowSmall][64], ss[kPowSmall][64], sev[kPowSmall][4][64];
+        const int K = (int)(hi - lo);
+        for (int k = 0; k < K; ++k) {
+          sm[k][lane] = (int32_t)G.m(lo + k);
+          sc[k][lane] = G.tcos[lo + k];
+          ss[k][lane] = G.tsin[lo + k];
+          for (int r = 0; r < 4; ++r) sev[k][r][lane] = G.ev[4 * (lo + k) + r];
+        }
+        power[c] = power_sparse(lo, hi, P, LdsTerms{sm, sc, ss, sev, lo, lane});  // NaN when empty
+#else
+        power[c] = power_sparse(lo, hi, P, G);  // NaN when empty
+#endif
+      } else {
+        is_big = true;
+      }
     }
     const uint64_t m = __ballot(is_big);
     if (m) {
@@ -1570,6 +1634,8 @@ struct rt_coverage {
   double *tcos = nullptr, *tsin = nullptr;  // per unique (cell, bin): phase terms of the power sweep
   double* ev = nullptr;                      // per unique (cell, bin): sin/cos at its start and end sample
   int32_t *cstart = nullptr, *cend = nullptr;  // per cell: its run in the unique keys
+  int32_t* cepoch = nullptr;                   // per cell: the run (range_epoch) that wrote cstart/cend
+  int32_t range_epoch = 0;
   int32_t* bigcells = nullptr;  // per cell slot: the cells k_power sweeps (more than kPowSmall terms)
   int32_t* runs = nullptr;  // exact run sums: [cap] head flags, [cap] their scan, [cap] run starts, [64] counters
   uint8_t* win = nullptr;
@@ -1852,7 +1918,8 @@ __global__ __launch_bounds__(256) void k_long_final(const int32_t* starts, const
 #ifndef RT_RUN_SUMS_V2
 #define RT_RUN_SUMS_V2 1
 #endif
-constexpr int64_t kMaxTiles = 2048;
+constexpr int64_t kMaxTiles = 4096;  // each wave of k_tile_sums sums the earlier tiles' heads: <= 64 per lane
+constexpr int64_t kMinTile = 256;    // 4 chunks per wave: enough waves to fill the GPU on a rank's ~1M records
 struct TileMeta {
   int32_t* heads;   // [ntiles]
   int64_t* tail_u;  // [ntiles] unique index of the run open at the tile's end, -1 if it ends there
@@ -2106,7 +2173,7 @@ int poison_plan(rt_coverage* c, hipStream_t s) {
               {c->trx, (size_t)c->cap * 4}, {c->list, (size_t)c->cap * 8}, {c->items, (size_t)c->item_cap * 8},
               {c->tmp, c->tmp_bytes}, {c->rord, c->rord_bytes}, {c->counters, 32}, {c->nuniq, 8},
               {c->cstart, sizeof(int32_t) * (size_t)nc}, {c->cend, sizeof(int32_t) * (size_t)nc},
-              {c->bigcells, sizeof(int32_t) * (size_t)nc},
+              {c->bigcells, sizeof(int32_t) * (size_t)nc}, {c->cepoch, sizeof(int32_t) * (size_t)nc},
               {c->bounds, c->bounds ? sizeof(int64_t) * (size_t)(c->nshard + 1) : 0},
               {c->runs, ((size_t)c->cap * 3 + 64) * 4}};
   for (auto& q : bufs)
@@ -2181,10 +2248,15 @@ __global__ __launch_bounds__(256) void k_owner_bounds(const uint64_t* ukeys, con
   }
 }
 
-__global__ __launch_bounds__(256) void k_strip_owner(const uint64_t* ukeys, int64_t n, int shift, uint64_t* out) {
+// the reduced records of a ray-sharded plan into the caller's send buffers: keys without the owner
+// field, and the exact sums (one launch for both)
+__global__ __launch_bounds__(256) void k_strip_owner(const uint64_t* ukeys, const Fx192* usums, int64_t n, int shift,
+                                                     uint64_t* out, Fx192* sums_out) {
   const uint64_t mask = (1ull << shift) - 1;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     out[i] = ukeys[i] & mask;
+    sums_out[i] = usums[i];
+  }
 }
 
 // field widths of the compact record key [owner | cell | bin | ray]
@@ -2410,9 +2482,7 @@ int grow_for(rt_coverage* c, int64_t n) {
 template <typename Val>
 int run_sums(rt_coverage* c, Val val, int64_t n, WideKey wk, hipStream_t s) {
   if (RT_RUN_SUMS_V2) {
-    const int64_t T = (n + 64 * kMaxTiles - 1) / (64 * kMaxTiles) * 64 > 1024
-                          ? (n + 64 * kMaxTiles - 1) / (64 * kMaxTiles) * 64
-                          : 1024;
+    const int64_t T = std::max<int64_t>(kMinTile, (n + 64 * kMaxTiles - 1) / (64 * kMaxTiles) * 64);
     const int64_t ntiles = (n + T - 1) / T;
     TileMeta tm;
     tm.heads = c->runs;
@@ -2468,10 +2538,8 @@ int cov_reduce_sums(rt_coverage* c, const uint64_t* keys, const Fx192* sums, int
                     hipStream_t s) {
   int rc = grow_for(c, n);
   if (rc) return rc;
-  int64_t* idx = reinterpret_cast<int64_t*>(c->oamps);
+  int64_t* idx = reinterpret_cast<int64_t*>(c->oamps);  // filled by k_compact_keys
   int64_t* idx_sorted = reinterpret_cast<int64_t*>(c->oamps_sorted);
-  const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 8192);
-  hipLaunchKernelGGL(k_iota, dim3(g), dim3(256), 0, s, n, idx);
   size_t tb = c->tmp_bytes;
   RT_HIP(sort_records(c->tmp, tb, keys, c->okeys_sorted, (const int64_t*)idx, idx_sorted, n,
                       sort_bits < 64 ? sort_bits : 64, s));
@@ -2495,20 +2563,17 @@ int cov_power(rt_coverage* c, int64_t nrec, int64_t n_bins, double alpha, double
   // so a sharded map's few thousand cells must still spread over every CU
   const unsigned grid_small = (unsigned)std::min<int64_t>((ncell / c->nshard + 64) / 64, 16384);
   const TermArrays terms{c->ukeys, c->tcos, c->tsin, c->ev};
-  if (c->nshard > 1) RT_HIP(hipMemsetAsync(power, 0, ncell * sizeof(double), s));  // cells of other ranks
-  RT_HIP(hipMemsetAsync(c->cstart, 0, ncell * sizeof(int32_t), s));
-  RT_HIP(hipMemsetAsync(c->cend, 0, ncell * sizeof(int32_t), s));
-  if (nrec > 0) {
-    const unsigned grid_u = (unsigned)std::min<int64_t>((nrec + 255) / 256, 8192);
-    hipLaunchKernelGGL(k_terms, dim3(grid_u), dim3(256), 0, s, c->ukeys, c->uamps, c->nuniq, P, c->tcos, c->tsin, c->ev);
-    hipLaunchKernelGGL(k_cell_ranges, dim3(grid_u), dim3(256), 0, s, c->ukeys, c->nuniq, ncell, c->cstart, c->cend);
-  }
-  // cells with more than kPowSmall terms, listed by k_power_small for k_power
+  // cells with more than kPowSmall terms, listed by k_power_small for k_power (count reset by k_cell_ranges)
   int32_t* big = c->bigcells;
   unsigned* nbig = reinterpret_cast<unsigned*>(c->runs + 3 * c->cap + 1);
-  RT_HIP(hipMemsetAsync(nbig, 0, 4, s));
-  hipLaunchKernelGGL(k_power_small, dim3(grid_small), dim3(64), 0, s, terms, c->cstart, c->cend, c->grid, c->shard,
-                     c->nshard, P, power, big, nbig);
+  const int32_t epoch = ++c->range_epoch;  // cells not stamped with it have no keys (k_cell_ranges)
+  const unsigned grid_u = (unsigned)std::max<int64_t>(1, std::min<int64_t>((nrec + 255) / 256, 8192));
+  if (nrec > 0)
+    hipLaunchKernelGGL(k_terms, dim3(grid_u), dim3(256), 0, s, c->ukeys, c->uamps, c->nuniq, P, c->tcos, c->tsin, c->ev);
+  hipLaunchKernelGGL(k_cell_ranges, dim3(grid_u), dim3(256), 0, s, c->ukeys, c->nuniq, ncell, c->cstart, c->cend,
+                     c->cepoch, epoch, nbig);
+  hipLaunchKernelGGL(k_power_small, dim3(grid_small), dim3(64), 0, s, terms, c->cstart, c->cend, c->cepoch, epoch,
+                     c->grid, c->shard, c->nshard, P, power, big, nbig);
   if (nrec > 0)
     hipLaunchKernelGGL(k_power, dim3(grid_cells), dim3(256), 0, s, terms, c->cstart, c->cend, big, nbig, P, power);
   RT_HIP(hipGetLastError());
@@ -2552,6 +2617,8 @@ int rt_coverage_create(int device, const rt_mesh* env, int max_bounces, int64_t 
   if (e == hipSuccess) e = hipMalloc(&c->cstart, sizeof(int32_t) * nc);
   if (e == hipSuccess) e = hipMalloc(&c->cend, sizeof(int32_t) * nc);
   if (e == hipSuccess) e = hipMalloc(&c->bigcells, sizeof(int32_t) * nc);
+  if (e == hipSuccess) e = hipMalloc(&c->cepoch, sizeof(int32_t) * nc);
+  if (e == hipSuccess) e = hipMemset(c->cepoch, 0, sizeof(int32_t) * nc);  // epochs start at 1
   if (e != hipSuccess) {
     rt_coverage_destroy(c);
     return rt::hip_fail(e, "rt_coverage_create");
@@ -2577,6 +2644,7 @@ int rt_coverage_destroy(rt_coverage* c) {
   if (c->cstart) (void)hipFree(c->cstart);
   if (c->cend) (void)hipFree(c->cend);
   if (c->bigcells) (void)hipFree(c->bigcells);
+  if (c->cepoch) (void)hipFree(c->cepoch);
   if (c->items) (void)hipFree(c->items);
   if (c->bounds) (void)hipFree(c->bounds);
   if (c->work) (void)hipFree(c->work);
@@ -2695,9 +2763,8 @@ int rt_coverage_records(rt_coverage* c, uint64_t* keys_out, uint64_t* sums_out, 
   rt::DeviceGuard dg(c->device);
   RT_HIP(dg.err);
   hipLaunchKernelGGL(k_strip_owner, dim3((unsigned)std::min<int64_t>((c->n_out + 255) / 256, 4096)), dim3(256), 0, s,
-                     c->ukeys, c->n_out, own_shift(c), keys_out);
+                     c->ukeys, plan_sums(c), c->n_out, own_shift(c), keys_out, (Fx192*)sums_out);
   RT_HIP(hipGetLastError());
-  RT_HIP(hipMemcpyAsync(sums_out, plan_sums(c), sizeof(Fx192) * c->n_out, hipMemcpyDeviceToDevice, s));
   return RT_OK;
 }
 
@@ -2736,7 +2803,7 @@ int rt_coverage_power_records(rt_coverage* c, const uint64_t* keys, const uint64
     kb.own = 0;
     kb.cell = std::max(1, bits_for((uint64_t)(cov_ncell(c) - 1)));  // received keys carry global cells
     hipLaunchKernelGGL(k_compact_keys, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 8192)), dim3(256), 0, s, keys,
-                       n, kb.bin, c->keys_sorted);
+                       n, kb.bin, c->keys_sorted, reinterpret_cast<int64_t*>(c->oamps));
     RT_HIP(hipGetLastError());
     // received keys are valid ones (a ~0 key, never sent, would need the extra bit to sort last)
     const bool safe = ((1ll << kb.bin) - 1 >= n_bins) || ((1ll << kb.cell) - 1 >= cov_ncell(c));
