@@ -147,6 +147,42 @@ __device__ __forceinline__ void store_row_fixed(float* dst, const float (*pts)[3
   }
 }
 
+// RT_ROW_PERMUTE (K2's 48-B rows, P = 4): the wave's 64 rows are one contiguous 3,072-B block, but
+// each lane storing its own row writes 16-B pieces at a 48-B stride, so every store instruction
+// touches all 24 lines of the block (WRITE_SIZE 111.7 MB per 100 MB of rows, r2zm).  Here the rows
+// are transposed across the wave with ds_bpermute (no LDS allocation) so that store j writes bytes
+// [1024 j, 1024 (j + 1)) of the block: lane L stores 16-B piece q = 64 j + L, which is part q % 3
+// of row q / 3.  Only for full waves of consecutive rows (every lane valid, no row order).
+#ifndef RT_ROW_PERMUTE
+#define RT_ROW_PERMUTE 0
+#endif
+__device__ __forceinline__ float bperm_f(float v, int src_lane) {
+  return __int_as_float(__builtin_amdgcn_ds_bpermute(src_lane << 2, __float_as_int(v)));
+}
+__device__ __forceinline__ void store_rows_wave4(float* wave_dst, const float (*pts)[3]) {
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  const int lane = threadIdx.x & 63;
+  float f[12];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) f[i] = pts[i / 3][i % 3];
+  f4v* d4 = reinterpret_cast<f4v*>(wave_dst);
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int q = 64 * j + lane, r = q / 3, part = q - 3 * r;
+    f4v v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float a0 = bperm_f(f[e], r), a1 = bperm_f(f[4 + e], r), a2 = bperm_f(f[8 + e], r);
+      v[e] = part == 0 ? a0 : (part == 1 ? a1 : a2);
+    }
+#if RT_NT_ROWS
+    __builtin_nontemporal_store(v, d4 + q);
+#else
+    d4[q] = v;
+#endif
+  }
+}
+
 __device__ __forceinline__ void store_row(float* dst, const float (*pts)[3], int P) {
   // rows are 12*P bytes; use 16-byte stores whenever the row start allows it
   for (int i = 0; i < P; ++i) {
@@ -441,7 +477,16 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
       if (a.hit_kind) a.hit_kind[row * B + b] = kind;
       if (a.hit_face) a.hit_face[row * B + b] = face;
     }
-    if (a.traced) store_row_fixed<P>(a.traced + row * (P * 3), path);
+    // a full wave of consecutive rows (brute force, no row order): transposed 1-KB stores
+    const bool wave_rows = RT_ROW_PERMUTE && P == 4 && !a.order && chunk * 256 + (threadIdx.x | 63) < a.n;
+    if (a.traced) {
+      if constexpr (P == 4) {
+        if (wave_rows) store_rows_wave4(a.traced + (row - (threadIdx.x & 63)) * (P * 3), path);
+        else store_row_fixed<P>(a.traced + row * (P * 3), path);
+      } else {
+        store_row_fixed<P>(a.traced + row * (P * 3), path);
+      }
+    }
     if (a.received) {
       float rec[P][3];
 #pragma unroll
@@ -451,7 +496,12 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
         rec[i][1] = keep ? path[i][1] : qnan;
         rec[i][2] = keep ? path[i][2] : qnan;
       }
-      store_row_fixed<P>(a.received + row * (P * 3), rec);
+      if constexpr (P == 4) {
+        if (wave_rows) store_rows_wave4(a.received + (row - (threadIdx.x & 63)) * (P * 3), rec);
+        else store_row_fixed<P>(a.received + row * (P * 3), rec);
+      } else {
+        store_row_fixed<P>(a.received + row * (P * 3), rec);
+      }
     }
     if (a.mask) {
 #if RT_NT_ROWS
