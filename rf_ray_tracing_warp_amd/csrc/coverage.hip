@@ -1332,7 +1332,7 @@ constexpr int kPowSmall = RT_POW_SMALL;  // cells with at most this many terms: 
 // loads, one memory latency), then sweeps them there -- instead of a chain of dependent global
 // loads per interval (~37 us for a K3 rank's 8k cells, profiles/r3e_k3.timeline.txt)
 #ifndef RT_POW_SMALL_LDS
-#define RT_POW_SMALL_LDS 1
+#define RT_POW_SMALL_LDS 0  // measured: K3 rank 37 -> 33 us, but K5 rank 42 -> 65 us (53 KB of LDS: 3 waves per CU), r3f
 #endif
 struct LdsTerms {  // a thread's terms k = lo .. lo + K - 1 at column `lane` of the block's arrays
   const int32_t (*sm)[64];

@@ -106,6 +106,13 @@ __device__ __forceinline__ bool rx_maybe(const TraceArgs& a, float3 o, float3 d,
 #ifndef RT_ROW_X2
 #define RT_ROW_X2 0  // 8-byte stores for rows of P = 2, 6 points (A/B builds)
 #endif
+// RT_XCD_WINDOWS: BVH bursts of at least 64 windows are traced window by window, each window on one
+// XCD (xcd_chunk); 0 keeps the device-wide direction sort.  Measured: no less write traffic (1.02
+// GB per K4 launch either way), 5x the node fetches, K4 1347 -> 1441 us (profiles/r3c_*).  Off, and
+// compiled out of the trace loop (its index arithmetic cost the K2 kernel 10 more spilled VGPRs).
+#ifndef RT_XCD_WINDOWS
+#define RT_XCD_WINDOWS 0
+#endif
 template <int P>
 __device__ __forceinline__ void store_row_fixed(float* dst, const float (*pts)[3]) {
   if constexpr ((P * 3) % 4 == 0) {  // 16-B aligned rows (P = 4, 8): 16-byte stores
@@ -413,10 +420,14 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
   const float qnan = __builtin_nanf("");
   // block-uniform loop over 256-row chunks (the same rows per thread as a grid-stride loop), so a
   // wave can list its part of a chunk's received rows for rt_trace_cir
+#if RT_XCD_WINDOWS
   const int64_t nchunks = (a.n + 255) / 256;
   for (int64_t it = 0;; ++it) {
     const int64_t chunk = a.win_chunks > 0 ? xcd_chunk(a.win_chunks, nchunks, it) : blockIdx.x + it * gridDim.x;
     if (chunk < 0 || chunk >= nchunks) break;
+#else
+  for (int64_t chunk = blockIdx.x; chunk * 256 < a.n; chunk += gridDim.x) {
+#endif
     const int64_t irow = chunk * 256 + threadIdx.x;
     bool got = false;
     if (irow < a.n) {
@@ -903,11 +914,6 @@ const int32_t* dir_order_windows(int64_t ray_offset, int64_t n, hipStream_t stre
   return (const int32_t*)*ws;
 }
 
-// RT_XCD_WINDOWS: BVH bursts of at least 64 windows are traced window by window, each window on one
-// XCD (xcd_chunk); 0 keeps the device-wide direction sort
-#ifndef RT_XCD_WINDOWS
-#define RT_XCD_WINDOWS 0  // measured: no less write traffic (1.02 GB either way), 5x the node fetches, K4 1347 -> 1441 us (profiles/r3c_*)
-#endif
 
 void trace_mark(int i, hipStream_t s);
 void trace_events(hipEvent_t* e0, hipEvent_t* e1);
