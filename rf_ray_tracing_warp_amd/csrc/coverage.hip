@@ -84,8 +84,19 @@ __device__ __forceinline__ float4 traj_d(const CovParams& p, int64_t r, int k) {
 
 __device__ __forceinline__ int64_t ncells(const rt_grid& g) { return g.nx * g.ny * g.nz; }
 
+// cell -> (i, j, k) in 32-bit unsigned arithmetic (cells < 2^32, rt_coverage_create): a 64-bit
+// division by a run-time divisor is a ~100-instruction sequence on the GPU, and the receiver tests
+// of k_win and k_replay take the cell's centre on every query
+__device__ __forceinline__ void cell_ijk(const rt_grid& g, int64_t cell, uint32_t& i, uint32_t& j, uint32_t& k) {
+  const uint32_t c = (uint32_t)cell, nx = (uint32_t)g.nx, ny = (uint32_t)g.ny;
+  const uint32_t q = c / nx;
+  i = c - q * nx;
+  k = q / ny;
+  j = q - k * ny;
+}
 __device__ __forceinline__ void cell_center(const rt_grid& g, int64_t cell, double c[3]) {
-  const int64_t i = cell % g.nx, j = (cell / g.nx) % g.ny, k = cell / (g.nx * g.ny);
+  uint32_t i, j, k;
+  cell_ijk(g, cell, i, j, k);
   c[0] = g.x0 + (double)i * g.dx;
   c[1] = g.y0 + (double)j * g.dy;
   c[2] = g.z0 + (double)k * g.dz;
@@ -810,10 +821,10 @@ struct PathAcc {
 __device__ __forceinline__ uint64_t record_key(const CovParams& p, int64_t cell, int64_t bin) {
   uint64_t own = 0, lc = (uint64_t)cell;
   if (p.own_world > 1) {
-    const int64_t ix = cell % p.g.nx, rest = cell / p.g.nx;
-    const int64_t nxo = (p.g.nx + p.own_world - 1) / p.own_world;
-    own = (uint64_t)(ix % p.own_world);
-    lc = (uint64_t)(rest * nxo + ix / p.own_world);
+    const uint32_t nx = (uint32_t)p.g.nx, w = (uint32_t)p.own_world, c = (uint32_t)cell;
+    const uint32_t rest = c / nx, ix = c - rest * nx, nxo = (nx + w - 1) / w, iq = ix / w;
+    own = (uint64_t)(ix - iq * w);
+    lc = (uint64_t)rest * nxo + iq;
   }
   return (own << p.cell_bits | lc) << p.bin_bits | (uint64_t)bin;
 }
@@ -1029,8 +1040,9 @@ __device__ __forceinline__ uint16_t replay_key(const CovParams& p, uint64_t key)
     }
     const uint32_t dx = (uint32_t)fminf(fmaxf((x + 1.0f) * 4.0f, 0.0f), 7.0f);
     const uint32_t dy = (uint32_t)fminf(fmaxf((y + 1.0f) * 4.0f, 0.0f), 7.0f);
-    const int64_t ix = cell % p.g.nx, iy = (cell / p.g.nx) % p.g.ny;
-    const uint32_t cx = (uint32_t)(ix * 32 / p.g.nx), cy = (uint32_t)(iy * 32 / p.g.ny);
+    uint32_t ix, iy, iz;
+    cell_ijk(p.g, cell, ix, iy, iz);
+    const uint32_t cx = (uint32_t)((uint64_t)ix * 32 / (uint64_t)p.g.nx), cy = (uint32_t)((uint64_t)iy * 32 / (uint64_t)p.g.ny);
     uint32_t mz = 0;
 #pragma unroll
     for (int b = 0; b < 5; ++b) mz |= ((cx >> b) & 1u) << (2 * b) | ((cy >> b) & 1u) << (2 * b + 1);
