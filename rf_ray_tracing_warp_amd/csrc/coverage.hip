@@ -446,7 +446,10 @@ __global__ __launch_bounds__(256, RT_COV_TRAJ_WAVES) void k_traj(CovParams p) {
     for (int k = 0; k < p.B; ++k) {
       const rt::Shear s = rt::make_shear(pos, dir);
       const rt::Hit he = env_query<USE_BVH>(p, lds_tab, s, pos, dir);
-      float4* tp = p.traj + 2 * (r * p.B + k);
+      // stored at slot ir, the processing position: the ray's identity downstream is its slot (only
+      // the initial direction needs the global id), so a direction-sorted burst writes its
+      // trajectories contiguously instead of scattering 32-B pieces over the array
+      float4* tp = p.traj + 2 * (ir * p.B + k);
       tp[0] = make_float4(pos.x, pos.y, pos.z, he.face < 0 ? INFINITY : he.t);
       tp[1] = make_float4(dir.x, dir.y, dir.z, 0.0f);
       nseg = k + 1;
@@ -461,7 +464,7 @@ __global__ __launch_bounds__(256, RT_COV_TRAJ_WAVES) void k_traj(CovParams p) {
       dir.y = fmaf(-sc, n.y, dir.y);
       dir.z = fmaf(-sc, n.z, dir.z);
     }
-    p.nseg[r] = (uint8_t)nseg;
+    p.nseg[ir] = (uint8_t)nseg;
   }
 }
 
@@ -506,7 +509,7 @@ __global__ __launch_bounds__(256, RT_COV_TRAJ_WAVES) void k_traj_split(CovParams
       const rt::Hit he = rt::group_hit<G>(w.h);
       if (!alive) continue;
       if (j == 0) {
-        float4* tp = p.traj + 2 * (r * p.B + k);
+        float4* tp = p.traj + 2 * (ir * p.B + k);  // slot ir, as k_traj
         tp[0] = make_float4(pos.x, pos.y, pos.z, he.face < 0 ? INFINITY : he.t);
         tp[1] = make_float4(dir.x, dir.y, dir.z, 0.0f);
       }
@@ -525,7 +528,7 @@ __global__ __launch_bounds__(256, RT_COV_TRAJ_WAVES) void k_traj_split(CovParams
       dir.y = fmaf(-sc, n.y, dir.y);
       dir.z = fmaf(-sc, n.z, dir.z);
     }
-    if (valid && j == 0) p.nseg[r] = (uint8_t)nseg;
+    if (valid && j == 0) p.nseg[ir] = (uint8_t)nseg;
   }
 }
 
@@ -811,6 +814,46 @@ struct PathAcc {
   }
 };
 
+// PathAcc with the previous point and segment (6 floats, read and written once per path vertex)
+// in the thread's LDS column instead of registers (RT_REPLAY_ACC_LDS): the replay's bounce loop
+// keeps its queries' state in registers and spilled ~17 VGPRs to scratch (r3a_kernel_resources).
+// Same operations on the same values, so the same bits.
+#ifndef RT_REPLAY_ACC_LDS
+#define RT_REPLAY_ACC_LDS 0
+#endif
+struct PathAccL {
+  float* col;  // [6][256]: prev xyz, seg xyz at col[256 * i]
+  int npts;
+  float dist;
+  double amp;
+  __device__ __forceinline__ void start(float x, float y, float z, double amp0) {
+    col[0] = x;
+    col[256] = y;
+    col[512] = z;
+    npts = 1;
+    dist = 0.0f;
+    amp = amp0;
+  }
+  __device__ __forceinline__ void add(float x, float y, float z) {
+    const float prev[3] = {col[0], col[256], col[512]};
+    const float s2[3] = {x - prev[0], y - prev[1], z - prev[2]};
+    if (npts >= 2) {
+      const float seg[3] = {col[768], col[1024], col[1280]};
+      const float l1 = sqrtf(npdot(seg, seg));
+      const float cosv = npdot(seg, s2) / (l1 * sqrtf(npdot(s2, s2)));
+      amp *= bounce_amp((float)acos((double)cosv));
+    }
+    dist += sqrtf(npdot(s2, s2));
+    col[768] = s2[0];
+    col[1024] = s2[1];
+    col[1280] = s2[2];
+    col[0] = x;
+    col[256] = y;
+    col[512] = z;
+    ++npts;
+  }
+};
+
 // ------------------------------------------------------------------ 3-4. receiver test, first win, replay
 // Record key (compact): [owner | cell | bin] with the field widths of CovParams.  Sorting it groups
 // the records by destination rank, then (cell, bin); the bins are summed exactly (Fx192), so the
@@ -851,7 +894,13 @@ __device__ __forceinline__ bool rx_wins(const CovParams& p, const RxLds& L, int6
 template <bool USE_BVH, bool RX_FIRST>
 __device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab, const RxLds& L, int64_t cell,
                                        int64_t r, int k0, float tr, uint64_t& okey, double& oamp) {
+#if RT_REPLAY_ACC_LDS
+  __shared__ float acc_lds[6 * 256];
+  PathAccL acc;
+  acc.col = acc_lds + threadIdx.x;
+#else
   PathAcc acc;
+#endif
   const float4 t0 = traj_p(p, r, 0);
   acc.start(t0.x, t0.y, t0.z, p.amp0);  // p_0 = tx
   for (int q = 1; q <= k0; ++q) {       // environment prefix p_1 .. p_k0
@@ -1113,7 +1162,10 @@ __global__ __launch_bounds__(256, RT_COV_REPLAY_WAVES) void k_replay(CovParams p
     const int64_t i = list[li];
     const uint64_t key = keys[i];
     const int64_t cell = (int64_t)(key >> 28), r = (int64_t)((key >> 4) & 0xFFFFFF);
-    replay<USE_BVH, RX_FIRST>(p, lds_tab, L, cell, r, (int)(key & 15), trx[i], out_key[li], out_amp[li]);
+    // records at the processing position jl: their order is irrelevant (they are sorted by key
+    // and summed exactly), and consecutive lanes then write consecutive 8-B words instead of
+    // scattering them (K3 k_replay wrote 445 MB for 126 MB of records, r2zm)
+    replay<USE_BVH, RX_FIRST>(p, lds_tab, L, cell, r, (int)(key & 15), trx[i], out_key[jl], out_amp[jl]);
   }
 }
 
