@@ -135,7 +135,8 @@ int rt_coverage_run(rt_coverage* cov, const float* tx_pos, double tx_power, doub
  *   2. rt_coverage_trace_records -> counts[world]      (records for each destination rank; syncs)
  *   3. rt_coverage_records -> caller device buffers    (grouped by destination, rank 0 first)
  *   4. all-to-all of the records (the caller's collective: RCCL via torch.distributed)
- *   5. rt_coverage_power_records on the received records, concatenated in source-rank order
+ *   5. rt_coverage_power_segments on the received records, concatenated in source-rank order
+ *      (or rt_coverage_power_records for records in any order)
  *   6. sum-reduce of the power maps (other ranks' cells are 0 here). */
 int rt_coverage_create_rays(int device, const rt_mesh* env, int max_bounces, int64_t n_rays_total, int64_t ray_offset,
                             int64_t n_rays, const rt_grid* grid, double rx_radius, int rank, int world,
@@ -148,6 +149,11 @@ int rt_coverage_records(rt_coverage* cov, uint64_t* keys_out, uint64_t* sums_out
 /* keys (cell << 32 | bin) and sums (3 uint64 per record) received from every rank, in any order. */
 int rt_coverage_power_records(rt_coverage* cov, const uint64_t* keys, const uint64_t* sums, int64_t n, int64_t n_bins,
                               double alpha, double* power, void* stream);
+/* rt_coverage_power_records for records that arrive as nseg (<= 64) segments of seg_counts[t]
+ * records (host array), segment t from rank t, each in rt_coverage_records' order (ascending keys,
+ * no repeated key): the segments are merged by rank instead of sorted (one launch). */
+int rt_coverage_power_segments(rt_coverage* cov, const uint64_t* keys, const uint64_t* sums, const int64_t* seg_counts,
+                               int nseg, int64_t n_bins, double alpha, double* power, void* stream);
 /* f64 amplitudes (finite, >= 0, below 2^56) -> the exact fixed-point sums of rt_coverage_records
  * (truncated below 2^-136), on the device. */
 int rt_coverage_amps_to_sums(const double* amps, int64_t n, uint64_t* sums, void* stream);

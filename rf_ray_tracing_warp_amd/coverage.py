@@ -172,17 +172,28 @@ class Coverage:
               "rt_coverage_records")
         return keys[:n], sums[:n], [int(c) for c in counts]
 
-    def power_from_records(self, keys, sums):
+    def power_from_records(self, keys, sums, counts=None):
         """Ray mode, last stage: the power of this rank's cells from the records every rank sent it
-        (keys and (n, 3) fixed-point sums, any order); the (num_cells,) float64 device map, 0
-        elsewhere."""
+        (keys and (n, 3) fixed-point sums); the (num_cells,) float64 device map, 0 elsewhere.
+        counts: the number of records from each source rank, when they arrive as consecutive
+        segments in trace_records' order (ascending keys per segment, as exchange_records delivers
+        them): the segments are merged by rank (rt_coverage_power_segments).  Without counts the
+        records may come in any order and are sorted (rt_coverage_power_records)."""
         n = int(keys.numel())
         if n and tuple(sums.shape) != (n, 3):
             raise ValueError(f"sums must be (n, 3) int64 fixed point, got {tuple(sums.shape)}")
+        alpha = phase_step(self.sample_window_s, self.n_bins)
+        s = _lib.stream_handle(self.device)
+        if counts is not None:
+            c = np.ascontiguousarray(np.asarray(counts, dtype=np.int64))
+            if int(c.sum()) != n or (c < 0).any():
+                raise ValueError(f"segment counts {c.tolist()} do not add up to the {n} records")
+            check(lib().rt_coverage_power_segments(self._h, ptr(keys) if n else None, ptr(sums) if n else None,
+                                                   c.ctypes.data, len(c), self.n_bins, alpha, ptr(self.power), s),
+                  "rt_coverage_power_segments")
+            return self.power
         check(lib().rt_coverage_power_records(self._h, ptr(keys) if n else None, ptr(sums) if n else None, n,
-                                              self.n_bins, phase_step(self.sample_window_s, self.n_bins),
-                                              ptr(self.power), _lib.stream_handle(self.device)),
-              "rt_coverage_power_records")
+                                              self.n_bins, alpha, ptr(self.power), s), "rt_coverage_power_records")
         return self.power
 
     def power_from_amplitudes(self, keys, amps):
@@ -201,8 +212,8 @@ class Coverage:
         if self.shard_mode == "rays":
             keys, sums, counts = self.trace_records(tx_pos, tx_power)
             if self.shard_count > 1:
-                keys, sums = rdist.exchange_records(keys, sums, counts, process_group)
-            return self.power_from_records(keys, sums)
+                keys, sums, counts = rdist.exchange_records(keys, sums, counts, process_group, return_counts=True)
+            return self.power_from_records(keys, sums, counts)
         tx = np.ascontiguousarray(np.asarray(tx_pos, dtype=np.float64).astype(np.float32))
         stats = np.zeros(2, np.int64)
         check(lib().rt_coverage_run(self._h, tx.ctypes.data, float(tx_power), float(self.light_speed_mps),

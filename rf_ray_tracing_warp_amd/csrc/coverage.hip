@@ -1173,8 +1173,9 @@ __global__ __launch_bounds__(256, RT_COV_REPLAY_WAVES) void k_replay(CovParams p
 struct WideKey {
   int ray_bits, bin_bits, cell_bits, own_shift;
   int64_t nx, world;  // world > 1: the cell field is owner-local (record_key)
+  bool identity = false;  // the keys are wide already (merged received segments)
   __host__ __device__ __forceinline__ uint64_t operator()(uint64_t k) const {
-    if (k == ~0ull) return ~0ull;
+    if (k == ~0ull || identity) return k;
     const uint64_t bin = (k >> ray_bits) & ((1ull << bin_bits) - 1);
     uint64_t cell = (k >> (ray_bits + bin_bits)) & ((1ull << cell_bits) - 1);
     const uint64_t own = k >> (ray_bits + bin_bits + cell_bits);
@@ -1194,6 +1195,41 @@ __global__ __launch_bounds__(256) void k_compact_keys(const uint64_t* in, int64_
     const uint64_t k = in[i];
     out[i] = k == ~0ull ? ~0ull : ((k >> 32) << bin_bits | (k & 0xFFFFFFFFull));
     idx[i] = i;
+  }
+}
+
+// The owner stage's records arrive as nseg segments (one per source rank), each sorted by its wide
+// key (rt_coverage_records' order).  Their stable merge by (key, segment) needs no sort: the merged
+// position of element i of segment s is its index in s plus, over every other segment, the number
+// of elements with a smaller key (a larger-or-equal one for the segments before s) -- nseg - 1
+// binary searches over L2-resident keys.  One launch instead of a record sort (rocPRIM's merge sort,
+// 9 launches, ~77 us for a K3 rank's 200k records).
+constexpr int kMaxSegs = 64;
+struct SegOffsets {
+  int64_t off[kMaxSegs + 1];
+  int nseg;
+};
+__global__ __launch_bounds__(256) void k_merge_segments(const uint64_t* keys, SegOffsets so, uint64_t* keys_out,
+                                                        int64_t* idx_out) {
+  const int64_t n = so.off[so.nseg];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int sg = 0;
+    while (sg + 1 < so.nseg && so.off[sg + 1] <= i) ++sg;
+    const uint64_t k = keys[i];
+    int64_t pos = i - so.off[sg];
+    for (int t = 0; t < so.nseg; ++t) {
+      if (t == sg) continue;
+      int64_t a = so.off[t], b = so.off[t + 1];  // first element > k (t < sg) or >= k (t > sg)
+      while (a < b) {
+        const int64_t m = (a + b) >> 1;
+        const uint64_t km = keys[m];
+        if (km < k || (t < sg && km == k)) a = m + 1;
+        else b = m;
+      }
+      pos += a - so.off[t];
+    }
+    keys_out[pos] = k;
+    idx_out[pos] = i;
   }
 }
 
@@ -2873,6 +2909,51 @@ int rt_coverage_power_records(rt_coverage* c, const uint64_t* keys, const uint64
     const bool safe = ((1ll << kb.bin) - 1 >= n_bins) || ((1ll << kb.cell) - 1 >= cov_ncell(c));
     rc = cov_reduce_sums(c, c->keys_sorted, (const Fx192*)sums, n, kb.total() + (safe ? 0 : 1), wide_key(c, kb, false),
                          s);
+  } else {
+    RT_HIP(hipMemsetAsync(c->nuniq, 0, 8, s));
+  }
+  if (!rc) rc = cov_power(c, n, n_bins, alpha, power, s);
+  if (!rc) prof_mark(c, 7, s);
+  return rc;
+}
+
+int rt_coverage_power_segments(rt_coverage* c, const uint64_t* keys, const uint64_t* sums, const int64_t* seg_counts,
+                               int nseg, int64_t n_bins, double alpha, double* power, void* stream) {
+  if (!c || !c->ray_mode || nseg < 1 || nseg > kMaxSegs || !seg_counts || !power || n_bins < 1 ||
+      n_bins >= ((int64_t)1 << 32)) {
+    rt::set_error("rt_coverage_power_segments: invalid arguments (1 <= nseg <= 64)");
+    return RT_EINVAL;
+  }
+  SegOffsets so{};
+  so.nseg = nseg;
+  for (int t = 0; t < nseg; ++t) {
+    if (seg_counts[t] < 0) {
+      rt::set_error("rt_coverage_power_segments: negative segment count");
+      return RT_EINVAL;
+    }
+    so.off[t + 1] = so.off[t] + seg_counts[t];
+  }
+  const int64_t n = so.off[nseg];
+  if ((n > 0 && (!keys || !sums)) || n > ((int64_t)1 << 31) - 1) {
+    rt::set_error("rt_coverage_power_segments: invalid arguments");
+    return RT_EINVAL;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  rt::DeviceGuard dg(c->device);
+  RT_HIP(dg.err);
+  int rc = rt::g_poison >= 0 ? poison_plan(c, s) : RT_OK;
+  if (rc) return rc;
+  c->ev_rec[6] = c->ev_rec[7] = false;
+  prof_mark(c, 6, s);
+  if (n > 0) {
+    if ((rc = grow_for(c, n))) return rc;
+    int64_t* idx_sorted = reinterpret_cast<int64_t*>(c->oamps_sorted);
+    hipLaunchKernelGGL(k_merge_segments, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 8192)), dim3(256), 0, s, keys,
+                       so, c->okeys_sorted, idx_sorted);
+    RT_HIP(hipGetLastError());
+    WideKey wk{};
+    wk.identity = true;
+    rc = run_sums(c, SumVal{(const Fx192*)sums, idx_sorted}, n, wk, s);
   } else {
     RT_HIP(hipMemsetAsync(c->nuniq, 0, 8, s));
   }

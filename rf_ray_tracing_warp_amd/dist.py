@@ -105,14 +105,15 @@ def reduce_max(value: float, device, group=None) -> float:
     return value
 
 
-def exchange_records(keys, vals, send_counts, group=None):
+def exchange_records(keys, vals, send_counts, group=None, return_counts=False):
     """Sparse all-to-all of coverage records: this rank's (key, value) pairs, grouped by
     destination rank with send_counts[d] for rank d, go to their owners.  vals is (n,) float64
     or (n, k) int64 (the exact fixed-point sums of Coverage.trace_records).  Returns the received
     (keys int64, vals of the same dtype and width), concatenated in source-rank order.  Keys and
     values travel as one (n, 1 + k) int64 buffer: one collective for the counts, one for the
     records.  (gloo, used by the CPU tests, moves device tensors through host memory; "nccl" =
-    RCCL sends them device to device over xGMI.)"""
+    RCCL sends them device to device over xGMI.)  return_counts: also return the number of records
+    received from each rank (the segments Coverage.power_from_records merges)."""
     import torch
     import torch.distributed as dist
     home = keys.device
@@ -134,4 +135,5 @@ def exchange_records(keys, vals, send_counts, group=None):
     dist.all_to_all_single(out, packed, recv_counts, send_counts, group=group)
     out = out.to(home)
     rv = out[:, 1:].contiguous()
-    return out[:, 0].contiguous(), (rv.view(torch.float64).reshape(-1) if is_f64 else rv)
+    res = (out[:, 0].contiguous(), (rv.view(torch.float64).reshape(-1) if is_f64 else rv))
+    return res + (recv_counts,) if return_counts else res

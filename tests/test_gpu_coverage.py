@@ -139,22 +139,24 @@ def test_coverage_on_bvh_terrain():
     cov.close()
 
 
-def _ray_sharded(env, grid, tx, B, N, S, win=100e-9, env_mesh=None):
+def _ray_sharded(env, grid, tx, B, N, S, win=100e-9, env_mesh=None, segments=False):
     """S ray-mode plans in one process: each traces its share of the rays for every cell, the
     records are routed to their owners as the all-to-all would (source-rank order), every owner
-    computes its cells, and the maps are summed (what run() does across S GPUs)."""
+    computes its cells, and the maps are summed (what run() does across S GPUs).  segments: the
+    owners merge the per-source segments (rt_coverage_power_segments) instead of sorting."""
     plans = [Coverage(env, 2.998e8, 100e9, win, B, N, grid, shard_index=r, shard_count=S, shard_mode="rays",
                       env_mesh=env_mesh) for r in range(S)]
     sent = [p.trace_records(tx, 1) for p in plans]
     total = torch.zeros(grid.num_cells, dtype=torch.float64, device="cuda")
     irs = []
     for d, p in enumerate(plans):
-        ks, as_ = [], []
+        ks, as_, segs = [], [], []
         for keys, amps, counts in sent:  # source ranks in order
             off = sum(counts[:d])
             ks.append(keys[off:off + counts[d]])
             as_.append(amps[off:off + counts[d]])
-        total += p.power_from_records(torch.cat(ks), torch.cat(as_))
+            segs.append(counts[d])
+        total += p.power_from_records(torch.cat(ks), torch.cat(as_), segs if segments else None)
         irs.append(p.impulse_responses())
     for p in plans:
         p.close()
@@ -183,6 +185,20 @@ def test_coverage_ray_sharded_equals_whole(room, S):
     np.testing.assert_array_equal(c[o], wc)
     np.testing.assert_array_equal(b[o], wb)
     np.testing.assert_allclose(a[o], wa, rtol=1e-12)
+
+
+@pytest.mark.parametrize("S", [1, 3, 8])
+def test_power_segments_equal_sorted_records(room, S):
+    """The owner stage's segment merge (each source rank's records arrive sorted, merged by rank:
+    rt_coverage_power_segments) gives exactly the sorted path's maps and impulse responses."""
+    grid, tx, B, N = CoverageGrid(8.0, -2.5, 4.6, 0.37, 0.41, 0.4, 13, 12, 2), (10, 0, 5), 3, 60_000
+    t_sort, irs_sort = _ray_sharded(room, grid, tx, B, N, S)
+    t_merge, irs_merge = _ray_sharded(room, grid, tx, B, N, S, segments=True)
+    assert t_sort.tobytes() == t_merge.tobytes()
+    assert np.isfinite(t_sort).sum() >= 20
+    for a, b in zip(irs_sort, irs_merge):
+        for x, y in zip(a, b):
+            assert x.tobytes() == y.tobytes()
 
 
 def test_coverage_ray_sharded_vs_oracle(room):

@@ -216,7 +216,8 @@ def _ray_sharded_map(plans, tx, num_cells):
         keys = torch.cat([sent[r][d][0] for r in range(W)])
         sums = torch.cat([sent[r][d][1] for r in range(W)])
         nrec.append(int(keys.numel()))
-        total += p.power_from_records(keys, sums)
+        # per-source segments merged by rank, as Coverage.run_device does after exchange_records
+        total += p.power_from_records(keys, sums, [int(sent[r][d][0].numel()) for r in range(W)])
     return total.cpu().numpy(), nrec
 
 

@@ -73,14 +73,16 @@ def rays_case(case, m, grid, tx, win, B, env, S, reps):
             t_trace.append(dt)
         t_own, nrec = [], []
         for d, p in enumerate(plans):
-            ks, as_ = [], []
+            ks, as_, segs = [], [], []
             for keys, amps, counts in sent:
                 off = sum(counts[:d])
                 ks.append(keys[off:off + counts[d]])
                 as_.append(amps[off:off + counts[d]])
+                segs.append(counts[d])
             k, a = torch.cat(ks), torch.cat(as_)
             nrec.append(int(k.numel()))
-            _, dt = timed(lambda: p.power_from_records(k, a))
+            # the received records as exchange_records delivers them: one sorted segment per source
+            _, dt = timed(lambda: p.power_from_records(k, a, None if os.environ.get("OWNER_SORT") else segs))
             t_own.append(dt)
         per_rank = [a + b for a, b in zip(t_trace, t_own)]
         if best is None or max(per_rank) < max(best[0]):
