@@ -144,6 +144,12 @@ int rt_coverage_create_rays(int device, const rt_mesh* env, int max_bounces, int
 int rt_coverage_trace_records(rt_coverage* cov, const float* tx_pos, double tx_power, double light_speed,
                               double sample_rate, int flags, int64_t n_bins, int64_t* counts, int64_t* stats,
                               void* stream);
+/* rt_coverage_trace_records that also writes the records (rt_coverage_records' layout) into the
+ * caller's device buffers of max_out records before it synchronizes, when they fit: stats[2] = 1
+ * then (else 0, and the caller takes them with rt_coverage_records).  stats: 3 int64. */
+int rt_coverage_trace_records_to(rt_coverage* cov, const float* tx_pos, double tx_power, double light_speed,
+                                 double sample_rate, int flags, int64_t n_bins, uint64_t* keys_out, uint64_t* sums_out,
+                                 int64_t max_out, int64_t* counts, int64_t* stats, void* stream);
 /* keys_out (cell << 32 | bin), sums_out (3 uint64 per record): device, max_out >= sum(counts). */
 int rt_coverage_records(rt_coverage* cov, uint64_t* keys_out, uint64_t* sums_out, int64_t max_out, void* stream);
 /* keys (cell << 32 | bin) and sums (3 uint64 per record) received from every rank, in any order. */

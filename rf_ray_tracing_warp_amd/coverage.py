@@ -153,23 +153,31 @@ class Coverage:
             raise _lib.RfrtError("trace_records needs shard_mode='rays'")
         tx = np.ascontiguousarray(np.asarray(tx_pos, dtype=np.float64).astype(np.float32))
         counts = np.zeros(self.shard_count, np.int64)
-        stats = np.zeros(2, np.int64)
-        check(lib().rt_coverage_trace_records(self._h, tx.ctypes.data, float(tx_power), float(self.light_speed_mps),
-                                              float(self.sample_rate_hz),
-                                              cir_flags(self.light_speed_mps, self.sample_rate_hz), self.n_bins,
-                                              counts.ctypes.data, stats.ctypes.data, _lib.stream_handle(self.device)),
-              "rt_coverage_trace_records")
-        self.last_candidates = int(stats[0])
-        n = int(counts.sum())
-        # grow-only record buffers: a fresh allocation per map measured ~0.25 ms of host time per
-        # rank (rocprofv3 gap before k_strip_owner); the slices stay valid until the next call
-        if self._rec is None or self._rec[0].numel() < max(n, 1):
+        stats = np.zeros(3, np.int64)
+        # grow-only record buffers, handed to the trace so that it fills them before it synchronizes
+        # (a fresh allocation per map measured ~0.25 ms of host time per rank; a second call after
+        # the synchronize, one launch and the ctypes round trip); the slices stay valid until the
+        # next call
+        if self._rec is None:
             dev = f"cuda:{self.device}"
-            m = max(n + n // 4, 1024)
+            m = max(self.ray_count * 2, 1 << 16)
             self._rec = (torch.empty(m, dtype=torch.int64, device=dev), torch.empty((m, 3), dtype=torch.int64, device=dev))
         keys, sums = self._rec
-        check(lib().rt_coverage_records(self._h, ptr(keys), ptr(sums), n, _lib.stream_handle(self.device)),
-              "rt_coverage_records")
+        check(lib().rt_coverage_trace_records_to(self._h, tx.ctypes.data, float(tx_power), float(self.light_speed_mps),
+                                                 float(self.sample_rate_hz),
+                                                 cir_flags(self.light_speed_mps, self.sample_rate_hz), self.n_bins,
+                                                 ptr(keys), ptr(sums), keys.numel(), counts.ctypes.data,
+                                                 stats.ctypes.data, _lib.stream_handle(self.device)),
+              "rt_coverage_trace_records_to")
+        self.last_candidates = int(stats[0])
+        n = int(counts.sum())
+        if not stats[2]:  # more records than the buffers hold: grow them and fetch the records
+            dev = f"cuda:{self.device}"
+            m = n + n // 4 + 1024
+            self._rec = (torch.empty(m, dtype=torch.int64, device=dev), torch.empty((m, 3), dtype=torch.int64, device=dev))
+            keys, sums = self._rec
+            check(lib().rt_coverage_records(self._h, ptr(keys), ptr(sums), n, _lib.stream_handle(self.device)),
+                  "rt_coverage_records")
         return keys[:n], sums[:n], [int(c) for c in counts]
 
     def power_from_records(self, keys, sums, counts=None):

@@ -56,6 +56,7 @@ struct CovParams {
   double r_pad;      // conservative ball radius for candidate search
   int shard, nshard;  // cells in x columns ix % nshard == shard are ours
   const int32_t* order;  // k_traj row order (direction-sorted for BVH environments) or null
+  unsigned long long* zero_ctr;  // k_traj zeroes these 4 counters for the candidate passes (no fill launch)
   // trajectory SoA [k][n]
   // trajectories, [ray][bounce] x 2 float4: (p.xyz, t_env), (d.xyz, 0) -- 32 B per ray-bounce,
   // so a random (ray, bounce) read or a direction-sorted write touches one or two lines
@@ -436,6 +437,7 @@ __device__ __forceinline__ rt::Hit rx_query_v(const RxLds& L, const rt_grid& g, 
 template <bool USE_BVH>
 __global__ __launch_bounds__(256, RT_COV_TRAJ_WAVES) void k_traj(CovParams p) {
   extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
+  if (p.zero_ctr && blockIdx.x == 0 && threadIdx.x < 4) p.zero_ctr[threadIdx.x] = 0ull;
   stage_env<USE_BVH>(p, lds_tab);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t ir = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; ir < p.n; ir += stride) {
@@ -478,6 +480,7 @@ __global__ __launch_bounds__(256, RT_COV_TRAJ_WAVES) void k_traj(CovParams p) {
 template <int G>
 __global__ __launch_bounds__(256, RT_COV_TRAJ_WAVES) void k_traj_split(CovParams p) {
   constexpr int LG = G == 16 ? 4 : 2;
+  if (p.zero_ctr && blockIdx.x == 0 && threadIdx.x < 4) p.zero_ctr[threadIdx.x] = 0ull;
   const int j = threadIdx.x & (G - 1);
   const int64_t stride = ((int64_t)gridDim.x * blockDim.x) >> LG;
   // every lane of a wave runs the same number of iterations (the shuffles need them all)
@@ -2348,6 +2351,19 @@ __global__ __launch_bounds__(256) void k_owner_bounds(const uint64_t* ukeys, con
   }
 }
 
+// as k_strip_owner, before the host knows the count: n = bounds[world] on the device, and nothing
+// is written when it exceeds the caller's capacity
+__global__ __launch_bounds__(256) void k_strip_owner_dev(const uint64_t* ukeys, const Fx192* usums, const int64_t* bounds,
+                                                         int world, int64_t cap, int shift, uint64_t* out,
+                                                         Fx192* sums_out) {
+  const int64_t n = bounds[world];
+  if (n > cap) return;
+  const uint64_t mask = (1ull << shift) - 1;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    out[i] = ukeys[i] & mask;
+    sums_out[i] = usums[i];
+  }
+}
 // the reduced records of a ray-sharded plan into the caller's send buffers: keys without the owner
 // field, and the exact sums (one launch for both)
 __global__ __launch_bounds__(256) void k_strip_owner(const uint64_t* ukeys, const Fx192* usums, int64_t n, int shift,
@@ -2434,6 +2450,7 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
   const size_t lds = bvh ? 0 : (size_t)p.env_nf * 18 * sizeof(float4);
   const unsigned grid_rays = (unsigned)std::min<int64_t>((c->n + 255) / 256, 4096);
   p.order = nullptr;
+  p.zero_ctr = c->counters;  // zeroed by the trajectory kernel (first attempt; retries use a fill)
   for (bool& r : c->ev_rec) r = false;
   if (bvh) {  // direction-sorted rows: coherent BVH traversal (as rt_trace)
     void* ws = nullptr;
@@ -2476,7 +2493,7 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
     p.item_cap = c->item_cap;
     p.keys = c->keys;
     p.cap = c->cap;
-    RT_HIP(hipMemsetAsync(c->counters, 0, 32, s));
+    if (attempt > 0) RT_HIP(hipMemsetAsync(c->counters, 0, 32, s));
     hipLaunchKernelGGL(k_cols, dim3(grid_rays), dim3(256), 0, s, p);
     hipLaunchKernelGGL(k_cells, dim3(grid_items), dim3(256), 0, s, p);
     const unsigned grid_c = (unsigned)std::min<int64_t>((c->cap + 255) / 256, 8192);
@@ -2814,10 +2831,28 @@ int rt_coverage_create_rays(int device, const rt_mesh* env, int max_bounces, int
   return RT_OK;
 }
 
+int rt_coverage_trace_records_to(rt_coverage* c, const float* tx_pos, double tx_power, double light_speed,
+                                 double sample_rate, int flags, int64_t n_bins, uint64_t* keys_out, uint64_t* sums_out,
+                                 int64_t max_out, int64_t* counts, int64_t* stats, void* stream);
+
 int rt_coverage_trace_records(rt_coverage* c, const float* tx_pos, double tx_power, double light_speed,
                               double sample_rate, int flags, int64_t n_bins, int64_t* counts, int64_t* stats,
                               void* stream) {
-  if (!c || !c->ray_mode || !tx_pos || !counts || n_bins < 1 || n_bins >= ((int64_t)1 << 32)) {
+  int64_t st3[3] = {0, 0, 0};
+  const int rc = rt_coverage_trace_records_to(c, tx_pos, tx_power, light_speed, sample_rate, flags, n_bins, nullptr,
+                                              nullptr, 0, counts, st3, stream);
+  if (!rc && stats) {
+    stats[0] = st3[0];
+    stats[1] = st3[1];
+  }
+  return rc;
+}
+
+int rt_coverage_trace_records_to(rt_coverage* c, const float* tx_pos, double tx_power, double light_speed,
+                                 double sample_rate, int flags, int64_t n_bins, uint64_t* keys_out, uint64_t* sums_out,
+                                 int64_t max_out, int64_t* counts, int64_t* stats, void* stream) {
+  if (!c || !c->ray_mode || !tx_pos || !counts || n_bins < 1 || n_bins >= ((int64_t)1 << 32) ||
+      ((keys_out || sums_out) && (!keys_out || !sums_out || max_out < 0))) {
     rt::set_error("rt_coverage_trace_records: invalid arguments (needs a plan from rt_coverage_create_rays)");
     return RT_EINVAL;
   }
@@ -2839,6 +2874,10 @@ int rt_coverage_trace_records(rt_coverage* c, const float* tx_pos, double tx_pow
     if (rc) return rc;
     hipLaunchKernelGGL(k_owner_bounds, dim3((unsigned)std::min<int64_t>((nlist + 255) / 256, 4096)), dim3(256), 0, s,
                        c->ukeys, c->nuniq, world, own_shift(c), c->bounds);
+    if (keys_out)  // the send buffers are filled before the host synchronizes (no launch after it)
+      hipLaunchKernelGGL(k_strip_owner_dev, dim3((unsigned)std::min<int64_t>((nlist + 255) / 256, 4096)), dim3(256), 0,
+                         s, c->ukeys, plan_sums(c), c->bounds, world, max_out, own_shift(c), keys_out,
+                         (Fx192*)sums_out);
     RT_HIP(hipGetLastError());
     prof_mark(c, 7, s);
     RT_HIP(hipMemcpyAsync(b.data(), c->bounds, sizeof(int64_t) * (world + 1), hipMemcpyDeviceToHost, s));
@@ -2849,6 +2888,7 @@ int rt_coverage_trace_records(rt_coverage* c, const float* tx_pos, double tx_pow
   if (stats) {
     stats[0] = ncand;
     stats[1] = nlist;
+    stats[2] = keys_out && c->n_out <= max_out ? 1 : 0;  // the records are in keys_out / sums_out
   }
   return RT_OK;
 }

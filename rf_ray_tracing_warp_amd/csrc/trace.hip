@@ -722,6 +722,185 @@ __global__ __launch_bounds__(256, RT_BVH_WAVES) void k_trace_bvh(TraceArgs a) {
   trace_body<B, true>(a);
 }
 
+// ------------------------------------------------------------------ wavefront BVH trace (RT_WAVEFRONT)
+// The north star's "ballot/prefix-sum active-ray compaction between bounces", as an A/B form of
+// k_trace_bvh: one launch per bounce over the compacted list of live rays (in the burst's
+// direction-sorted order), ray state in HBM between bounces, the path points by slot, and one final
+// pass that writes every row.  Per bounce:
+//   k_wf_bounce   one thread per live entry: the same env + receiver query and decision as
+//                 trace_body, the point by slot, the state in place, an alive flag
+//   k_wf_count    per tile of kWfTile entries: its live count
+//   k_wf_scatter  per tile: the live entries, in order (ballot + mbcnt + the tiles before it), into
+//                 the next list; the last tile writes the next count
+// then k_wf_rows writes traced / received / row_mask (and the dead bounces' hit kinds) for every ray.
+// Same operations on the same values per ray, so the same bits.  No atomics: MI355X executes
+// them at the memory side (profiles/r3b_hash_bench.jsonl).
+#ifndef RT_WAVEFRONT
+#define RT_WAVEFRONT 0
+#endif
+constexpr int kWfTile = 4096;
+__device__ __forceinline__ int wf_block_sum(int v, int* s4) {  // 256-thread blocks
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) s4[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return s4[0] + s4[1] + s4[2] + s4[3];
+}
+struct WfArgs {
+  TraceArgs t;
+  int B;
+  float4* st_a;          // list entries: (pos.xyz, slot bits), (dir.xyz, row bits), 2 float4 each
+  float4* st_b;
+  uint8_t* alive;        // per entry of the current list
+  int32_t* tile_cnt;     // per tile of the current list
+  unsigned* cnt;         // [0..B]: live entries entering bounce b
+  float4* pts;           // [(B + 1) * n]: point k of slot ir at pts[k * n + ir]
+  int8_t* last_rx;       // per slot
+  int8_t* npts;          // per slot: points on the path (B + 1 if it never missed)
+};
+__global__ __launch_bounds__(256) void k_wf_start(WfArgs w) {
+  const TraceArgs& a = w.t;
+  for (int64_t ir = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; ir < a.n; ir += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = a.order[ir];
+    const float3 d = rt::ray_dir(a.ray_offset + row);
+    w.st_a[2 * ir] = make_float4(a.tx[0], a.tx[1], a.tx[2], __int_as_float((int)ir));
+    w.st_a[2 * ir + 1] = make_float4(d.x, d.y, d.z, __int_as_float((int)row));
+    w.pts[ir] = make_float4(a.tx[0], a.tx[1], a.tx[2], 0.0f);
+    w.last_rx[ir] = -1;
+    w.npts[ir] = (int8_t)(w.B + 1);
+    if (ir == 0) w.cnt[0] = (unsigned)a.n;
+  }
+}
+__global__ __launch_bounds__(256, RT_BVH_WAVES) void k_wf_bounce(WfArgs w, int b, float4* st) {
+  const TraceArgs& a = w.t;
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nin = w.cnt[b];
+  if (j >= nin) return;
+  const float4 s0 = st[2 * j], s1 = st[2 * j + 1];
+  float3 pos = make_float3(s0.x, s0.y, s0.z), dir = make_float3(s1.x, s1.y, s1.z);
+  const int64_t ir = __float_as_int(s0.w), row = __float_as_int(s1.w);
+  const rt::Shear s = rt::make_shear(pos, dir);
+  const rt::Hit he = env_hit_query<true>(a, nullptr, s, pos, dir);
+  const bool env_hit = he.face >= 0;
+  rt::Hit hr;
+  rt::hit_init(hr);
+  if (a.rx_nf > 0 && rx_maybe(a, pos, dir, env_hit ? he.t : RT_MAX_T)) hr = query_faces(a.rx_perm, a.rx_nf, s);
+  const bool rx_hit = hr.face >= 0;
+  int kind = 0, face = -1;
+  bool live = true;
+  if (rx_hit && (!env_hit || he.t > hr.t)) {  // kernel.py:85
+    pos.x = fmaf(dir.x, hr.t, pos.x);
+    pos.y = fmaf(dir.y, hr.t, pos.y);
+    pos.z = fmaf(dir.z, hr.t, pos.z);
+    w.last_rx[ir] = (int8_t)(b + 1);
+    kind = 2;
+    face = hr.face;
+  } else if (env_hit) {  // kernel.py:93-96
+    pos.x = fmaf(dir.x, he.t, pos.x);
+    pos.y = fmaf(dir.y, he.t, pos.y);
+    pos.z = fmaf(dir.z, he.t, pos.z);
+    const float4 n4 = a.env_nrm[he.face];
+    const float3 n = make_float3(n4.x, n4.y, n4.z);
+    const float sc = 2.0f * rt::dot3(dir, n);
+    dir.x = fmaf(-sc, n.x, dir.x);
+    dir.y = fmaf(-sc, n.y, dir.y);
+    dir.z = fmaf(-sc, n.z, dir.z);
+    kind = 1;
+    face = he.face;
+  } else {
+    live = false;  // kernel.py:97-98: every later iteration repeats this miss
+    w.npts[ir] = (int8_t)(b + 1);
+  }
+  if (live) {
+    w.pts[(int64_t)(b + 1) * a.n + ir] = make_float4(pos.x, pos.y, pos.z, 0.0f);
+    st[2 * j] = make_float4(pos.x, pos.y, pos.z, s0.w);
+    st[2 * j + 1] = make_float4(dir.x, dir.y, dir.z, s1.w);
+  }
+  w.alive[j] = live ? 1 : 0;
+  if (a.hit_kind) a.hit_kind[row * w.B + b] = kind;
+  if (a.hit_face) a.hit_face[row * w.B + b] = face;
+}
+__global__ __launch_bounds__(256) void k_wf_count(WfArgs w, int b) {
+  __shared__ int s4[4];
+  const int64_t nin = w.cnt[b];
+  const int64_t lo = (int64_t)blockIdx.x * kWfTile;
+  if (lo >= nin) return;  // block-uniform
+  const int64_t hi = lo + kWfTile < nin ? lo + kWfTile : nin;
+  int c = 0;
+  for (int64_t j = lo + threadIdx.x; j < hi; j += blockDim.x) c += w.alive[j];
+  c = wf_block_sum(c, s4);
+  if (threadIdx.x == 0) w.tile_cnt[blockIdx.x] = c;
+}
+__global__ __launch_bounds__(256) void k_wf_scatter(WfArgs w, int b, const float4* in, float4* out) {
+  __shared__ int s4[4];
+  __shared__ int w4[4];
+  const int64_t nin = w.cnt[b];
+  const int64_t ntiles = (nin + kWfTile - 1) / kWfTile;
+  const int64_t t = blockIdx.x;
+  if (t >= ntiles) {
+    if (t == 0 && threadIdx.x == 0) w.cnt[b + 1] = 0;  // nothing was live
+    return;
+  }
+  int before = 0;
+  for (int64_t q = threadIdx.x; q < t; q += blockDim.x) before += w.tile_cnt[q];
+  int64_t base = wf_block_sum(before, s4);
+  if (t == ntiles - 1 && threadIdx.x == 0) w.cnt[b + 1] = (unsigned)(base + w.tile_cnt[t]);
+  const int64_t lo = t * kWfTile, hi = lo + kWfTile < nin ? lo + kWfTile : nin;
+  const int wave = threadIdx.x >> 6;
+  for (int64_t j0 = lo; j0 < hi; j0 += blockDim.x) {  // block-uniform
+    const int64_t j = j0 + threadIdx.x;
+    const bool f = j < hi && w.alive[j] != 0;
+    const uint64_t m = __ballot(f);
+    if ((threadIdx.x & 63) == 0) w4[wave] = __popcll(m);
+    __syncthreads();
+    int off = 0;
+    for (int q = 0; q < wave; ++q) off += w4[q];
+    const int step = w4[0] + w4[1] + w4[2] + w4[3];
+    if (f) {
+      const int64_t k = base + off + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      out[2 * k] = in[2 * j];
+      out[2 * k + 1] = in[2 * j + 1];
+    }
+    base += step;
+    __syncthreads();
+  }
+}
+template <int B>
+__global__ __launch_bounds__(256) void k_wf_rows(WfArgs w) {
+  constexpr int P = B + 1;
+  const TraceArgs& a = w.t;
+  const float qnan = __builtin_nanf("");
+  for (int64_t ir = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; ir < a.n; ir += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = a.order[ir];
+    const int np = w.npts[ir], lr = w.last_rx[ir];
+    float path[P][3];
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      const float4 q = k < np ? w.pts[(int64_t)k * a.n + ir] : make_float4(qnan, qnan, qnan, 0.0f);
+      path[k][0] = q.x;
+      path[k][1] = q.y;
+      path[k][2] = q.z;
+    }
+    if (a.traced) store_row_fixed<P>(a.traced + row * (P * 3), path);
+    if (a.received) {
+      float rec[P][3];
+#pragma unroll
+      for (int i = 0; i < P; ++i) {
+        const bool keep = i <= lr;
+        rec[i][0] = keep ? path[i][0] : qnan;
+        rec[i][1] = keep ? path[i][1] : qnan;
+        rec[i][2] = keep ? path[i][2] : qnan;
+      }
+      store_row_fixed<P>(a.received + row * (P * 3), rec);
+    }
+    if (a.mask) a.mask[row] = lr >= 0 ? 1u : 0u;
+    for (int b = np; b < B; ++b) {  // bounces after the miss repeat it: kind 0, no face
+      if (a.hit_kind) a.hit_kind[row * B + b] = 0;
+      if (a.hit_face) a.hit_face[row * B + b] = -1;
+    }
+  }
+}
+
 // Generic fallback for B beyond the register-resident instantiations: the path lives in
 // the output rows themselves (same semantics, slower).
 template <bool USE_BVH>
@@ -983,6 +1162,62 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
   }
   // xcd_chunk needs whole groups of 8 blocks (one per XCD)
   const int grid = windows ? (grid0 + 7) / 8 * 8 : grid0;
+  if (RT_WAVEFRONT && bvh && a.order && B <= 8) {
+    const int64_t tiles = (n + kWfTile - 1) / kWfTile;
+    const size_t st_bytes = (size_t)n * 32, pts_bytes = (size_t)(B + 1) * n * 16;
+    const size_t bytes = 2 * st_bytes + pts_bytes + (size_t)n * 3 + (size_t)tiles * 4 + 64 + 256;
+    void* wf = nullptr;
+    RT_HIP(hipMallocAsync(&wf, bytes, stream));
+    WfArgs w{};
+    w.t = a;
+    w.B = B;
+    char* q = (char*)wf;
+    w.st_a = (float4*)q;
+    q += st_bytes;
+    w.st_b = (float4*)q;
+    q += st_bytes;
+    w.pts = (float4*)q;
+    q += pts_bytes;
+    w.cnt = (unsigned*)q;
+    q += 64;
+    w.tile_cnt = (int32_t*)q;
+    q += (size_t)tiles * 4;
+    w.alive = (uint8_t*)q;
+    q += n;
+    w.last_rx = (int8_t*)q;
+    q += n;
+    w.npts = (int8_t*)q;
+    hipEvent_t wev0 = nullptr, wev1 = nullptr;
+    trace_events(&wev0, &wev1);
+    if (wev0) RT_HIP(hipEventRecord(wev0, stream));
+    const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_wf_start, dim3(g), dim3(256), 0, stream, w);
+    float4* cur = w.st_a;
+    float4* nxt = w.st_b;
+    for (int b = 0; b < B; ++b) {
+      hipLaunchKernelGGL(k_wf_bounce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, w, b, cur);
+      if (b + 1 < B) {
+        hipLaunchKernelGGL(k_wf_count, dim3((unsigned)tiles), dim3(256), 0, stream, w, b);
+        hipLaunchKernelGGL(k_wf_scatter, dim3((unsigned)tiles), dim3(256), 0, stream, w, b, cur, nxt);
+        std::swap(cur, nxt);
+      }
+    }
+    switch (B) {
+#define RT_WF_ROWS(BB) \
+  case BB:             \
+    hipLaunchKernelGGL(k_wf_rows<BB>, dim3(g), dim3(256), 0, stream, w); \
+    break;
+      RT_WF_ROWS(1) RT_WF_ROWS(2) RT_WF_ROWS(3) RT_WF_ROWS(4) RT_WF_ROWS(5) RT_WF_ROWS(6) RT_WF_ROWS(7) RT_WF_ROWS(8)
+#undef RT_WF_ROWS
+      default:
+        break;
+    }
+    if (wev1) RT_HIP(hipEventRecord(wev1, stream));
+    RT_HIP(hipGetLastError());
+    RT_HIP(hipFreeAsync(wf, stream));
+    if (sort_ws) RT_HIP(hipFreeAsync(sort_ws, stream));
+    return 0;
+  }
   // profiling: the kernel's own dispatch packet carries the start/stop timestamps
   // (hipExtLaunchKernelGGL), so timing adds no marker packets -- and no gaps -- to the stream
   hipEvent_t ev0 = nullptr, ev1 = nullptr;

@@ -283,3 +283,20 @@ def test_fixed_point_bin_sums_are_exact(room):
     assert len(a) == len(exact)
     for cc, bb, x in zip(c, b, a):
         assert x == float(exact[(int(cc), int(bb))] * unit), (cc, bb)
+
+
+def test_trace_records_into_small_buffers_falls_back(room):
+    """Coverage.trace_records hands its grow-only buffers to rt_coverage_trace_records_to, which fills
+    them before it synchronizes; when they are too small it says so and the records come from
+    rt_coverage_records into larger ones -- the same records either way."""
+    grid, tx, B, N = CoverageGrid(8.0, -2.5, 4.6, 0.37, 0.41, 0.4, 13, 12, 2), (10, 0, 5), 3, 60_000
+    p = Coverage(room, 2.998e8, 100e9, 100e-9, B, N, grid, shard_index=1, shard_count=3, shard_mode="rays")
+    k1, s1, c1 = p.trace_records(tx, 1)
+    k1, s1 = k1.clone(), s1.clone()
+    assert sum(c1) > 100
+    p._rec = (torch.empty(1, dtype=torch.int64, device="cuda"), torch.empty((1, 3), dtype=torch.int64, device="cuda"))
+    k2, s2, c2 = p.trace_records(tx, 1)
+    assert c1 == c2 and p._rec[0].numel() > 1
+    assert k1.cpu().numpy().tobytes() == k2.cpu().numpy().tobytes()
+    assert s1.cpu().numpy().tobytes() == s2.cpu().numpy().tobytes()
+    p.close()
