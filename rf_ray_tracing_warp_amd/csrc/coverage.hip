@@ -1132,11 +1132,16 @@ constexpr int kReplayWin = 1024 * RT_REPLAY_WIN_ITEMS;
 #define RT_REPLAY_WINDOW_MAX (1 << 21)
 #endif
 constexpr int64_t kReplayWindowMax = RT_REPLAY_WINDOW_MAX;
+#ifndef RT_REPLAY_EARLY
+#define RT_REPLAY_EARLY 1
+#endif
 template <bool USE_BVH>
 __global__ __launch_bounds__(1024) void k_replay_order(CovParams p, const uint64_t* keys, const int64_t* list,
-                                                       int64_t nl, int32_t* order) {
+                                                       int64_t nl, const unsigned long long* nl_dev, int32_t* order) {
   using Sort = rocprim::block_radix_sort<uint16_t, 1024, RT_REPLAY_WIN_ITEMS, int32_t>;
   __shared__ typename Sort::storage_type st;
+  if (nl_dev) nl = min(nl, (int64_t)*nl_dev);  // launched before the host knows the list length
+  if ((int64_t)blockIdx.x * kReplayWin >= nl) return;
   const int64_t base = (int64_t)blockIdx.x * kReplayWin + (int64_t)threadIdx.x * RT_REPLAY_WIN_ITEMS;
   uint16_t k[RT_REPLAY_WIN_ITEMS];
   int32_t v[RT_REPLAY_WIN_ITEMS];
@@ -1154,10 +1159,12 @@ __global__ __launch_bounds__(1024) void k_replay_order(CovParams p, const uint64
 
 template <bool USE_BVH, bool RX_FIRST>
 __global__ __launch_bounds__(256, RT_COV_REPLAY_WAVES) void k_replay(CovParams p, const uint64_t* keys, const float* trx,
-                                                const int64_t* list, int64_t nl, const int32_t* order,
-                                                uint64_t* out_key, double* out_amp) {
+                                                const int64_t* list, int64_t nl, const unsigned long long* nl_dev,
+                                                const int32_t* order, uint64_t* out_key, double* out_amp) {
   extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
   __shared__ RxLds L;
+  if (nl_dev) nl = min(nl, (int64_t)*nl_dev);  // see k_replay_order
+  if ((int64_t)blockIdx.x * blockDim.x >= nl) return;
   stage_rx(L, p.r_rx);
   stage_env<USE_BVH>(p, lds_tab);
   for (int64_t jl = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; jl < nl; jl += (int64_t)gridDim.x * blockDim.x) {
@@ -1753,6 +1760,7 @@ struct rt_coverage {
   size_t tmp_bytes = 0;
   int64_t cap = 0;
   int64_t last_candidates = 0;
+  int64_t last_list = 0;  // first wins of the last run (sizes the early replay's grid)
   int64_t last_received = 0;  // first-win (cell, ray) records of the last run
   void* rord = nullptr;        // replay-order sort workspace (16-bit keys + int32 rows, x2, + hipCUB)
   size_t rord_bytes = 0;
@@ -1762,6 +1770,8 @@ struct rt_coverage {
   // ray-bounces = sum of the trajectories' segments, [1] replayed ray-bounces)
   bool profile = false;
   hipEvent_t pev[8] = {};
+  unsigned long long* hcnt = nullptr;  // pinned copy of counters[0..2] (the candidate stage's read-back)
+  hipEvent_t ev_cnt = nullptr;         // recorded after that copy
   bool ev_rec[8] = {};
   unsigned long long* work = nullptr;
 };
@@ -2488,6 +2498,55 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
   p.cell_bits = kb.cell;
   int64_t ncand = 0, nrec = 0, nlist = 0;
   const unsigned grid_items = 4096;
+  // Replay launched before the list length reaches the host (RT_REPLAY_EARLY): the kernels read it
+  // from the device counter, so the host's counter read-back and its wake-up (~36 us per K3 rank
+  // of 8, profiles/r3j_k3.timeline.txt) overlap the replay instead of idling the GPU.  Only for
+  // lists the window order takes (a rank's share); the whole-map lists keep the device-wide sort,
+  // which needs the length on the host.  The previous run's length sizes the grid.
+  auto launch_replay = [&](int64_t nl, const unsigned long long* nl_dev, bool windows, int64_t grid_hint) {
+    const unsigned grid_l = (unsigned)std::max<int64_t>(1, std::min<int64_t>((grid_hint + 255) / 256, 8192));
+    const size_t kbs = rord_key_bytes(nl), rbs = rord_row_bytes(nl);
+    size_t cub_bytes = c->rord_bytes - 2 * kbs - 2 * rbs;  // the workspace was sized for cap >= nl
+    void* ws = c->rord;
+    uint16_t* k_in = (uint16_t*)ws;
+    uint16_t* k_out = (uint16_t*)((char*)ws + kbs);
+    int32_t* v_in = (int32_t*)((char*)ws + 2 * kbs);
+    int32_t* v_out = (int32_t*)((char*)ws + 2 * kbs + rbs);
+    if (windows) {
+      const unsigned grid_w = (unsigned)((nl + kReplayWin - 1) / kReplayWin);
+      if (bvh)
+        hipLaunchKernelGGL(k_replay_order<true>, dim3(grid_w), dim3(1024), 0, s, p, c->keys, c->list, nl, nl_dev,
+                           v_out);
+      else
+        hipLaunchKernelGGL(k_replay_order<false>, dim3(grid_w), dim3(1024), 0, s, p, c->keys, c->list, nl, nl_dev,
+                           v_out);
+    } else {
+      if (bvh)
+        hipLaunchKernelGGL(k_replay_keys<true>, dim3(grid_l), dim3(256), 0, s, p, c->keys, c->list, nl, k_in, v_in);
+      else
+        hipLaunchKernelGGL(k_replay_keys<false>, dim3(grid_l), dim3(256), 0, s, p, c->keys, c->list, nl, k_in, v_in);
+      RT_HIP(hipcub::DeviceRadixSort::SortPairs((char*)ws + 2 * kbs + 2 * rbs, cub_bytes, k_in, k_out, v_in, v_out,
+                                                (int)nl, 0, 16, s));
+    }
+    prof_mark(c, 4, s);
+    // BVH scenes: receiver first, the traversal culled at its t (K5 replay 3.47 -> 2.7 ms); the
+    // LDS brute force tests every face anyway (a plane-culled variant measured 5% slower on K3,
+    // a receiver-first one skipping faces beyond the receiver's t 5% slower too: 2.50 vs 2.63 ms,
+    // profiles/r2x_cov_rxfirst_lds_ab.jsonl)
+    if (bvh && replay_rx_first())
+      hipLaunchKernelGGL((k_replay<true, true>), dim3(grid_l), dim3(256), 0, s, p, c->keys, c->trx, c->list, nl,
+                         nl_dev, v_out, c->okeys, c->oamps);
+    else if (bvh)
+      hipLaunchKernelGGL((k_replay<true, false>), dim3(grid_l), dim3(256), 0, s, p, c->keys, c->trx, c->list, nl,
+                         nl_dev, v_out, c->okeys, c->oamps);
+    else
+      hipLaunchKernelGGL((k_replay<false, false>), dim3(grid_l), dim3(256), lds, s, p, c->keys, c->trx, c->list, nl,
+                         nl_dev, v_out, c->okeys, c->oamps);
+    prof_mark(c, 5, s);
+    RT_HIP(hipGetLastError());
+    return 0;
+  };
+  bool replayed = false;
   for (int attempt = 0;; ++attempt) {
     p.items = c->items;
     p.item_cap = c->item_cap;
@@ -2510,9 +2569,18 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
                          (const unsigned long long*)c->counters, c->cap, tiles, c->list, c->counters + 2);
     }
     RT_HIP(hipGetLastError());
-    unsigned long long h[3] = {0, 0, 0};
-    RT_HIP(hipMemcpyAsync(h, c->counters, 24, hipMemcpyDeviceToHost, s));
-    RT_HIP(hipStreamSynchronize(s));
+    // the counters go to pinned memory ahead of the replay, and the host waits for that copy only;
+    // the list holds at most cap entries (one per candidate)
+    RT_HIP(hipMemcpyAsync(c->hcnt, c->counters, 24, hipMemcpyDeviceToHost, s));
+    RT_HIP(hipEventRecord(c->ev_cnt, s));
+    replayed = RT_REPLAY_EARLY && RT_REPLAY_WINDOW && (c->last_list > 0 ? c->last_list : c->cap) <= kReplayWindowMax;
+    if (replayed) {
+      int rc = launch_replay(c->cap, (const unsigned long long*)c->counters + 2, true,
+                             c->last_list > 0 ? c->last_list + c->last_list / 8 : c->cap);
+      if (rc) return rc;
+    }
+    RT_HIP(hipEventSynchronize(c->ev_cnt));
+    const unsigned long long h[3] = {c->hcnt[0], c->hcnt[1], c->hcnt[2]};
     ncand = (int64_t)h[0];
     const int64_t nitems = (int64_t)h[1];
     nlist = (int64_t)h[2];
@@ -2534,49 +2602,14 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
     return RT_EINVAL;
   }
   c->last_candidates = ncand;
+  c->last_list = nlist;
   *ncand_out = ncand;
   if (ncand > 0) {
     if (nlist > 0) {
-      // coherent processing order (16-bit keys through hipCUB, workspace stream-ordered)
-      const unsigned grid_l = (unsigned)std::min<int64_t>((nlist + 255) / 256, 8192);
-      const size_t kbs = rord_key_bytes(nlist), rbs = rord_row_bytes(nlist);
-      size_t cub_bytes = c->rord_bytes - 2 * kbs - 2 * rbs;  // the workspace was sized for cap >= nlist
-      void* ws = c->rord;
-      uint16_t* k_in = (uint16_t*)ws;
-      uint16_t* k_out = (uint16_t*)((char*)ws + kbs);
-      int32_t* v_in = (int32_t*)((char*)ws + 2 * kbs);
-      int32_t* v_out = (int32_t*)((char*)ws + 2 * kbs + rbs);
-      if (RT_REPLAY_WINDOW && nlist <= kReplayWindowMax) {
-        const unsigned grid_w = (unsigned)((nlist + kReplayWin - 1) / kReplayWin);
-        if (bvh)
-          hipLaunchKernelGGL(k_replay_order<true>, dim3(grid_w), dim3(1024), 0, s, p, c->keys, c->list, nlist, v_out);
-        else
-          hipLaunchKernelGGL(k_replay_order<false>, dim3(grid_w), dim3(1024), 0, s, p, c->keys, c->list, nlist, v_out);
-      } else {
-        if (bvh)
-          hipLaunchKernelGGL(k_replay_keys<true>, dim3(grid_l), dim3(256), 0, s, p, c->keys, c->list, nlist, k_in, v_in);
-        else
-          hipLaunchKernelGGL(k_replay_keys<false>, dim3(grid_l), dim3(256), 0, s, p, c->keys, c->list, nlist, k_in,
-                             v_in);
-        RT_HIP(hipcub::DeviceRadixSort::SortPairs((char*)ws + 2 * kbs + 2 * rbs, cub_bytes, k_in, k_out, v_in, v_out,
-                                                  (int)nlist, 0, 16, s));
+      if (!replayed) {
+        int rc = launch_replay(nlist, nullptr, RT_REPLAY_WINDOW && nlist <= kReplayWindowMax, nlist);
+        if (rc) return rc;
       }
-      prof_mark(c, 4, s);
-      // BVH scenes: receiver first, the traversal culled at its t (K5 replay 3.47 -> 2.7 ms); the
-      // LDS brute force tests every face anyway (a plane-culled variant measured 5% slower on K3,
-      // a receiver-first one skipping faces beyond the receiver's t 5% slower too: 2.50 vs 2.63 ms,
-      // profiles/r2x_cov_rxfirst_lds_ab.jsonl)
-      if (bvh && replay_rx_first())
-        hipLaunchKernelGGL((k_replay<true, true>), dim3(grid_l), dim3(256), 0, s, p, c->keys, c->trx, c->list, nlist,
-                           v_out, c->okeys, c->oamps);
-      else if (bvh)
-        hipLaunchKernelGGL((k_replay<true, false>), dim3(grid_l), dim3(256), 0, s, p, c->keys, c->trx, c->list, nlist,
-                           v_out, c->okeys, c->oamps);
-      else
-        hipLaunchKernelGGL((k_replay<false, false>), dim3(grid_l), dim3(256), lds, s, p, c->keys, c->trx, c->list,
-                           nlist, v_out, c->okeys, c->oamps);
-      prof_mark(c, 5, s);
-      RT_HIP(hipGetLastError());
       if (c->profile)
         hipLaunchKernelGGL(k_count_replay, dim3(1024), dim3(256), 0, s, c->keys, c->list, nlist, p.B, c->work + 1);
     }
@@ -2736,6 +2769,8 @@ int rt_coverage_create(int device, const rt_mesh* env, int max_bounces, int64_t 
   if (e == hipSuccess) e = hipMalloc(&c->bigcells, sizeof(int32_t) * nc);
   if (e == hipSuccess) e = hipMalloc(&c->cepoch, sizeof(int32_t) * nc);
   if (e == hipSuccess) e = hipMemset(c->cepoch, 0, sizeof(int32_t) * nc);  // epochs start at 1
+  if (e == hipSuccess) e = hipHostMalloc((void**)&c->hcnt, 32, hipHostMallocDefault);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_cnt, hipEventDisableTiming);
   if (e != hipSuccess) {
     rt_coverage_destroy(c);
     return rt::hip_fail(e, "rt_coverage_create");
@@ -2767,6 +2802,8 @@ int rt_coverage_destroy(rt_coverage* c) {
   if (c->work) (void)hipFree(c->work);
   for (hipEvent_t e : c->pev)
     if (e) (void)hipEventDestroy(e);
+  if (c->ev_cnt) (void)hipEventDestroy(c->ev_cnt);
+  if (c->hcnt) (void)hipHostFree(c->hcnt);
   delete c;
   return RT_OK;
 }
