@@ -242,6 +242,9 @@ __device__ __forceinline__ void cas(float& ta, int& ra, float& tb, int& rb) {
   rb = r1;
 }
 
+#ifndef RT_BVH_PREFETCH
+#define RT_BVH_PREFETCH 0
+#endif
 struct Walk4 {
   Hit h;
   RayBox r;
@@ -291,6 +294,26 @@ struct Walk4 {
     cas(l0, p0, l2, p2);
     cas(l1, p1, l3, p3);
     cas(l1, p1, l2, p2);
+#if RT_BVH_PREFETCH
+    // the node the next step will most likely visit (the nearest hit inner child, else the stack
+    // top), touched before the leaf tests so that its fetch overlaps theirs
+    float pf = 0.0f;
+    if (l0 <= cull_limit(h, tc)) {
+      const float lim0 = cull_limit(h, tc);
+      const float tn = fminf(fminf(c0 >= 0 ? t0 : INFINITY, c1 >= 0 ? t1 : INFINITY),
+                             fminf(c2 >= 0 ? t2 : INFINITY, c3 >= 0 ? t3 : INFINITY));
+      int nx = -1;
+      if (tn <= lim0) {
+        nx = (c0 >= 0 && t0 == tn) ? c0 : (c1 >= 0 && t1 == tn) ? c1 : (c2 >= 0 && t2 == tn) ? c2 : c3;
+      } else if (sp > 0) {
+        nx = st.get_node(sp - 1);
+      }
+      if (nx >= 0) {
+        const float* nw = reinterpret_cast<const float*>(b.wide + 8 * (int64_t)nx);
+        pf = nw[0] + nw[16];
+      }
+    }
+#endif
 #pragma unroll 1
     for (int q = 0; q < 4; ++q) {  // one leaf4 body in the code; the sorted list shifts down
       if (!(l0 <= cull_limit(h, tc))) break;
@@ -317,6 +340,9 @@ struct Walk4 {
     } else {
       cur = -1;
     }
+#if RT_BVH_PREFETCH
+    asm volatile("" ::"v"(pf));  // keeps the touch; its wait lands here, after the leaf tests
+#endif
     }
     return true;
   }
@@ -397,13 +423,38 @@ using Walk = Walk4;
 using Walk = Walk2;
 #endif
 
+// RT_COUNT_STEPS (diagnostic builds only, tools/walk_stats.py): per query, the lane's walk steps and
+// its share of the wave's loop iterations (1 / active lanes per iteration, so the shares of a wave
+// add up to its iteration count), summed over 16 slots by block; the max steps of one query.
+#ifndef RT_COUNT_STEPS
+#define RT_COUNT_STEPS 0
+#endif
+#if RT_COUNT_STEPS
+static __device__ unsigned long long g_walk_stats[16 * 4];  // steps, iterations * 2^16, queries, max steps
+#endif
+
 __device__ __forceinline__ Hit bvh_query(const BvhView& b, const Shear& s, float3 o, float3 d,
                                          float tcull = RT_MAX_T) {
   Walk w;
   WalkStack st = make_stack();
   w.init(o, d, tcull);
   bool active = true;
+#if RT_COUNT_STEPS
+  unsigned steps = 0;
+  float iters = 0.0f;
+  while (active) {
+    iters += 1.0f / (float)__popcll(__ballot(1));
+    ++steps;
+    active = w.step(b, s, st);
+  }
+  unsigned long long* g = g_walk_stats + 4 * (blockIdx.x & 15);
+  atomicAdd(g + 0, (unsigned long long)steps);
+  atomicAdd(g + 1, (unsigned long long)(iters * 65536.0f + 0.5f));
+  atomicAdd(g + 2, 1ull);
+  atomicMax(g + 3, (unsigned long long)steps);
+#else
   while (active) active = w.step(b, s, st);
+#endif
   return w.h;
 }
 

@@ -17,6 +17,7 @@
 #include <hipcub/hipcub.hpp>
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 #include <mutex>
 
 #include "rt_bvh.h"
@@ -1323,3 +1324,26 @@ int trace_profile_stats(double* out, int n) {
 }
 
 }  // namespace rt
+
+#if RT_COUNT_STEPS
+// diagnostic builds only (RT_COUNT_STEPS=1, tools/walk_stats.py): the walk statistics of this file's
+// kernels since the last reset -- out[0..3] = lane steps, wave iterations, queries, max steps
+extern "C" int rt_debug_walk_stats(double* out, int reset) {
+  unsigned long long h[16 * 4];
+  if (hipDeviceSynchronize() != hipSuccess) return RT_EHIP;
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(rt::g_walk_stats), sizeof h) != hipSuccess) return RT_EHIP;
+  double a[4] = {0, 0, 0, 0};
+  for (int i = 0; i < 16; ++i) {
+    a[0] += (double)h[4 * i];
+    a[1] += (double)h[4 * i + 1] / 65536.0;
+    a[2] += (double)h[4 * i + 2];
+    a[3] = std::max(a[3], (double)h[4 * i + 3]);
+  }
+  for (int k = 0; k < 4; ++k) out[k] = a[k];
+  if (reset) {
+    std::memset(h, 0, sizeof h);
+    if (hipMemcpyToSymbol(HIP_SYMBOL(rt::g_walk_stats), h, sizeof h) != hipSuccess) return RT_EHIP;
+  }
+  return RT_OK;
+}
+#endif

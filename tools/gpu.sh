@@ -16,7 +16,7 @@
 #   stats     rocprofv3 --kernel-trace --stats over bench.py ${PROF_ARGS}    -> prof_${TAG}/stats
 #   pmc       one rocprofv3 --pmc pass per group of ${PASSES} over bench.py  -> prof_${TAG}/p<i>
 #   ranks     tools/cov_profile.py (K3/K5, 1 and 8 ray-shard ranks)          -> ${TAG}_cov_ranks.jsonl
-#   timeline  rocprofv3 kernel trace of one rank-of-8 pass + rank_timeline   -> ${TAG}_<case>.timeline.txt
+#   timeline  rocprofv3 kernel trace of one rank-of-8 pass (TL_SHARDS=1: the whole map) + rank_timeline -> ${TAG}_<case>.timeline.txt
 #   covvar    tools/cov_variants.py over LIBS (A/B, hashed)                  -> ${TAG}_cov.jsonl
 #   tracevar  tools/trace_variants.py over LIBS (SCENE=room|terrain)         -> ${TAG}_trace.jsonl
 #   k2var     tools/k2_fused_variants.py over LIBS                           -> ${TAG}_k2.jsonl
@@ -73,7 +73,7 @@ run_task() {
       rc=$?; cut -c1-260 ${O}_cov_ranks.jsonl; step_rc $rc ranks ;;
     timeline)
       for c in ${CASES:-k3 k5}; do
-        CASES=$c SHARDS=8 REPS=1 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d ${O}_tl_$c -- \
+        CASES=$c SHARDS=${TL_SHARDS:-8} REPS=1 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d ${O}_tl_$c -- \
           python3 tools/cov_profile.py > ${O}_tl_$c.log 2>&1
         rc=$?; step_rc $rc "timeline $c"
         python3 tools/rank_timeline.py ${O}_tl_$c > ${O}_$c.timeline.txt; tail -30 ${O}_$c.timeline.txt
