@@ -134,9 +134,10 @@ int rt_coverage_run(rt_coverage* cov, const float* tx_pos, double tx_power, doub
  *   1. rt_coverage_create_rays                         (once)
  *   2. rt_coverage_trace_records -> counts[world]      (records for each destination rank; syncs)
  *   3. rt_coverage_records -> caller device buffers    (grouped by destination, rank 0 first)
+ *      (2+3 in one call: rt_coverage_trace_records_to, or _packed for one row per record)
  *   4. all-to-all of the records (the caller's collective: RCCL via torch.distributed)
  *   5. rt_coverage_power_segments on the received records, concatenated in source-rank order
- *      (or rt_coverage_power_records for records in any order)
+ *      (rt_coverage_power_packed for packed rows; rt_coverage_power_records for any order)
  *   6. sum-reduce of the power maps (other ranks' cells are 0 here). */
 int rt_coverage_create_rays(int device, const rt_mesh* env, int max_bounces, int64_t n_rays_total, int64_t ray_offset,
                             int64_t n_rays, const rt_grid* grid, double rx_radius, int rank, int world,
@@ -150,6 +151,12 @@ int rt_coverage_trace_records(rt_coverage* cov, const float* tx_pos, double tx_p
 int rt_coverage_trace_records_to(rt_coverage* cov, const float* tx_pos, double tx_power, double light_speed,
                                  double sample_rate, int flags, int64_t n_bins, uint64_t* keys_out, uint64_t* sums_out,
                                  int64_t max_out, int64_t* counts, int64_t* stats, void* stream);
+/* rt_coverage_trace_records_to with each record as one 32-B row (key, sum word 0, 1, 2) of
+ * rows_out (device, 16-B aligned, max_out rows): the layout the all-to-all sends as it is, so the
+ * caller packs nothing (rt_coverage_power_packed takes the received rows).  stats: 3 int64. */
+int rt_coverage_trace_records_packed(rt_coverage* cov, const float* tx_pos, double tx_power, double light_speed,
+                                     double sample_rate, int flags, int64_t n_bins, uint64_t* rows_out,
+                                     int64_t max_out, int64_t* counts, int64_t* stats, void* stream);
 /* keys_out (cell << 32 | bin), sums_out (3 uint64 per record): device, max_out >= sum(counts). */
 int rt_coverage_records(rt_coverage* cov, uint64_t* keys_out, uint64_t* sums_out, int64_t max_out, void* stream);
 /* keys (cell << 32 | bin) and sums (3 uint64 per record) received from every rank, in any order. */
@@ -160,6 +167,10 @@ int rt_coverage_power_records(rt_coverage* cov, const uint64_t* keys, const uint
  * no repeated key): the segments are merged by rank instead of sorted (one launch). */
 int rt_coverage_power_segments(rt_coverage* cov, const uint64_t* keys, const uint64_t* sums, const int64_t* seg_counts,
                                int nseg, int64_t n_bins, double alpha, double* power, void* stream);
+/* rt_coverage_power_segments on received (key, sum) rows of rt_coverage_trace_records_packed's
+ * layout, segment t = seg_counts[t] rows from rank t. */
+int rt_coverage_power_packed(rt_coverage* cov, const uint64_t* rows, const int64_t* seg_counts, int nseg,
+                             int64_t n_bins, double alpha, double* power, void* stream);
 /* f64 amplitudes (finite, >= 0, below 2^56) -> the exact fixed-point sums of rt_coverage_records
  * (truncated below 2^-136), on the device. */
 int rt_coverage_amps_to_sums(const double* amps, int64_t n, uint64_t* sums, void* stream);

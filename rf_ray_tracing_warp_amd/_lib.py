@@ -70,6 +70,9 @@ def lib():
                                                _i64, _vp, _vp, _i64, _vp, _vp, _vp]
     L.rt_coverage_power_records.argtypes = [_vp, _vp, _vp, _i64, _i64, ctypes.c_double, _vp, _vp]
     L.rt_coverage_power_segments.argtypes = [_vp, _vp, _vp, _vp, _int, _i64, ctypes.c_double, _vp, _vp]
+    L.rt_coverage_trace_records_packed.argtypes = [_vp, _vp, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                                   _int, _i64, _vp, _i64, _vp, _vp, _vp]
+    L.rt_coverage_power_packed.argtypes = [_vp, _vp, _vp, _int, _i64, ctypes.c_double, _vp, _vp]
     L.rt_coverage_amps_to_sums.argtypes = [_vp, _i64, _vp, _vp]
     L.rt_coverage_received.argtypes = [_vp, _vp, _vp, _i64, ctypes.POINTER(_i64), _vp]
     L.rt_power_dense.argtypes = [_vp, _i64, _i64, ctypes.c_double, _vp, _i64, _vp, _vp]
@@ -86,7 +89,8 @@ def lib():
     for name in ("rt_mesh_create", "rt_mesh_create_ex", "rt_mesh_destroy", "rt_mesh_info", "rt_bvh_info", "rt_trace", "rt_compact", "rt_cir", "rt_trace_cir",
                  "rt_coverage_create", "rt_coverage_destroy", "rt_coverage_run", "rt_coverage_received",
                  "rt_coverage_create_rays", "rt_coverage_trace_records", "rt_coverage_trace_records_to", "rt_coverage_records",
-                 "rt_coverage_power_records", "rt_coverage_power_segments", "rt_coverage_amps_to_sums", "rt_coverage_profile", "rt_coverage_last_profile", "rt_debug_poison",
+                 "rt_coverage_power_records", "rt_coverage_power_segments", "rt_coverage_trace_records_packed",
+                 "rt_coverage_power_packed", "rt_coverage_amps_to_sums", "rt_coverage_profile", "rt_coverage_last_profile", "rt_debug_poison",
                  "rt_profile", "rt_trace_last_profile", "rt_trace_profile_stats",
                  "rt_power_dense", "rt_selftest_math", "rt_ray_dirs", "rt_query", "rt_selftest_fx"):
         getattr(L, name).restype = _int

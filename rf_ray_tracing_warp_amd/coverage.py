@@ -180,6 +180,51 @@ class Coverage:
                   "rt_coverage_records")
         return keys[:n], sums[:n], [int(c) for c in counts]
 
+    def trace_rows(self, tx_pos, tx_power=1):
+        """trace_records with every record as one (n, 4) int64 row (key, sum words 0..2): the
+        layout exchange_rows sends as it is and power_from_rows takes (no packing copies on either
+        side of the all-to-all).  Returns (rows, counts); rows is a view of this plan's buffer,
+        overwritten by its next call."""
+        import torch
+
+        if self.shard_mode != "rays":
+            raise _lib.RfrtError("trace_rows needs shard_mode='rays'")
+        tx = np.ascontiguousarray(np.asarray(tx_pos, dtype=np.float64).astype(np.float32))
+        counts = np.zeros(self.shard_count, np.int64)
+        stats = np.zeros(3, np.int64)
+        dev = f"cuda:{self.device}"
+        if getattr(self, "_rows", None) is None:
+            self._rows = torch.empty((max(self.ray_count * 2, 1 << 16), 4), dtype=torch.int64, device=dev)
+        for attempt in range(2):
+            rows = self._rows
+            check(lib().rt_coverage_trace_records_packed(
+                self._h, tx.ctypes.data, float(tx_power), float(self.light_speed_mps), float(self.sample_rate_hz),
+                cir_flags(self.light_speed_mps, self.sample_rate_hz), self.n_bins, ptr(rows), rows.shape[0],
+                counts.ctypes.data, stats.ctypes.data, _lib.stream_handle(self.device)),
+                "rt_coverage_trace_records_packed")
+            n = int(counts.sum())
+            if stats[2] or n == 0:
+                break
+            # more records than the buffer holds: grow it and trace again (the plan keeps no
+            # packed copy to fetch; this happens once per plan at most)
+            self._rows = torch.empty((n + n // 4 + 1024, 4), dtype=torch.int64, device=dev)
+        self.last_candidates = int(stats[0])
+        return rows[:n], [int(c) for c in counts]
+
+    def power_from_rows(self, rows, counts):
+        """power_from_records for (n, 4) int64 rows of trace_rows' layout arriving as consecutive
+        segments, counts[t] rows from rank t (exchange_rows' output)."""
+        n = int(rows.shape[0]) if rows.dim() == 2 else 0
+        if n and (tuple(rows.shape) != (n, 4) or not rows.is_contiguous()):
+            raise ValueError(f"rows must be a contiguous (n, 4) int64 tensor, got {tuple(rows.shape)}")
+        c = np.ascontiguousarray(np.asarray(counts, dtype=np.int64))
+        if int(c.sum()) != n or (c < 0).any():
+            raise ValueError(f"segment counts {c.tolist()} do not add up to the {n} rows")
+        check(lib().rt_coverage_power_packed(self._h, ptr(rows) if n else None, c.ctypes.data, len(c), self.n_bins,
+                                             phase_step(self.sample_window_s, self.n_bins), ptr(self.power),
+                                             _lib.stream_handle(self.device)), "rt_coverage_power_packed")
+        return self.power
+
     def power_from_records(self, keys, sums, counts=None):
         """Ray mode, last stage: the power of this rank's cells from the records every rank sent it
         (keys and (n, 3) fixed-point sums); the (num_cells,) float64 device map, 0 elsewhere.
@@ -218,10 +263,10 @@ class Coverage:
 
     def _run_device(self, tx_pos, tx_power, process_group):
         if self.shard_mode == "rays":
-            keys, sums, counts = self.trace_records(tx_pos, tx_power)
+            rows, counts = self.trace_rows(tx_pos, tx_power)
             if self.shard_count > 1:
-                keys, sums, counts = rdist.exchange_records(keys, sums, counts, process_group, return_counts=True)
-            return self.power_from_records(keys, sums, counts)
+                rows, counts = rdist.exchange_rows(rows, counts, process_group)
+            return self.power_from_rows(rows, counts)
         tx = np.ascontiguousarray(np.asarray(tx_pos, dtype=np.float64).astype(np.float32))
         stats = np.zeros(2, np.int64)
         check(lib().rt_coverage_run(self._h, tx.ctypes.data, float(tx_power), float(self.light_speed_mps),

@@ -1219,20 +1219,20 @@ struct SegOffsets {
   int64_t off[kMaxSegs + 1];
   int nseg;
 };
-__global__ __launch_bounds__(256) void k_merge_segments(const uint64_t* keys, SegOffsets so, uint64_t* keys_out,
-                                                        int64_t* idx_out) {
+__global__ __launch_bounds__(256) void k_merge_segments(const uint64_t* keys, int64_t kstride, SegOffsets so,
+                                                        uint64_t* keys_out, int64_t* idx_out) {
   const int64_t n = so.off[so.nseg];
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     int sg = 0;
     while (sg + 1 < so.nseg && so.off[sg + 1] <= i) ++sg;
-    const uint64_t k = keys[i];
+    const uint64_t k = keys[i * kstride];
     int64_t pos = i - so.off[sg];
     for (int t = 0; t < so.nseg; ++t) {
       if (t == sg) continue;
       int64_t a = so.off[t], b = so.off[t + 1];  // first element > k (t < sg) or >= k (t > sg)
       while (a < b) {
         const int64_t m = (a + b) >> 1;
-        const uint64_t km = keys[m];
+        const uint64_t km = keys[m * kstride];
         if (km < k || (t < sg && km == k)) a = m + 1;
         else b = m;
       }
@@ -1885,9 +1885,13 @@ struct AmpVal {  // sorted replay records: f64 amplitudes
   __device__ __forceinline__ Fx192 operator()(int64_t i) const { return fx_from_double(a[i]); }
 };
 struct SumVal {  // received records: fixed-point sums, in sorted-index order
-  const Fx192* sums;
+  const uint64_t* words;  // sum of record j at words[j * stride .. + 2]
   const int64_t* idx;
-  __device__ __forceinline__ Fx192 operator()(int64_t i) const { return sums[idx[i]]; }
+  int64_t stride = 3;     // 3: an Fx192 array; 4: packed (key, sum) rows, words = rows + 1
+  __device__ __forceinline__ Fx192 operator()(int64_t i) const {
+    const uint64_t* q = words + idx[i] * stride;
+    return Fx192{q[0], q[1], q[2]};
+  }
 };
 
 __global__ __launch_bounds__(256) void k_run_flags(const uint64_t* keys, int64_t n, int32_t* flags) {
@@ -2363,15 +2367,25 @@ __global__ __launch_bounds__(256) void k_owner_bounds(const uint64_t* ukeys, con
 
 // as k_strip_owner, before the host knows the count: n = bounds[world] on the device, and nothing
 // is written when it exceeds the caller's capacity
+// (packed = 1: one (key, sum) row of 4 words per record at out, sums_out unused)
 __global__ __launch_bounds__(256) void k_strip_owner_dev(const uint64_t* ukeys, const Fx192* usums, const int64_t* bounds,
                                                          int world, int64_t cap, int shift, uint64_t* out,
-                                                         Fx192* sums_out) {
+                                                         Fx192* sums_out, int packed) {
   const int64_t n = bounds[world];
   if (n > cap) return;
   const uint64_t mask = (1ull << shift) - 1;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    out[i] = ukeys[i] & mask;
-    sums_out[i] = usums[i];
+    const uint64_t k = ukeys[i] & mask;
+    const Fx192 v = usums[i];
+    if (packed) {
+      typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+      u64x2* row = reinterpret_cast<u64x2*>(out + 4 * i);  // 32-B rows: two 16-B stores
+      row[0] = u64x2{k, v.w0};
+      row[1] = u64x2{v.w1, v.w2};
+    } else {
+      out[i] = k;
+      sums_out[i] = v;
+    }
   }
 }
 // the reduced records of a ray-sharded plan into the caller's send buffers: keys without the owner
@@ -2693,7 +2707,7 @@ int cov_reduce_sums(rt_coverage* c, const uint64_t* keys, const Fx192* sums, int
   size_t tb = c->tmp_bytes;
   RT_HIP(sort_records(c->tmp, tb, keys, c->okeys_sorted, (const int64_t*)idx, idx_sorted, n,
                       sort_bits < 64 ? sort_bits : 64, s));
-  return run_sums(c, SumVal{sums, idx_sorted}, n, wk, s);
+  return run_sums(c, SumVal{(const uint64_t*)sums, idx_sorted}, n, wk, s);
 }
 
 // Closed-form signal power of this plan's cells from the reduced records in c->ukeys / c->uamps
@@ -2885,11 +2899,39 @@ int rt_coverage_trace_records(rt_coverage* c, const float* tx_pos, double tx_pow
   return rc;
 }
 
+namespace {
+int trace_records_impl(rt_coverage* c, const float* tx_pos, double tx_power, double light_speed, double sample_rate,
+                       int flags, int64_t n_bins, uint64_t* keys_out, uint64_t* sums_out, bool packed,
+                       int64_t max_out, int64_t* counts, int64_t* stats, void* stream);
+}
+
 int rt_coverage_trace_records_to(rt_coverage* c, const float* tx_pos, double tx_power, double light_speed,
                                  double sample_rate, int flags, int64_t n_bins, uint64_t* keys_out, uint64_t* sums_out,
                                  int64_t max_out, int64_t* counts, int64_t* stats, void* stream) {
-  if (!c || !c->ray_mode || !tx_pos || !counts || n_bins < 1 || n_bins >= ((int64_t)1 << 32) ||
-      ((keys_out || sums_out) && (!keys_out || !sums_out || max_out < 0))) {
+  if ((keys_out || sums_out) && (!keys_out || !sums_out || max_out < 0)) {
+    rt::set_error("rt_coverage_trace_records: invalid arguments (keys_out and sums_out go together)");
+    return RT_EINVAL;
+  }
+  return trace_records_impl(c, tx_pos, tx_power, light_speed, sample_rate, flags, n_bins, keys_out, sums_out, false,
+                            max_out, counts, stats, stream);
+}
+
+int rt_coverage_trace_records_packed(rt_coverage* c, const float* tx_pos, double tx_power, double light_speed,
+                                     double sample_rate, int flags, int64_t n_bins, uint64_t* rows_out,
+                                     int64_t max_out, int64_t* counts, int64_t* stats, void* stream) {
+  if (!rows_out || max_out < 0 || (reinterpret_cast<uintptr_t>(rows_out) & 15)) {
+    rt::set_error("rt_coverage_trace_records_packed: invalid arguments (16-B aligned rows_out, max_out >= 0)");
+    return RT_EINVAL;
+  }
+  return trace_records_impl(c, tx_pos, tx_power, light_speed, sample_rate, flags, n_bins, rows_out, nullptr, true,
+                            max_out, counts, stats, stream);
+}
+
+namespace {
+int trace_records_impl(rt_coverage* c, const float* tx_pos, double tx_power, double light_speed, double sample_rate,
+                       int flags, int64_t n_bins, uint64_t* keys_out, uint64_t* sums_out, bool packed,
+                       int64_t max_out, int64_t* counts, int64_t* stats, void* stream) {
+  if (!c || !c->ray_mode || !tx_pos || !counts || n_bins < 1 || n_bins >= ((int64_t)1 << 32)) {
     rt::set_error("rt_coverage_trace_records: invalid arguments (needs a plan from rt_coverage_create_rays)");
     return RT_EINVAL;
   }
@@ -2914,7 +2956,7 @@ int rt_coverage_trace_records_to(rt_coverage* c, const float* tx_pos, double tx_
     if (keys_out)  // the send buffers are filled before the host synchronizes (no launch after it)
       hipLaunchKernelGGL(k_strip_owner_dev, dim3((unsigned)std::min<int64_t>((nlist + 255) / 256, 4096)), dim3(256), 0,
                          s, c->ukeys, plan_sums(c), c->bounds, world, max_out, own_shift(c), keys_out,
-                         (Fx192*)sums_out);
+                         (Fx192*)sums_out, packed ? 1 : 0);
     RT_HIP(hipGetLastError());
     prof_mark(c, 7, s);
     RT_HIP(hipMemcpyAsync(b.data(), c->bounds, sizeof(int64_t) * (world + 1), hipMemcpyDeviceToHost, s));
@@ -2929,6 +2971,7 @@ int rt_coverage_trace_records_to(rt_coverage* c, const float* tx_pos, double tx_
   }
   return RT_OK;
 }
+}  // namespace
 
 int rt_coverage_records(rt_coverage* c, uint64_t* keys_out, uint64_t* sums_out, int64_t max_out, void* stream) {
   if (!c || !c->ray_mode || (c->n_out > 0 && (!keys_out || !sums_out)) || max_out < c->n_out) {
@@ -2994,8 +3037,25 @@ int rt_coverage_power_records(rt_coverage* c, const uint64_t* keys, const uint64
   return rc;
 }
 
+namespace {
+int power_segments_impl(rt_coverage* c, const uint64_t* keys, const uint64_t* sums, int64_t stride,
+                        const int64_t* seg_counts, int nseg, int64_t n_bins, double alpha, double* power, void* stream);
+}
+
 int rt_coverage_power_segments(rt_coverage* c, const uint64_t* keys, const uint64_t* sums, const int64_t* seg_counts,
                                int nseg, int64_t n_bins, double alpha, double* power, void* stream) {
+  return power_segments_impl(c, keys, sums, 1, seg_counts, nseg, n_bins, alpha, power, stream);
+}
+
+int rt_coverage_power_packed(rt_coverage* c, const uint64_t* rows, const int64_t* seg_counts, int nseg, int64_t n_bins,
+                             double alpha, double* power, void* stream) {
+  return power_segments_impl(c, rows, rows ? rows + 1 : nullptr, 4, seg_counts, nseg, n_bins, alpha, power, stream);
+}
+
+namespace {
+// stride 1: keys[n] and Fx192 sums[n]; stride 4: (key, sum) rows, keys = rows, sums = rows + 1
+int power_segments_impl(rt_coverage* c, const uint64_t* keys, const uint64_t* sums, int64_t stride,
+                        const int64_t* seg_counts, int nseg, int64_t n_bins, double alpha, double* power, void* stream) {
   if (!c || !c->ray_mode || nseg < 1 || nseg > kMaxSegs || !seg_counts || !power || n_bins < 1 ||
       n_bins >= ((int64_t)1 << 32)) {
     rt::set_error("rt_coverage_power_segments: invalid arguments (1 <= nseg <= 64)");
@@ -3026,11 +3086,11 @@ int rt_coverage_power_segments(rt_coverage* c, const uint64_t* keys, const uint6
     if ((rc = grow_for(c, n))) return rc;
     int64_t* idx_sorted = reinterpret_cast<int64_t*>(c->oamps_sorted);
     hipLaunchKernelGGL(k_merge_segments, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 8192)), dim3(256), 0, s, keys,
-                       so, c->okeys_sorted, idx_sorted);
+                       stride, so, c->okeys_sorted, idx_sorted);
     RT_HIP(hipGetLastError());
     WideKey wk{};
     wk.identity = true;
-    rc = run_sums(c, SumVal{(const Fx192*)sums, idx_sorted}, n, wk, s);
+    rc = run_sums(c, SumVal{sums, idx_sorted, stride == 1 ? 3 : stride}, n, wk, s);
   } else {
     RT_HIP(hipMemsetAsync(c->nuniq, 0, 8, s));
   }
@@ -3038,6 +3098,7 @@ int rt_coverage_power_segments(rt_coverage* c, const uint64_t* keys, const uint6
   if (!rc) prof_mark(c, 7, s);
   return rc;
 }
+}  // namespace
 
 int rt_coverage_profile(rt_coverage* c, int enable) {
   if (!c) {

@@ -105,6 +105,27 @@ def reduce_max(value: float, device, group=None) -> float:
     return value
 
 
+def exchange_rows(rows, send_counts, group=None):
+    """Sparse all-to-all of packed coverage records: rows (n, w) int64 grouped by destination rank,
+    send_counts[d] rows for rank d (Coverage.trace_rows).  One collective for the counts, one for
+    the rows, nothing packed or unpacked around them.  Returns (received rows, in source-rank order;
+    the number of rows from each rank)."""
+    import torch
+    import torch.distributed as dist
+    home = rows.device
+    wire = torch.device("cpu") if (home.type != "cpu" and dist.get_backend(group) == "gloo") else home
+    send_counts = [int(c) for c in send_counts]
+    n = sum(send_counts)
+    w = int(rows.shape[1]) if rows.dim() == 2 else 4
+    sc = torch.tensor(send_counts, dtype=torch.int64, device=wire)
+    rc = torch.empty_like(sc)
+    dist.all_to_all_single(rc, sc, group=group)
+    recv_counts = [int(c) for c in rc.tolist()]
+    out = torch.empty((sum(recv_counts), w), dtype=torch.int64, device=wire)
+    dist.all_to_all_single(out, rows[:n].reshape(n, w).to(wire), recv_counts, send_counts, group=group)
+    return out.to(home), recv_counts
+
+
 def exchange_records(keys, vals, send_counts, group=None, return_counts=False):
     """Sparse all-to-all of coverage records: this rank's (key, value) pairs, grouped by
     destination rank with send_counts[d] for rank d, go to their owners.  vals is (n,) float64

@@ -116,6 +116,9 @@ def _a2a_worker(rank, world, port, out):
     k3, s3 = rdist.exchange_records(keys, sums, counts)
     assert k3.tolist() == k.tolist() and s3.shape == (len(k), 3)
     assert s3[:, 0].tolist() == k.tolist() and (s3[:, 1] == 3 * s3[:, 0]).all() and (s3[:, 2] == -s3[:, 0]).all()
+    r4, rc = rdist.exchange_rows(torch.cat([keys.reshape(-1, 1), sums], dim=1), counts)
+    assert r4[:, 0].tolist() == k.tolist() and r4[:, 1:].tolist() == s3.tolist()
+    assert rc == [r + rank + 1 for r in range(world)]
     out.put((rank, k.tolist(), a.tolist()))
     dist.destroy_process_group()
 
@@ -185,6 +188,11 @@ def _a2a_empty_worker(rank, world, port, out):
     amps = keys.to(torch.float64) / 3.0
     k, s = rdist.exchange_records(keys, sums, counts)
     k1, a1 = rdist.exchange_records(keys, amps, counts)
+    # the packed rows of Coverage.trace_rows: (n, 4) int64, sent as they are
+    rows = torch.cat([keys.reshape(-1, 1), sums], dim=1) if n else torch.empty((0, 4), dtype=torch.int64)
+    r4, rc = rdist.exchange_rows(rows, counts)
+    assert r4.shape == (len(k), 4) and r4[:, 0].tolist() == k.tolist() and r4[:, 1:].tolist() == s.tolist()
+    assert rc == [0] + [2] * (world - 1)
     out.put((rank, k.tolist(), s.tolist(), k1.tolist(), a1.tolist()))
     dist.destroy_process_group()
 

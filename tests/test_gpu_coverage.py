@@ -139,6 +139,30 @@ def test_coverage_on_bvh_terrain():
     cov.close()
 
 
+def _ray_sharded_rows(env, grid, tx, B, N, S, win=100e-9, env_mesh=None):
+    """_ray_sharded through the packed path run() takes: trace_rows -> each owner's segments of
+    (key, sum) rows in source-rank order -> power_from_rows."""
+    plans = [Coverage(env, 2.998e8, 100e9, win, B, N, grid, shard_index=r, shard_count=S, shard_mode="rays",
+                      env_mesh=env_mesh) for r in range(S)]
+    sent = []
+    for p in plans:
+        rows, counts = p.trace_rows(tx, 1)
+        sent.append((rows.clone(), counts))
+    total = torch.zeros(grid.num_cells, dtype=torch.float64, device="cuda")
+    irs = []
+    for d, p in enumerate(plans):
+        parts, segs = [], []
+        for rows, counts in sent:
+            off = sum(counts[:d])
+            parts.append(rows[off:off + counts[d]])
+            segs.append(counts[d])
+        total += p.power_from_rows(torch.cat(parts), segs)
+        irs.append(p.impulse_responses())
+    for p in plans:
+        p.close()
+    return total.cpu().numpy(), irs
+
+
 def _ray_sharded(env, grid, tx, B, N, S, win=100e-9, env_mesh=None, segments=False):
     """S ray-mode plans in one process: each traces its share of the rays for every cell, the
     records are routed to their owners as the all-to-all would (source-rank order), every owner
@@ -199,6 +223,38 @@ def test_power_segments_equal_sorted_records(room, S):
     for a, b in zip(irs_sort, irs_merge):
         for x, y in zip(a, b):
             assert x.tobytes() == y.tobytes()
+
+
+@pytest.mark.parametrize("S", [1, 3, 8])
+def test_packed_rows_equal_records(room, S):
+    """trace_rows / power_from_rows (one 32-B row per record, sent as it is) give exactly the
+    maps and impulse responses of the separate key and sum buffers."""
+    grid, tx, B, N = CoverageGrid(8.0, -2.5, 4.6, 0.37, 0.41, 0.4, 13, 12, 2), (10, 0, 5), 3, 60_000
+    t_rec, irs_rec = _ray_sharded(room, grid, tx, B, N, S, segments=True)
+    t_rows, irs_rows = _ray_sharded_rows(room, grid, tx, B, N, S)
+    assert t_rec.tobytes() == t_rows.tobytes()
+    assert np.isfinite(t_rec).sum() >= 20
+    for a, b in zip(irs_rec, irs_rows):
+        for x, y in zip(a, b):
+            assert x.tobytes() == y.tobytes()
+
+
+def test_trace_rows_match_records_and_grow(room):
+    """trace_rows holds the same (key, sum) records as trace_records, row by row; a buffer too small
+    for them is grown and the trace repeated, with the same rows."""
+    grid, tx, B, N = CoverageGrid(8.0, -2.5, 4.6, 0.37, 0.41, 0.4, 13, 12, 2), (10, 0, 5), 3, 60_000
+    p = Coverage(room, 2.998e8, 100e9, 100e-9, B, N, grid, shard_index=2, shard_count=3, shard_mode="rays")
+    k, sm, c = p.trace_records(tx, 1)
+    k, sm = k.cpu().numpy(), sm.cpu().numpy()
+    rows, c2 = p.trace_rows(tx, 1)
+    r = rows.cpu().numpy()
+    assert c == c2 and sum(c) > 100
+    assert r[:, 0].tobytes() == k.tobytes() and np.ascontiguousarray(r[:, 1:]).tobytes() == sm.tobytes()
+    p._rows = torch.empty((1, 4), dtype=torch.int64, device="cuda")
+    rows3, c3 = p.trace_rows(tx, 1)
+    assert c3 == c and p._rows.shape[0] > 1
+    assert rows3.cpu().numpy().tobytes() == r.tobytes()
+    p.close()
 
 
 def test_coverage_ray_sharded_vs_oracle(room):

@@ -67,12 +67,26 @@ def rays_case(case, m, grid, tx, win, B, env, S, reps):
     best = None
     for _ in range(reps + 1):  # first pass warms up
         sent, t_trace = [], []
+        rows_path = not os.environ.get("RECORDS") and not os.environ.get("OWNER_SORT")
         for p in plans:
-            out, dt = timed(lambda: p.trace_records(tx, 1))
+            # run()'s path: packed (key, sum) rows (RECORDS=1: separate key and sum buffers)
+            out, dt = timed(lambda: p.trace_rows(tx, 1) if rows_path else p.trace_records(tx, 1))
             sent.append(out)
             t_trace.append(dt)
         t_own, nrec = [], []
         for d, p in enumerate(plans):
+            if rows_path:
+                parts, segs = [], []
+                for rows, counts in sent:
+                    off = sum(counts[:d])
+                    parts.append(rows[off:off + counts[d]])
+                    segs.append(counts[d])
+                r = torch.cat(parts)
+                nrec.append(int(r.shape[0]))
+                # the received rows as exchange_rows delivers them: one sorted segment per source
+                _, dt = timed(lambda: p.power_from_rows(r, segs))
+                t_own.append(dt)
+                continue
             ks, as_, segs = [], [], []
             for keys, amps, counts in sent:
                 off = sum(counts[:d])
@@ -86,7 +100,7 @@ def rays_case(case, m, grid, tx, win, B, env, S, reps):
             t_own.append(dt)
         per_rank = [a + b for a, b in zip(t_trace, t_own)]
         if best is None or max(per_rank) < max(best[0]):
-            best = (per_rank, t_trace, t_own, nrec, [sum(c) for _, _, c in sent])
+            best = (per_rank, t_trace, t_own, nrec, [sum(x[-1]) for x in sent])
     per_rank, t_trace, t_own, nrec, nsent = best
     print(json.dumps({"case": case, "mode": "rays", "shards": S, "ms_per_map_max_rank": max(per_rank) * 1e3,
                       "ms_trace_stage": [round(x * 1e3, 3) for x in t_trace],
