@@ -194,7 +194,7 @@ class Coverage:
         stats = np.zeros(3, np.int64)
         dev = f"cuda:{self.device}"
         if getattr(self, "_rows", None) is None:
-            self._rows = torch.empty((max(self.ray_count * 2, 1 << 16), 4), dtype=torch.int64, device=dev)
+            self._rows = torch.empty((max(self.ray_count * 4, 1 << 16), 4), dtype=torch.int64, device=dev)
         for attempt in range(2):
             rows = self._rows
             check(lib().rt_coverage_trace_records_packed(
