@@ -1,4 +1,4 @@
-"""Summarize a tools/prof_r2.sh run (gpurun_out/prof_<TAG>/{stats,p1..}) into profiles/:
+"""Summarize a tools/gpu.sh stats + pmc run (gpurun_out/prof_<TAG>/{stats,p1..}) into profiles/:
 
   <tag>_kernel_stats.csv   rocprofv3 --stats of the trace pass (average duration per kernel)
   <tag>_pmc.json           per-launch means of every PMC counter for the kernels of the hot path,
@@ -75,7 +75,7 @@ def main(tag, note=""):
         shutil.copy(stats[0], os.path.join(ROOT, "profiles", f"{tag}_kernel_stats.csv"))
     pmc, dur = counters(base), durations(base)
     out = {"tag": tag, "note": note,
-           "how": "rocprofv3 --kernel-trace --stats pass + one --pmc pass per counter group (tools/prof_r2.sh); "
+           "how": "rocprofv3 --kernel-trace --stats pass + one --pmc pass per counter group (tools/gpu.sh stats, pmc); "
                   "means per dispatch; HBM bytes = (2 x FETCH_SIZE + WRITE_SIZE) KB x 1024",
            "kernels": {}}
     for k in sorted(set(pmc) | set(dur)):
@@ -104,7 +104,7 @@ def main(tag, note=""):
                    "algorithmic_bytes_per_launch": 1_000_000 * (24 * 4 + 4), "tag": tag},
                   open(os.path.join(ROOT, "profiles", "traffic_k2.json"), "w"), indent=1)
         if "SQ_INSTS_VALU" in c:
-            json.dump(dict(c, source=f"profiles/{tag}_pmc.json (k_trace_bf<3, false>, tools/prof_r2.sh)"),
+            json.dump(dict(c, source=f"profiles/{tag}_pmc.json (k_trace_bf<3, false>, tools/gpu.sh pmc)"),
                       open(os.path.join(ROOT, "profiles", "k2_sq_counters.json"), "w"), indent=1)
     for k, v in out["kernels"].items():
         print(f"{k:18s} avg {v['avg_us'] or 0:9.1f} us  HBM {v.get('hbm_bytes_per_launch', 0) / 1e6:8.2f} MB  "
