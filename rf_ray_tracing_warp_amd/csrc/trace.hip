@@ -100,7 +100,11 @@ __device__ __forceinline__ bool rx_maybe(const TraceArgs& a, float3 o, float3 d,
 
 // Row stores of the register-resident kernels.  RT_NT_ROWS: non-temporal (streaming) stores --
 // the rows are written once and not read back by this step, so they need not sit dirty in L2
-// until the end-of-kernel writeback.
+// until the end-of-kernel writeback.  Brute-force kernels only: there a wave's rows are
+// consecutive, so its stores fill whole lines.  The BVH kernels write direction-sorted rows at
+// scattered row indices, every 72-B row a few partial lines; streaming stores sent each piece to
+// memory on its own (1.0 GB written per K4 launch for 0.31 GB of rows), while ordinary stores let
+// L2 merge a row's pieces first: 0.47 GB, and the K4 kernel 1230 -> 880 us (profiles/r3s_*).
 #ifndef RT_NT_ROWS
 #define RT_NT_ROWS 1
 #endif
@@ -114,7 +118,7 @@ __device__ __forceinline__ bool rx_maybe(const TraceArgs& a, float3 o, float3 d,
 #ifndef RT_XCD_WINDOWS
 #define RT_XCD_WINDOWS 0
 #endif
-template <int P>
+template <int P, bool NT = (RT_NT_ROWS != 0)>
 __device__ __forceinline__ void store_row_fixed(float* dst, const float (*pts)[3]) {
   if constexpr ((P * 3) % 4 == 0) {  // 16-B aligned rows (P = 4, 8): 16-byte stores
     typedef float f4v __attribute__((ext_vector_type(4)));
@@ -124,11 +128,8 @@ __device__ __forceinline__ void store_row_fixed(float* dst, const float (*pts)[3
       const int i = 4 * j;
       const f4v v = {pts[i / 3][i % 3], pts[(i + 1) / 3][(i + 1) % 3], pts[(i + 2) / 3][(i + 2) % 3],
                      pts[(i + 3) / 3][(i + 3) % 3]};
-#if RT_NT_ROWS
-      __builtin_nontemporal_store(v, d4 + j);
-#else
-      d4[j] = v;
-#endif
+      if constexpr (NT) __builtin_nontemporal_store(v, d4 + j);
+      else d4[j] = v;
     }
   } else if constexpr (RT_ROW_X2 && (P * 3) % 2 == 0) {  // 8-B aligned rows (P = 2, 6): 8-byte stores
     typedef float f2v __attribute__((ext_vector_type(2)));
@@ -137,20 +138,14 @@ __device__ __forceinline__ void store_row_fixed(float* dst, const float (*pts)[3
     for (int j = 0; j < P * 3 / 2; ++j) {
       const int i = 2 * j;
       const f2v v = {pts[i / 3][i % 3], pts[(i + 1) / 3][(i + 1) % 3]};
-#if RT_NT_ROWS
-      __builtin_nontemporal_store(v, d2 + j);
-#else
-      d2[j] = v;
-#endif
+      if constexpr (NT) __builtin_nontemporal_store(v, d2 + j);
+      else d2[j] = v;
     }
   } else {
 #pragma unroll
     for (int i = 0; i < P * 3; ++i) {
-#if RT_NT_ROWS
-      __builtin_nontemporal_store(pts[i / 3][i % 3], dst + i);
-#else
-      dst[i] = pts[i / 3][i % 3];
-#endif
+      if constexpr (NT) __builtin_nontemporal_store(pts[i / 3][i % 3], dst + i);
+      else dst[i] = pts[i / 3][i % 3];
     }
   }
 }
@@ -412,6 +407,7 @@ __device__ __forceinline__ int64_t xcd_chunk(int win_chunks, int64_t nchunks, in
 template <int B, bool USE_BVH>
 __device__ __forceinline__ void trace_body(const TraceArgs& a) {
   constexpr int P = B + 1;
+  constexpr bool kNtRows = RT_NT_ROWS && !USE_BVH;  // see store_row_fixed
   extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
   float4* cone = lds_tab + (size_t)a.env_nf * 18;  // bounce-0 edge normals after the face table
   const bool use_cone = RT_CONE && !USE_BVH && a.env_nf <= kConeMaxFaces;
@@ -494,9 +490,9 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
     if (a.traced) {
       if constexpr (P == 4) {
         if (wave_rows) store_rows_wave4(a.traced + (row - (threadIdx.x & 63)) * (P * 3), path);
-        else store_row_fixed<P>(a.traced + row * (P * 3), path);
+        else store_row_fixed<P, kNtRows>(a.traced + row * (P * 3), path);
       } else {
-        store_row_fixed<P>(a.traced + row * (P * 3), path);
+        store_row_fixed<P, kNtRows>(a.traced + row * (P * 3), path);
       }
     }
     if (a.received) {
@@ -510,17 +506,14 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
       }
       if constexpr (P == 4) {
         if (wave_rows) store_rows_wave4(a.received + (row - (threadIdx.x & 63)) * (P * 3), rec);
-        else store_row_fixed<P>(a.received + row * (P * 3), rec);
+        else store_row_fixed<P, kNtRows>(a.received + row * (P * 3), rec);
       } else {
-        store_row_fixed<P>(a.received + row * (P * 3), rec);
+        store_row_fixed<P, kNtRows>(a.received + row * (P * 3), rec);
       }
     }
     if (a.mask) {
-#if RT_NT_ROWS
-      __builtin_nontemporal_store(last_rx >= 0 ? 1u : 0u, a.mask + row);
-#else
-      a.mask[row] = last_rx >= 0 ? 1u : 0u;
-#endif
+      if constexpr (kNtRows) __builtin_nontemporal_store(last_rx >= 0 ? 1u : 0u, a.mask + row);
+      else a.mask[row] = last_rx >= 0 ? 1u : 0u;
     }
     got = last_rx >= 0;
     }
@@ -882,7 +875,7 @@ __global__ __launch_bounds__(256) void k_wf_rows(WfArgs w) {
       path[k][1] = q.y;
       path[k][2] = q.z;
     }
-    if (a.traced) store_row_fixed<P>(a.traced + row * (P * 3), path);
+    if (a.traced) store_row_fixed<P, false>(a.traced + row * (P * 3), path);
     if (a.received) {
       float rec[P][3];
 #pragma unroll
@@ -892,7 +885,7 @@ __global__ __launch_bounds__(256) void k_wf_rows(WfArgs w) {
         rec[i][1] = keep ? path[i][1] : qnan;
         rec[i][2] = keep ? path[i][2] : qnan;
       }
-      store_row_fixed<P>(a.received + row * (P * 3), rec);
+      store_row_fixed<P, false>(a.received + row * (P * 3), rec);
     }
     if (a.mask) a.mask[row] = lr >= 0 ? 1u : 0u;
     for (int b = np; b < B; ++b) {  // bounces after the miss repeat it: kind 0, no face
