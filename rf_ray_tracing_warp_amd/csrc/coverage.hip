@@ -945,6 +945,9 @@ __device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab
       rec_dist = acc.dist;  // received_paths = traced prefix through this point (kernel.py:89-90)
       rec_amp = acc.amp;
     } else if (env_hit) {
+      // after the last bounce only a receiver hit could still change the record: an environment
+      // hit there ends the path, its vertex (and its angle's f64 amplitude) unused
+      if (b + 1 >= p.B) break;
       pos.x = fmaf(d.x, he.t, pos.x);
       pos.y = fmaf(d.y, he.t, pos.y);
       pos.z = fmaf(d.z, he.t, pos.z);
@@ -3085,6 +3088,8 @@ int power_segments_impl(rt_coverage* c, const uint64_t* keys, const uint64_t* su
   if (n > 0) {
     if ((rc = grow_for(c, n))) return rc;
     int64_t* idx_sorted = reinterpret_cast<int64_t*>(c->oamps_sorted);
+    // (G lanes per element, one binary search each, then a group sum: no faster on K3's 200k
+    // records, 46 -> 76 us on K5's 465k -- the searches' loads, not their latency, set the time)
     hipLaunchKernelGGL(k_merge_segments, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 8192)), dim3(256), 0, s, keys,
                        stride, so, c->okeys_sorted, idx_sorted);
     RT_HIP(hipGetLastError());
