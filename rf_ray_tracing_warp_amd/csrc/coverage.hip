@@ -924,17 +924,19 @@ __device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab
   for (int b = k0 + 1; b < p.B; ++b) {  // kernel.py:57-98 with this cell's receiver
     const rt::Shear s = rt::make_shear(pos, d);
     rt::Hit he, hr;
+    // receiver first: at the last bounce only a receiver hit can still change the record, so a
+    // miss there ends the path without the environment query (K3: most first wins at bounce 0
+    // leave their receiver at bounce 1 and miss it at bounce 2)
+    hr = USE_BVH ? rx_query_v<RT_COV_RXQ_BVH>(L, p.g, cell, p.r_rx, pos, d)
+                 : rx_query_v<RT_COV_RXQ>(L, p.g, cell, p.r_rx, pos, d);
+    if (hr.face < 0 && b + 1 >= p.B) break;
     if constexpr (RX_FIRST) {
-      // receiver first, then the environment culled at the receiver's t: every environment hit
-      // with t <= hr.t is still found exactly (rt_bvh.h), and one beyond it loses to the receiver
-      // whatever it is (kernel.py:85), so the decision and the chosen hit are unchanged
-      hr = USE_BVH ? rx_query_v<RT_COV_RXQ_BVH>(L, p.g, cell, p.r_rx, pos, d)
-                   : rx_query_v<RT_COV_RXQ>(L, p.g, cell, p.r_rx, pos, d);
+      // the environment culled at the receiver's t: every environment hit with t <= hr.t is
+      // still found exactly (rt_bvh.h), and one beyond it loses to the receiver whatever it is
+      // (kernel.py:85), so the decision and the chosen hit are unchanged
       he = env_query<USE_BVH>(p, lds_tab, s, pos, d, hr.face >= 0 ? hr.t : RT_MAX_T);
     } else {
       he = env_query<USE_BVH>(p, lds_tab, s, pos, d);
-      hr = USE_BVH ? rx_query_v<RT_COV_RXQ_BVH>(L, p.g, cell, p.r_rx, pos, d)
-                   : rx_query_v<RT_COV_RXQ>(L, p.g, cell, p.r_rx, pos, d);
     }
     const bool env_hit = he.face >= 0, rx_hit = hr.face >= 0;
     if (rx_hit && (!env_hit || he.t > hr.t)) {
@@ -2334,8 +2336,8 @@ int64_t traj_split_max_rays() {
   return v;
 }
 
-// replay query order on BVH scenes: receiver first and the traversal culled at its t (default), or
-// the reference's order, environment then receiver (RFRT_COV_RXFIRST=0, for A/B checks)
+// replay on BVH scenes: the environment traversal culled at the receiver's t (default), or not
+// culled (RFRT_COV_RXFIRST=0, for A/B checks); either way the receiver is queried first
 bool replay_rx_first() {
   static const bool v = [] {
     const char* e = getenv("RFRT_COV_RXFIRST");
