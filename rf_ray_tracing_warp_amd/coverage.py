@@ -100,18 +100,11 @@ class Coverage:
 
     def __init__(self, environment_trimesh, light_speed_mps, sample_rate_hz, sample_window_s, max_bounces,
                  tx_num_rays, grid: CoverageGrid, rx_radius=0.1, device: int | None = None, shard_index: int = 0,
-                 shard_count: int = 1, env_mesh: DeviceMesh | None = None, shard_mode: str = "cells",
-                 sub_plans: int = 1, ray_range=None, stream=None):
+                 shard_count: int = 1, env_mesh: DeviceMesh | None = None, shard_mode: str = "cells"):
         """shard_index / shard_count: this rank of the job.  shard_mode "cells": this rank traces all
         tx_num_rays rays for the cells of its x columns (ix % shard_count == shard_index); "rays":
         it traces its contiguous share of the rays (dist.ray_range) for every cell and exchanges
-        records with the other ranks in run() (dist.exchange_records).
-
-        Ray mode only: sub_plans = K > 1 splits this rank's rays over K plans traced concurrently on
-        K HIP streams (a rank's share is too small to fill the GPU, and each plan's chain of short
-        launches, sorts and host waits then overlaps the others' kernels); each sends its own sorted
-        segment per owner.  ray_range = (offset, count) overrides the rays of this
-        plan, stream (a torch.cuda.Stream) the stream it launches on (default: the current one)."""
+        records with the other ranks in run() (dist.exchange_records)."""
         import torch
 
         if not torch.cuda.is_available():
@@ -130,23 +123,11 @@ class Coverage:
         if shard_mode not in ("cells", "rays"):
             raise ValueError(f"shard_mode must be 'cells' or 'rays', not {shard_mode!r}")
         self.shard_mode = shard_mode
-        self.sub_plans = int(sub_plans)
-        if self.sub_plans < 1 or (self.sub_plans > 1 and shard_mode != "rays"):
-            raise ValueError("sub_plans > 1 needs shard_mode='rays'")
-        if self.sub_plans * self.shard_count > 64:
-            raise ValueError("sub_plans x shard_count must be <= 64 (segments an owner merges)")
-        self._stream = stream
-        self._subs, self._pool = [], None
         self.env = env_mesh or DeviceMesh(environment_trimesh.vertices, environment_trimesh.faces, self.device)
         self._h = _lib._vp()
         g = grid._c()
         if shard_mode == "rays":
-            self.ray_offset, self.ray_count = (rdist.ray_range(self.shard_index, self.shard_count, self.tx_num_rays)
-                                               if ray_range is None else (int(ray_range[0]), int(ray_range[1])))
-            if self.sub_plans > 1:  # this object is sub-plan 0: the first part of the rank's rays
-                parts = [rdist.ray_range(k, self.sub_plans, self.ray_count) for k in range(self.sub_plans)]
-                base = self.ray_offset
-                self.ray_offset, self.ray_count = base + parts[0][0], parts[0][1]
+            self.ray_offset, self.ray_count = rdist.ray_range(self.shard_index, self.shard_count, self.tx_num_rays)
             check(lib().rt_coverage_create_rays(self.device, self.env.handle, self.max_bounces, self.tx_num_rays,
                                                 self.ray_offset, self.ray_count, ctypes.byref(g), self.rx_radius,
                                                 self.shard_index, self.shard_count, ctypes.byref(self._h)),
@@ -159,20 +140,6 @@ class Coverage:
         self.power = torch.empty(grid.num_cells, dtype=torch.float64, device=f"cuda:{self.device}")
         self.last_candidates = 0
         self._rec = None  # ray mode: (keys, sums) record buffers of trace_records
-        if self.sub_plans > 1:
-            from concurrent.futures import ThreadPoolExecutor
-            for k in range(1, self.sub_plans):
-                self._subs.append(Coverage(environment_trimesh, light_speed_mps, sample_rate_hz, sample_window_s,
-                                           max_bounces, tx_num_rays, grid, rx_radius, device=self.device,
-                                           shard_index=self.shard_index, shard_count=self.shard_count,
-                                           env_mesh=self.env, shard_mode="rays",
-                                           ray_range=(base + parts[k][0], parts[k][1]),
-                                           stream=torch.cuda.Stream(device=self.device)))
-            # ctypes releases the GIL for the duration of each call: one host thread per extra plan
-            self._pool = ThreadPoolExecutor(max_workers=self.sub_plans - 1)
-
-    def _sh(self):
-        return self._stream.cuda_stream if self._stream is not None else _lib.stream_handle(self.device)
 
     def trace_records(self, tx_pos, tx_power=1):
         """Ray mode, stage 1: this rank's rays for every cell.  Returns (keys, sums, counts): device
@@ -200,7 +167,7 @@ class Coverage:
                                                  float(self.sample_rate_hz),
                                                  cir_flags(self.light_speed_mps, self.sample_rate_hz), self.n_bins,
                                                  ptr(keys), ptr(sums), keys.numel(), counts.ctypes.data,
-                                                 stats.ctypes.data, self._sh()),
+                                                 stats.ctypes.data, _lib.stream_handle(self.device)),
               "rt_coverage_trace_records_to")
         self.last_candidates = int(stats[0])
         n = int(counts.sum())
@@ -209,7 +176,7 @@ class Coverage:
             m = n + n // 4 + 1024
             self._rec = (torch.empty(m, dtype=torch.int64, device=dev), torch.empty((m, 3), dtype=torch.int64, device=dev))
             keys, sums = self._rec
-            check(lib().rt_coverage_records(self._h, ptr(keys), ptr(sums), n, self._sh()),
+            check(lib().rt_coverage_records(self._h, ptr(keys), ptr(sums), n, _lib.stream_handle(self.device)),
                   "rt_coverage_records")
         return keys[:n], sums[:n], [int(c) for c in counts]
 
@@ -217,31 +184,7 @@ class Coverage:
         """trace_records with every record as one (n, 4) int64 row (key, sum words 0..2): the
         layout exchange_rows sends as it is and power_from_rows takes (no packing copies on either
         side of the all-to-all).  Returns (rows, counts); rows is a view of this plan's buffer,
-        overwritten by its next call.  With sub_plans = K > 1, counts has shard_count * K entries,
-        (owner, sub-plan) in that order: the rows for each owner are K sorted segments, one per
-        sub-plan, gathered owner by owner (exchange_rows(..., segs_per_dest=K) sends them so)."""
-        if not self._subs:
-            return self._trace_rows_one(tx_pos, tx_power)
-        import torch
-        cur = torch.cuda.current_stream(self.device)
-        for sp in self._subs:  # their buffers may still be read by this stream's previous gather
-            sp._stream.wait_stream(cur)
-        futs = [self._pool.submit(sp._trace_rows_one, tx_pos, tx_power) for sp in self._subs]
-        outs = [self._trace_rows_one(tx_pos, tx_power)] + [f.result() for f in futs]
-        self.last_candidates = sum(sp.last_candidates for sp in [self] + self._subs)
-        world, K = self.shard_count, len(outs)
-        offs = [np.concatenate([[0], np.cumsum(c)]) for _, c in outs]
-        parts, counts = [], []
-        for d in range(world):  # owner-major: each owner's K segments side by side
-            for k, (rows, c) in enumerate(outs):
-                if c[d]:
-                    parts.append(rows[int(offs[k][d]):int(offs[k][d + 1])])
-                counts.append(int(c[d]))
-        if not parts:
-            return outs[0][0][:0], counts
-        return (parts[0] if len(parts) == 1 else torch.cat(parts)), counts
-
-    def _trace_rows_one(self, tx_pos, tx_power=1):
+        overwritten by its next call."""
         import torch
 
         if self.shard_mode != "rays":
@@ -257,7 +200,7 @@ class Coverage:
             check(lib().rt_coverage_trace_records_packed(
                 self._h, tx.ctypes.data, float(tx_power), float(self.light_speed_mps), float(self.sample_rate_hz),
                 cir_flags(self.light_speed_mps, self.sample_rate_hz), self.n_bins, ptr(rows), rows.shape[0],
-                counts.ctypes.data, stats.ctypes.data, self._sh()),
+                counts.ctypes.data, stats.ctypes.data, _lib.stream_handle(self.device)),
                 "rt_coverage_trace_records_packed")
             n = int(counts.sum())
             if stats[2] or n == 0:
@@ -322,7 +265,7 @@ class Coverage:
         if self.shard_mode == "rays":
             rows, counts = self.trace_rows(tx_pos, tx_power)
             if self.shard_count > 1:
-                rows, counts = rdist.exchange_rows(rows, counts, process_group, segs_per_dest=self.sub_plans)
+                rows, counts = rdist.exchange_rows(rows, counts, process_group)
             return self.power_from_rows(rows, counts)
         tx = np.ascontiguousarray(np.asarray(tx_pos, dtype=np.float64).astype(np.float32))
         stats = np.zeros(2, np.int64)
@@ -377,12 +320,6 @@ class Coverage:
         return dict(zip(self.PROFILE_KEYS, (float(x) for x in out)))
 
     def close(self):
-        for sp in getattr(self, "_subs", []):
-            sp.close()
-        self._subs = []
-        if getattr(self, "_pool", None) is not None:
-            self._pool.shutdown(wait=True)
-            self._pool = None
         if getattr(self, "_h", None) and self._h.value and _lib._lib is not None:
             _lib._lib.rt_coverage_destroy(self._h)
             self._h = _lib._vp()

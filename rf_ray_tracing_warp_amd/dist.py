@@ -105,33 +105,25 @@ def reduce_max(value: float, device, group=None) -> float:
     return value
 
 
-def exchange_rows(rows, send_counts, group=None, segs_per_dest=1):
+def exchange_rows(rows, send_counts, group=None):
     """Sparse all-to-all of packed coverage records: rows (n, w) int64 grouped by destination rank,
     send_counts[d] rows for rank d (Coverage.trace_rows).  One collective for the counts, one for
     the rows, nothing packed or unpacked around them.  Returns (received rows, in source-rank order;
-    the number of rows from each rank).  segs_per_dest = K: the rows for each destination are K
-    segments and send_counts holds world * K counts, (destination, segment) in that order; the
-    returned counts are then world * K too, (source, segment)."""
+    the number of rows from each rank)."""
     import torch
     import torch.distributed as dist
     home = rows.device
     wire = torch.device("cpu") if (home.type != "cpu" and dist.get_backend(group) == "gloo") else home
-    K = int(segs_per_dest)
-    seg_counts = [int(c) for c in send_counts]
-    world = dist.get_world_size(group)
-    if len(seg_counts) != world * K:
-        raise ValueError(f"{len(seg_counts)} send counts for {world} ranks x {K} segments")
-    send_counts = [sum(seg_counts[d * K:(d + 1) * K]) for d in range(world)]
+    send_counts = [int(c) for c in send_counts]
     n = sum(send_counts)
     w = int(rows.shape[1]) if rows.dim() == 2 else 4
-    sc = torch.tensor(seg_counts, dtype=torch.int64, device=wire)
+    sc = torch.tensor(send_counts, dtype=torch.int64, device=wire)
     rc = torch.empty_like(sc)
     dist.all_to_all_single(rc, sc, group=group)
-    recv_segs = [int(c) for c in rc.tolist()]
-    recv_counts = [sum(recv_segs[s * K:(s + 1) * K]) for s in range(world)]
+    recv_counts = [int(c) for c in rc.tolist()]
     out = torch.empty((sum(recv_counts), w), dtype=torch.int64, device=wire)
     dist.all_to_all_single(out, rows[:n].reshape(n, w).to(wire), recv_counts, send_counts, group=group)
-    return out.to(home), (recv_segs if K > 1 else recv_counts)
+    return out.to(home), recv_counts
 
 
 def exchange_records(keys, vals, send_counts, group=None, return_counts=False):

@@ -210,34 +210,3 @@ def test_exchange_records_with_an_empty_sender():
         assert k == want and k1 == want
         assert s == [[x, x + 1, x + 2] for x in want]
         assert a1 == [float(np.float64(x) / 3.0) for x in want]
-
-
-def _a2a_segs_worker(rank, world, port, out):
-    import torch.distributed as dist
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    # two sub-plan segments per owner (Coverage(sub_plans=2).trace_rows): segment k for owner d holds
-    # rank + d + k rows, keyed (rank, d, k, i)
-    K = 2
-    seg = [rank + d + k for d in range(world) for k in range(K)]
-    keys = [rank * 1000 + d * 100 + k * 10 + i for d in range(world) for k in range(K) for i in range(rank + d + k)]
-    rows = torch.tensor([[x, x + 1, x + 2, x + 3] for x in keys], dtype=torch.int64).reshape(-1, 4)
-    r4, rc = rdist.exchange_rows(rows, seg, segs_per_dest=K)
-    out.put((rank, r4[:, 0].tolist(), rc))
-    dist.destroy_process_group()
-
-
-def test_exchange_rows_with_segments_per_destination():
-    """Sub-plans: K sorted segments per (source, owner) arrive in (source, segment) order, with
-    their counts."""
-    world, K = 2, 2
-    q = mp.get_context("spawn").Queue()
-    pc = mp.spawn(_a2a_segs_worker, args=(world, _port(), q), nprocs=world, join=False)
-    got = dict((r, rest) for r, *rest in (q.get(timeout=120) for _ in range(world)))
-    pc.join()
-    for d in range(world):
-        keys, rc = got[d]
-        assert rc == [src + d + k for src in range(world) for k in range(K)]
-        assert keys == [src * 1000 + d * 100 + k * 10 + i for src in range(world) for k in range(K)
-                        for i in range(src + d + k)]

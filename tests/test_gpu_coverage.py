@@ -139,26 +139,23 @@ def test_coverage_on_bvh_terrain():
     cov.close()
 
 
-def _ray_sharded_rows(env, grid, tx, B, N, S, win=100e-9, env_mesh=None, sub=1):
+def _ray_sharded_rows(env, grid, tx, B, N, S, win=100e-9, env_mesh=None):
     """_ray_sharded through the packed path run() takes: trace_rows -> each owner's segments of
-    (key, sum) rows in source-rank order -> power_from_rows.  sub = K: every rank's rays as K
-    concurrent sub-plans, K segments per (source, owner)."""
+    (key, sum) rows in source-rank order -> power_from_rows."""
     plans = [Coverage(env, 2.998e8, 100e9, win, B, N, grid, shard_index=r, shard_count=S, shard_mode="rays",
-                      env_mesh=env_mesh, sub_plans=sub) for r in range(S)]
+                      env_mesh=env_mesh) for r in range(S)]
     sent = []
     for p in plans:
         rows, counts = p.trace_rows(tx, 1)
-        assert len(counts) == S * sub
         sent.append((rows.clone(), counts))
     total = torch.zeros(grid.num_cells, dtype=torch.float64, device="cuda")
     irs = []
     for d, p in enumerate(plans):
         parts, segs = [], []
         for rows, counts in sent:
-            off = sum(counts[:d * sub])
-            mine = counts[d * sub:(d + 1) * sub]
-            parts.append(rows[off:off + sum(mine)])
-            segs.extend(mine)
+            off = sum(counts[:d])
+            parts.append(rows[off:off + counts[d]])
+            segs.append(counts[d])
         total += p.power_from_rows(torch.cat(parts), segs)
         irs.append(p.impulse_responses())
     for p in plans:
@@ -240,27 +237,6 @@ def test_packed_rows_equal_records(room, S):
     for a, b in zip(irs_rec, irs_rows):
         for x, y in zip(a, b):
             assert x.tobytes() == y.tobytes()
-
-
-@pytest.mark.parametrize("S,K", [(1, 2), (3, 2), (8, 3)])
-def test_sub_plans_equal_one_plan_per_rank(room, S, K):
-    """A rank's rays as K concurrent sub-plans on K streams (Coverage(sub_plans=K)): K segments per
-    (source, owner), the same maps and impulse responses bit for bit, on room and the BVH terrain."""
-    from rf_ray_tracing_warp_amd.mesh import synthetic_terrain
-    grid, tx, B, N = CoverageGrid(8.0, -2.5, 4.6, 0.37, 0.41, 0.4, 13, 12, 2), (10, 0, 5), 3, 60_000
-    for _ in range(2):  # the second pass reuses every plan's grown buffers and streams
-        t1, irs1 = _ray_sharded_rows(room, grid, tx, B, N, S)
-        tk, irsk = _ray_sharded_rows(room, grid, tx, B, N, S, sub=K)
-        assert t1.tobytes() == tk.tobytes()
-        assert np.isfinite(t1).sum() >= 20
-        for a, b in zip(irs1, irsk):
-            for x, y in zip(a, b):
-                assert x.tobytes() == y.tobytes()
-    t = synthetic_terrain(256, 50.0)
-    grid, tx = CoverageGrid(7.0, -1.0, 2.0, 0.7, 0.25, 1.0, 10, 10, 1), (10.0, 0.0, 4.5)
-    t1, _ = _ray_sharded_rows(t, grid, tx, 3, 40_000, S, win=200e-9)
-    tk, _ = _ray_sharded_rows(t, grid, tx, 3, 40_000, S, win=200e-9, sub=K)
-    assert t1.tobytes() == tk.tobytes() and np.isfinite(t1).sum() >= 3
 
 
 def test_trace_rows_match_records_and_grow(room):

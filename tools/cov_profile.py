@@ -3,9 +3,7 @@ estimates: K3 (room, 256^2) and K5 (terrain stand-in, 1024^2), each as the whole
 per-rank work of an S-GPU run.  MODE=cells: rank 0 of an S-way x-column cell shard.  MODE=rays
 (default): all S ray-shard plans run one after another on this GPU; per rank, the time of its
 trace + local reduce (stage 1) plus its owner stage on the records routed to it, and the slowest
-rank is reported (the all-to-all itself is not included).  SUB=K: each rank's rays as K
-concurrent sub-plans (Coverage(sub_plans=K)); SHARDS=1 with SUB=K > 1 is the one-GPU map as K
-concurrent sub-plans.  Prints one JSON line per case."""
+rank is reported (the all-to-all itself is not included).  Prints one JSON line per case."""
 import json
 import os
 import sys
@@ -33,7 +31,7 @@ def main():
             grid, tx, win, B = CoverageGrid.square(1024, 50.0, 2.0), (10.0, 0.0, 4.5), 200e-9, 3
         env = DeviceMesh(m.vertices, m.faces, 0)
         for S in shards:
-            if mode == "rays" and (S > 1 or int(os.environ.get("SUB", "1")) > 1):
+            if mode == "rays" and S > 1:
                 rays_case(case, m, grid, tx, win, B, env, S, reps)
                 continue
             per_rank = []
@@ -56,9 +54,8 @@ def main():
 def rays_case(case, m, grid, tx, win, B, env, S, reps):
     import torch
     from rf_ray_tracing_warp_amd.coverage import Coverage
-    K = int(os.environ.get("SUB", "1"))  # concurrent sub-plans per rank (Coverage(sub_plans=K))
     plans = [Coverage(m, 2.998e8, 100e9, win, B, 1_000_000, grid, 0.1, device=0, shard_index=r, shard_count=S,
-                      env_mesh=env, shard_mode="rays", sub_plans=K) for r in range(S)]
+                      env_mesh=env, shard_mode="rays") for r in range(S)]
 
     def timed(fn):
         torch.cuda.synchronize()
@@ -80,11 +77,10 @@ def rays_case(case, m, grid, tx, win, B, env, S, reps):
         for d, p in enumerate(plans):
             if rows_path:
                 parts, segs = [], []
-                for rows, counts in sent:  # counts: (owner, sub-plan) segments
-                    off = sum(counts[:d * K])
-                    mine = counts[d * K:(d + 1) * K]
-                    parts.append(rows[off:off + sum(mine)])
-                    segs.extend(mine)
+                for rows, counts in sent:
+                    off = sum(counts[:d])
+                    parts.append(rows[off:off + counts[d]])
+                    segs.append(counts[d])
                 r = torch.cat(parts)
                 nrec.append(int(r.shape[0]))
                 # the received rows as exchange_rows delivers them: one sorted segment per source
@@ -106,8 +102,7 @@ def rays_case(case, m, grid, tx, win, B, env, S, reps):
         if best is None or max(per_rank) < max(best[0]):
             best = (per_rank, t_trace, t_own, nrec, [sum(x[-1]) for x in sent])
     per_rank, t_trace, t_own, nrec, nsent = best
-    print(json.dumps({"case": case, "mode": "rays", "shards": S, "sub_plans": K,
-                      "ms_per_map_max_rank": max(per_rank) * 1e3,
+    print(json.dumps({"case": case, "mode": "rays", "shards": S, "ms_per_map_max_rank": max(per_rank) * 1e3,
                       "ms_trace_stage": [round(x * 1e3, 3) for x in t_trace],
                       "ms_owner_stage": [round(x * 1e3, 3) for x in t_own],
                       "records_sent": nsent, "records_received": nrec}), flush=True)
