@@ -477,8 +477,11 @@ __global__ __launch_bounds__(256, RT_COV_TRAJ_WAVES) void k_traj(CovParams p) {
 #ifndef RT_TRAJ_SPLIT_G
 #define RT_TRAJ_SPLIT_G 4
 #endif
+#ifndef RT_TRAJ_SPLIT_WAVES
+#define RT_TRAJ_SPLIT_WAVES RT_COV_TRAJ_WAVES
+#endif
 template <int G>
-__global__ __launch_bounds__(256, RT_COV_TRAJ_WAVES) void k_traj_split(CovParams p) {
+__global__ __launch_bounds__(256, RT_TRAJ_SPLIT_WAVES) void k_traj_split(CovParams p) {
   constexpr int LG = G == 16 ? 4 : 2;
   if (p.zero_ctr && blockIdx.x == 0 && threadIdx.x < 4) p.zero_ctr[threadIdx.x] = 0ull;
   const int j = threadIdx.x & (G - 1);
@@ -764,12 +767,46 @@ __device__ __forceinline__ float npdot(const float* a, const float* b) {
 #ifndef RT_AMP_SQRT
 #define RT_AMP_SQRT 1
 #endif
+// sin and cos of x in [0, pi/2 + 1e-6] (bounce_amp's theta): one Cody-Waite step against pi/2 above
+// pi/4 (x - pio2_1 is exact there), then the classic fdlibm kernels on [-pi/4, pi/4] (< 1 ulp).
+// ocml's general sincos carries the large-argument (Payne-Hanek) reduction, whose registers
+// k_replay cannot afford beside its other f64 work (18 VGPRs spilled, 76 B scratch per lane).
+// RT_AMP_SINCOS_Q1=0 restores ocml's sincos.
+#ifndef RT_AMP_SINCOS_Q1
+#define RT_AMP_SINCOS_Q1 1
+#endif
+__device__ __forceinline__ void sincos_q1(double x, double& s, double& c) {
+  const double pio2_1 = 1.57079632673412561417e+00, pio2_1t = 6.07710050650619224932e-11;
+  const bool hi = x > 0.78539816339744828;
+  const double a = hi ? x - pio2_1 : x;  // exact
+  const double r = hi ? a - pio2_1t : a;
+  const double rl = hi ? (a - r) - pio2_1t : 0.0;
+  const double z = r * r, w = z * z;
+  // __kernel_sin(r, rl, 1)
+  const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03, S3 = -1.98412698298579493134e-04,
+               S4 = 2.75573137070700676789e-06, S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+  const double sr = S2 + z * (S3 + z * S4) + z * w * (S5 + z * S6);
+  const double v = z * r;
+  const double sk = r - ((z * (0.5 * rl - v * sr) - rl) - v * S1);
+  // __kernel_cos(r, rl)
+  const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03, C3 = 2.48015872894767294178e-05,
+               C4 = -2.75573143513906633035e-07, C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+  const double cr = z * (C1 + z * (C2 + z * C3)) + w * w * (C4 + z * (C5 + z * C6));
+  const double hz = 0.5 * z, cw = 1.0 - hz;
+  const double ck = cw + (((1.0 - cw) - hz) + (z * cr - r * rl));
+  s = hi ? ck : sk;   // x = pi/2 + r: sin x = cos r, cos x = -sin r
+  c = hi ? -sk : ck;
+}
 __device__ __forceinline__ double bounce_amp(float angle) {
   if (isnan(angle)) return 0.0;
   const double theta = (double)(1.57079637050628662109375f - angle / 2.0f);
 #if RT_AMP_SQRT
   double st, ct;
+#if RT_AMP_SINCOS_Q1
+  sincos_q1(theta, st, ct);
+#else
   sincos(theta, &st, &ct);
+#endif
   const double x = st / 5.0;
   const double cti = sqrt(1.0 - x * x);
   const double q = (cti - 5.0 * ct) / (cti + 5.0 * ct);
@@ -857,6 +894,54 @@ struct PathAccL {
   }
 };
 
+// PathAcc with the amplitude deferred (RT_REPLAY_DEFER_AMP, default): during the bounce loop each
+// interior vertex's cosine (the f32 value acos is taken of) goes to the thread's LDS column, and
+// the f64 product of _bounce_amplitude factors is formed after the loop, in the same vertex order
+// -- the same multiplications of the same values, so the same bits.  The f64 acos and sincos then
+// no longer add their registers to the queries' live state: k_replay<false> spilled 21 VGPRs
+// (88 B of scratch per lane) with them inside the loop, 1 with them stubbed out.
+#ifndef RT_REPLAY_DEFER_AMP
+#define RT_REPLAY_DEFER_AMP 1
+#endif
+constexpr int kMaxInterior = 16;  // B <= 15 bounces: at most B - 1 interior vertices per path
+struct PathAccD {
+  float prev[3], seg[3];
+  float* cosv;  // this thread's LDS column: interior vertex i's cosine at cosv[256 * i]
+  int npts, nint;
+  float dist;
+  __device__ __forceinline__ void start(float x, float y, float z) {
+    prev[0] = x;
+    prev[1] = y;
+    prev[2] = z;
+    npts = 1;
+    nint = 0;
+    dist = 0.0f;
+  }
+  __device__ __forceinline__ void add(float x, float y, float z) {
+    const float s2[3] = {x - prev[0], y - prev[1], z - prev[2]};
+    if (npts >= 2) {  // vertex prev is interior: angle between seg (p1->p2) and s2 (p2->p3)
+      const float l1 = sqrtf(npdot(seg, seg));
+      if (nint < kMaxInterior) cosv[256 * nint] = npdot(seg, s2) / (l1 * sqrtf(npdot(s2, s2)));
+      ++nint;
+    }
+    dist += sqrtf(npdot(s2, s2));
+    seg[0] = s2[0];
+    seg[1] = s2[1];
+    seg[2] = s2[2];
+    prev[0] = x;
+    prev[1] = y;
+    prev[2] = z;
+    ++npts;
+  }
+};
+// amp0 times the factors of the first n interior vertices, in path order (PathAcc::amp's product)
+__device__ __forceinline__ double amp_product(const float* cosv, int n, double amp0) {
+  double amp = amp0;
+#pragma unroll 1
+  for (int i = 0; i < n; ++i) amp *= bounce_amp((float)acos((double)cosv[256 * i]));
+  return amp;
+}
+
 // ------------------------------------------------------------------ 3-4. receiver test, first win, replay
 // Record key (compact): [owner | cell | bin] with the field widths of CovParams.  Sorting it groups
 // the records by destination rank, then (cell, bin); the bins are summed exactly (Fx192), so the
@@ -897,7 +982,11 @@ __device__ __forceinline__ bool rx_wins(const CovParams& p, const RxLds& L, int6
 template <bool USE_BVH, bool RX_FIRST>
 __device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab, const RxLds& L, int64_t cell,
                                        int64_t r, int k0, float tr, uint64_t& okey, double& oamp) {
-#if RT_REPLAY_ACC_LDS
+#if RT_REPLAY_DEFER_AMP
+  __shared__ float cos_lds[kMaxInterior * 256];
+  PathAccD acc;
+  acc.cosv = cos_lds + threadIdx.x;
+#elif RT_REPLAY_ACC_LDS
   __shared__ float acc_lds[6 * 256];
   PathAccL acc;
   acc.col = acc_lds + threadIdx.x;
@@ -905,7 +994,11 @@ __device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab
   PathAcc acc;
 #endif
   const float4 t0 = traj_p(p, r, 0);
+#if RT_REPLAY_DEFER_AMP
+  acc.start(t0.x, t0.y, t0.z);  // p_0 = tx
+#else
   acc.start(t0.x, t0.y, t0.z, p.amp0);  // p_0 = tx
+#endif
   for (int q = 1; q <= k0; ++q) {       // environment prefix p_1 .. p_k0
     const float4 tq = traj_p(p, r, q);
     acc.add(tq.x, tq.y, tq.z);
@@ -919,7 +1012,11 @@ __device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab
   pos.z = fmaf(dir.z, tr, pos.z);
   acc.add(pos.x, pos.y, pos.z);
   float rec_dist = acc.dist;
+#if RT_REPLAY_DEFER_AMP
+  int rec_nint = acc.nint;
+#else
   double rec_amp = acc.amp;
+#endif
   float3 d = dir;
   for (int b = k0 + 1; b < p.B; ++b) {  // kernel.py:57-98 with this cell's receiver
     const rt::Shear s = rt::make_shear(pos, d);
@@ -945,7 +1042,11 @@ __device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab
       pos.z = fmaf(d.z, hr.t, pos.z);
       acc.add(pos.x, pos.y, pos.z);
       rec_dist = acc.dist;  // received_paths = traced prefix through this point (kernel.py:89-90)
+#if RT_REPLAY_DEFER_AMP
+      rec_nint = acc.nint;
+#else
       rec_amp = acc.amp;
+#endif
     } else if (env_hit) {
       // after the last bounce only a receiver hit could still change the record: an environment
       // hit there ends the path, its vertex (and its angle's f64 amplitude) unused
@@ -964,6 +1065,9 @@ __device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab
       break;
     }
   }
+#if RT_REPLAY_DEFER_AMP
+  const double rec_amp = amp_product(acc.cosv, rec_nint, p.amp0);
+#endif
   double dl;
   if (p.flags & RT_CIR_C_F64) {
     dl = ((double)rec_dist / p.c64) * p.fs64;
