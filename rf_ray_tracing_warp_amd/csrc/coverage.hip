@@ -477,8 +477,12 @@ __global__ __launch_bounds__(256, RT_COV_TRAJ_WAVES) void k_traj(CovParams p) {
 #ifndef RT_TRAJ_SPLIT_G
 #define RT_TRAJ_SPLIT_G 4
 #endif
+// (Splitting the ray's t range over the G lanes instead of the root's subtrees -- each lane opens
+// only boxes overlapping its piece of the ray, so a grazing ray's long run of leaves is divided G
+// ways -- was bit-identical and no faster: K5 rank of 8 1.134 ms vs 1.154 / 1.142 / 1.208 ms for
+// G = 4 / 8 / 16, profiles/r3za_k5_traj_tsplit_ab.jsonl.)
 #ifndef RT_TRAJ_SPLIT_WAVES
-#define RT_TRAJ_SPLIT_WAVES RT_COV_TRAJ_WAVES
+#define RT_TRAJ_SPLIT_WAVES 4  // 120 VGPRs, no spills (5: 96 + 23 spilled); K5 rank of 8 1.204 -> 1.154 ms (r3z)
 #endif
 template <int G>
 __global__ __launch_bounds__(256, RT_TRAJ_SPLIT_WAVES) void k_traj_split(CovParams p) {
