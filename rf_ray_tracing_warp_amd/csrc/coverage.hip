@@ -352,6 +352,10 @@ __device__ __forceinline__ void rx_group(const RxLds& L, const double c[3], cons
   }
 }
 
+// ROLLED: the 20-group ball test as a loop over the table (constants by scalar loads) instead of
+// unrolled -- fewer VGPRs (K3 k_replay 167 -> 125, so 4 waves per SIMD without spills), slower where
+// the occupancy does not change (k_win 0.95 -> 1.01 ms, K5 replay 1.23 -> 1.30 ms; r3zc)
+template <bool ROLLED = false>
 __device__ __forceinline__ rt::Hit rx_query_culled(const RxLds& L, const rt_grid& g, int64_t cell, double r, float3 o,
                                                    float3 d) {
   const rt::Shear s = rt::make_shear(o, d);
@@ -369,7 +373,7 @@ __device__ __forceinline__ rt::Hit rx_query_culled(const RxLds& L, const rt_grid
   const float pad = (float)(1e-3 * r + 2e-5 * (1.0 + amax) + 4e-6 * fabs(t0) * sqrt(dd));
   uint32_t near = 0, far = 0;
   float far_tmin = INFINITY;
-#pragma unroll
+#pragma unroll(ROLLED ? 1 : RT_ICO1_NF / 4)
   for (int gi = 0; gi < RT_ICO1_NF / 4; ++gi) {
     const float mx = rt_ico1_gball[gi][0] * rf, my = rt_ico1_gball[gi][1] * rf, mz = rt_ico1_gball[gi][2] * rf;
     const float wx = mx - ux, wy = my - uy, wz = mz - uz;  // ball centre relative to the closest point
@@ -411,13 +415,13 @@ __device__ __forceinline__ rt::Hit rx_query_culled(const RxLds& L, const rt_grid
 #ifndef RT_COV_RXQ_WIN
 #define RT_COV_RXQ_WIN 3
 #endif
-template <int V>
+template <int V, bool ROLLED = false>
 __device__ __forceinline__ rt::Hit rx_query_v(const RxLds& L, const rt_grid& g, int64_t cell, double r, float3 o,
                                               float3 d) {
   if constexpr (V == 0) return rx_query(g, cell, r, o, d);
   else if constexpr (V == 1) return rx_query_lean(g, cell, r, o, d);
   else if constexpr (V == 2) return rx_query_grouped(g, cell, r, o, d);
-  else return rx_query_culled(L, g, cell, r, o, d);
+  else return rx_query_culled<ROLLED>(L, g, cell, r, o, d);
 }
 
 // Minimum waves per SIMD the coverage kernels are built for (launch bounds; 1 = register-unbounded).
@@ -429,8 +433,14 @@ __device__ __forceinline__ rt::Hit rx_query_v(const RxLds& L, const rt_grid& g, 
 #ifndef RT_COV_TRAJ_WAVES
 #define RT_COV_TRAJ_WAVES 5
 #endif
+// LDS scenes (K3): 4 waves with the rolled receiver ball test (125 VGPRs, no spills): K3 replay
+// 2.067 -> 1.917 ms (r3zc, profiles/r3zc_cov_replay_waves_ab.jsonl); BVH scenes keep 3 (the walk
+// stack's 32 KB of LDS and 155 VGPRs)
 #ifndef RT_COV_REPLAY_WAVES
-#define RT_COV_REPLAY_WAVES 3
+#define RT_COV_REPLAY_WAVES 4
+#endif
+#ifndef RT_COV_REPLAY_WAVES_BVH
+#define RT_COV_REPLAY_WAVES_BVH 3
 #endif
 
 // ------------------------------------------------------------------ 1. environment trajectories
@@ -907,11 +917,11 @@ struct PathAccL {
 #ifndef RT_REPLAY_DEFER_AMP
 #define RT_REPLAY_DEFER_AMP 1
 #endif
-constexpr int kMaxInterior = 16;  // B <= 15 bounces: at most B - 1 interior vertices per path
+// A path has at most B + 1 points (the TX, then one per bounce), so at most B - 1 interior vertices.
 struct PathAccD {
   float prev[3], seg[3];
   float* cosv;  // this thread's LDS column: interior vertex i's cosine at cosv[256 * i]
-  int npts, nint;
+  int npts, nint, ncap;
   float dist;
   __device__ __forceinline__ void start(float x, float y, float z) {
     prev[0] = x;
@@ -925,7 +935,7 @@ struct PathAccD {
     const float s2[3] = {x - prev[0], y - prev[1], z - prev[2]};
     if (npts >= 2) {  // vertex prev is interior: angle between seg (p1->p2) and s2 (p2->p3)
       const float l1 = sqrtf(npdot(seg, seg));
-      if (nint < kMaxInterior) cosv[256 * nint] = npdot(seg, s2) / (l1 * sqrtf(npdot(s2, s2)));
+      if (nint < ncap) cosv[256 * nint] = npdot(seg, s2) / (l1 * sqrtf(npdot(s2, s2)));
       ++nint;
     }
     dist += sqrtf(npdot(s2, s2));
@@ -987,9 +997,10 @@ template <bool USE_BVH, bool RX_FIRST>
 __device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab, const RxLds& L, int64_t cell,
                                        int64_t r, int k0, float tr, uint64_t& okey, double& oamp) {
 #if RT_REPLAY_DEFER_AMP
-  __shared__ float cos_lds[kMaxInterior * 256];
+  // the B - 1 columns after the environment table in dynamic LDS (k_replay's launch sizes it)
   PathAccD acc;
-  acc.cosv = cos_lds + threadIdx.x;
+  acc.cosv = reinterpret_cast<float*>(const_cast<float4*>(lds_tab) + (USE_BVH ? 0 : (size_t)p.env_nf * 18)) + threadIdx.x;
+  acc.ncap = p.B - 1;
 #elif RT_REPLAY_ACC_LDS
   __shared__ float acc_lds[6 * 256];
   PathAccL acc;
@@ -1029,7 +1040,7 @@ __device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab
     // miss there ends the path without the environment query (K3: most first wins at bounce 0
     // leave their receiver at bounce 1 and miss it at bounce 2)
     hr = USE_BVH ? rx_query_v<RT_COV_RXQ_BVH>(L, p.g, cell, p.r_rx, pos, d)
-                 : rx_query_v<RT_COV_RXQ>(L, p.g, cell, p.r_rx, pos, d);
+                 : rx_query_v<RT_COV_RXQ, RT_COV_REPLAY_WAVES >= 4>(L, p.g, cell, p.r_rx, pos, d);
     if (hr.face < 0 && b + 1 >= p.B) break;
     if constexpr (RX_FIRST) {
       // the environment culled at the receiver's t: every environment hit with t <= hr.t is
@@ -1271,7 +1282,7 @@ __global__ __launch_bounds__(1024) void k_replay_order(CovParams p, const uint64
 }
 
 template <bool USE_BVH, bool RX_FIRST>
-__global__ __launch_bounds__(256, RT_COV_REPLAY_WAVES) void k_replay(CovParams p, const uint64_t* keys, const float* trx,
+__global__ __launch_bounds__(256, USE_BVH ? RT_COV_REPLAY_WAVES_BVH : RT_COV_REPLAY_WAVES) void k_replay(CovParams p, const uint64_t* keys, const float* trx,
                                                 const int64_t* list, int64_t nl, const unsigned long long* nl_dev,
                                                 const int32_t* order, uint64_t* out_key, double* out_amp) {
   extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
@@ -2585,6 +2596,8 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
   p.flags = flags;
   p.n_bins = n_bins;
   const size_t lds = bvh ? 0 : (size_t)p.env_nf * 18 * sizeof(float4);
+  // k_replay: the deferred amplitude's B - 1 cosine columns follow the environment table
+  const size_t lds_replay = lds + (RT_REPLAY_DEFER_AMP ? (size_t)std::max(p.B - 1, 1) * 256 * sizeof(float) : 0);
   const unsigned grid_rays = (unsigned)std::min<int64_t>((c->n + 255) / 256, 4096);
   p.order = nullptr;
   p.zero_ctr = c->counters;  // zeroed by the trajectory kernel (first attempt; retries use a fill)
@@ -2661,13 +2674,13 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
     // a receiver-first one skipping faces beyond the receiver's t 5% slower too: 2.50 vs 2.63 ms,
     // profiles/r2x_cov_rxfirst_lds_ab.jsonl)
     if (bvh && replay_rx_first())
-      hipLaunchKernelGGL((k_replay<true, true>), dim3(grid_l), dim3(256), 0, s, p, c->keys, c->trx, c->list, nl,
+      hipLaunchKernelGGL((k_replay<true, true>), dim3(grid_l), dim3(256), lds_replay, s, p, c->keys, c->trx, c->list, nl,
                          nl_dev, v_out, c->okeys, c->oamps);
     else if (bvh)
-      hipLaunchKernelGGL((k_replay<true, false>), dim3(grid_l), dim3(256), 0, s, p, c->keys, c->trx, c->list, nl,
+      hipLaunchKernelGGL((k_replay<true, false>), dim3(grid_l), dim3(256), lds_replay, s, p, c->keys, c->trx, c->list, nl,
                          nl_dev, v_out, c->okeys, c->oamps);
     else
-      hipLaunchKernelGGL((k_replay<false, false>), dim3(grid_l), dim3(256), lds, s, p, c->keys, c->trx, c->list, nl,
+      hipLaunchKernelGGL((k_replay<false, false>), dim3(grid_l), dim3(256), lds_replay, s, p, c->keys, c->trx, c->list, nl,
                          nl_dev, v_out, c->okeys, c->oamps);
     prof_mark(c, 5, s);
     RT_HIP(hipGetLastError());
