@@ -314,10 +314,12 @@ def run_coverage(cov, tx, runs, world, dist, local):
     """Time `runs` maps (profiling off), then one profiled map for the stage breakdown."""
     import torch
 
+    from rf_ray_tracing_warp_amd.dist import gather_power_map
+
     def one():
         p = cov.run_device(tx, 1)
-        if world > 1:
-            dist.all_reduce(p)
+        if world > 1:  # the sum-reduce of the owners' disjoint x columns, as an all-gather
+            p = gather_power_map(p, cov.grid.nx)
         return p
 
     one()

@@ -283,9 +283,14 @@ class Coverage:
         if process_group is not None or self.shard_count > 1:
             import torch.distributed as dist
             with torch.cuda.device(self.device):
-                wire = p.to(rdist.wire_device(process_group, self.device))
-                dist.all_reduce(wire, group=process_group)
-                p = wire
+                if (dist.get_world_size(process_group), dist.get_rank(process_group)) == \
+                        (self.shard_count, self.shard_index):
+                    # owners hold disjoint x columns: the sum-reduce is an all-gather of them
+                    p = rdist.gather_power_map(p, self.grid.nx, process_group)
+                else:
+                    wire = p.to(rdist.wire_device(process_group, self.device))
+                    dist.all_reduce(wire, group=process_group)
+                    p = wire
         g = self.grid
         return p.cpu().numpy().reshape(g.nz, g.ny, g.nx)
 

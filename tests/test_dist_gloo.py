@@ -210,3 +210,32 @@ def test_exchange_records_with_an_empty_sender():
         assert k == want and k1 == want
         assert s == [[x, x + 1, x + 2] for x in want]
         assert a1 == [float(np.float64(x) / 3.0) for x in want]
+
+
+def _gather_map_worker(rank, world, port, out):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rows, nx = 6, 7  # nx not a multiple of the world size
+    full = torch.arange(rows * nx, dtype=torch.float64) * 1.25 + 0.5
+    full[3] = float("nan")  # an owner's NaN (a cell that receives nothing)
+    ix = torch.arange(rows * nx) % nx
+    mine = torch.where(ix % world == rank, full, torch.zeros_like(full))
+    g = rdist.gather_power_map(mine.clone(), nx)
+    r = mine.clone()
+    dist.all_reduce(r)
+    out.put((rank, g.tolist(), r.tolist(), full.tolist()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_power_map_equals_the_sum_reduce(world):
+    """The owners' disjoint x columns gathered equal the sum-reduce of their maps, bit for bit."""
+    q = mp.get_context("spawn").Queue()
+    pc = mp.spawn(_gather_map_worker, args=(world, _port(), q), nprocs=world, join=False)
+    got = [q.get(timeout=120) for _ in range(world)]
+    pc.join()
+    for _, g, r, full in got:
+        a, b, f = np.array(g), np.array(r), np.array(full)
+        assert a.tobytes() == b.tobytes() and a.tobytes() == f.tobytes()
