@@ -322,13 +322,19 @@ __device__ __forceinline__ rt::Hit rx_query_grouped(const rt_grid& g, int64_t ce
 struct RxLds {
   double ur[RT_ICO1_NV][4];      // rt_ico1_v * r, the double product of make_rx_perm (w unused)
   uint64_t vid[RT_ICO1_NF / 4];  // the group's vertex ids c0 c1 c2 m01 m12 m20, 6 bits each
+  float4 gb[RT_ICO1_NF / 4];     // group ball: centre * r (f32) and radius * r
+  float gmm[RT_ICO1_NF / 4];     // |centre * r|^2
 };
 __device__ __forceinline__ void stage_rx(RxLds& L, double r) {
   for (int i = threadIdx.x; i < RT_ICO1_NV * 3; i += blockDim.x) L.ur[i / 3][i % 3] = rt_ico1_v[i / 3][i % 3] * r;
+  const float rf = (float)r;
   for (int g = threadIdx.x; g < RT_ICO1_NF / 4; g += blockDim.x) {
     uint64_t w = 0;
     for (int j = 0; j < 6; ++j) w |= (uint64_t)kIcoGroup.v[g][j] << (6 * j);
     L.vid[g] = w;
+    const float mx = rt_ico1_gball[g][0] * rf, my = rt_ico1_gball[g][1] * rf, mz = rt_ico1_gball[g][2] * rf;
+    L.gb[g] = make_float4(mx, my, mz, rt_ico1_gball[g][3] * rf);
+    L.gmm[g] = mx * mx + my * my + mz * mz;
   }
   __syncthreads();
 }
@@ -352,6 +358,9 @@ __device__ __forceinline__ void rx_group(const RxLds& L, const double c[3], cons
   }
 }
 
+#ifndef RT_RXQ_DOT_BALL
+#define RT_RXQ_DOT_BALL 1
+#endif
 // ROLLED: the 20-group ball test as a loop over the table (constants by scalar loads) instead of
 // unrolled -- fewer VGPRs (K3 k_replay 167 -> 125, so 4 waves per SIMD without spills), slower where
 // the occupancy does not change (k_win 0.95 -> 1.01 ms, K5 replay 1.23 -> 1.30 ms; r3zc)
@@ -373,6 +382,40 @@ __device__ __forceinline__ rt::Hit rx_query_culled(const RxLds& L, const rt_grid
   const float pad = (float)(1e-3 * r + 2e-5 * (1.0 + amax) + 4e-6 * fabs(t0) * sqrt(dd));
   uint32_t near = 0, far = 0;
   float far_tmin = INFINITY;
+#if RT_RXQ_DOT_BALL
+  // Per group, with the unit direction e = d / |d| and u perpendicular to it: the squared distance
+  // from the ball centre m to the line is |m - u|^2 - (m.e)^2 = |m|^2 + |u|^2 - 2 m.u - (m.e)^2, and
+  // the centre's line parameter is t0 + (m.e) / |d|.  ~20 VALU per group against ~45 for the cross
+  // product form below; its f32 rounding (~1e-7 r^2 in the squared distance) is far inside the
+  // pad (1e-3 r), so the test stays conservative and every hit is the same.
+  (void)ddf;
+  (void)inv_dd;
+  const float ex = d.x * inv_len, ey = d.y * inv_len, ez = d.z * inv_len;
+  const float uu = ux * ux + uy * uy + uz * uz;
+  // an opaque offset per query: otherwise the 100 loop-invariant LDS words are hoisted out of the
+  // callers' loops into registers (k_win 129 VGPRs spilled)
+  int z = 0;
+  asm volatile("" : "+v"(z));
+  const float4* gb = L.gb + z;
+  const float* gmm = L.gmm + z;
+#ifndef RT_RXQ_DOT_UNROLL
+#define RT_RXQ_DOT_UNROLL 4
+#endif
+#pragma unroll(ROLLED ? 1 : RT_RXQ_DOT_UNROLL)
+  for (int gi = 0; gi < RT_ICO1_NF / 4; ++gi) {
+    const float4 m = gb[gi];
+    const float me = fmaf(m.x, ex, fmaf(m.y, ey, m.z * ez));
+    const float mu = fmaf(m.x, ux, fmaf(m.y, uy, m.z * uz));
+    const float R = m.w + pad;
+    const float dist2 = fmaf(-me, me, fmaf(-2.0f, mu, gmm[gi] + uu));
+    const bool ok = dist2 <= R * R && fmaf(me + R, inv_len, t0f) >= 0.0f;
+    if (ok && me <= 0.0f) near |= 1u << gi;
+    if (ok && me > 0.0f) {
+      far |= 1u << gi;
+      far_tmin = fminf(far_tmin, fmaf(me - R, inv_len, t0f));
+    }
+  }
+#else
 #pragma unroll(ROLLED ? 1 : RT_ICO1_NF / 4)
   for (int gi = 0; gi < RT_ICO1_NF / 4; ++gi) {
     const float mx = rt_ico1_gball[gi][0] * rf, my = rt_ico1_gball[gi][1] * rf, mz = rt_ico1_gball[gi][2] * rf;
@@ -388,6 +431,7 @@ __device__ __forceinline__ rt::Hit rx_query_culled(const RxLds& L, const rt_grid
       far_tmin = fminf(far_tmin, tb - half);
     }
   }
+#endif
   rt::Hit h;
   rt::hit_init(h);
   while (near) {
@@ -1104,7 +1148,7 @@ __device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab
 // measured 37% slower on K3, 10.1 vs 7.4 ms per map: the replay's divergent tail and registers
 // held every candidate's wave.)
 #ifndef RT_WIN_WAVES
-#define RT_WIN_WAVES 5  // 96 VGPRs (60 B scratch) instead of 127: K3 k_win 1.03 -> 0.98 ms, K5 0.92 -> 0.875 ms (r2zj; 6 waves: 1.01 / 0.91)
+#define RT_WIN_WAVES 6  // 80 VGPRs, spill-free with the dot-form ball test: K3 k_win 0.935 -> 0.895 ms, K5 0.79 -> 0.76 (r3ze); before it, 5 waves (96 VGPRs, 60 B scratch) beat 4 and 6: 1.03 -> 0.98 ms (r2zj)
 #endif
 __global__ __launch_bounds__(256, RT_WIN_WAVES) void k_win(CovParams p, const uint64_t* keys, const unsigned long long* nkeys_dev,
                                              int64_t cap, uint8_t* first_flag, float* trx) {
