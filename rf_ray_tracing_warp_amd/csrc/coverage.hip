@@ -2520,42 +2520,34 @@ int own_shift(const rt_coverage* c) { return 32 + bits_for((uint64_t)cov_ncell(c
 
 // reduced ray-mode records are sorted by (owner, cell, bin): bounds[o] = first record of owner o,
 // bounds[world] = the valid records (the dropped ~0 keys sort last)
-__global__ __launch_bounds__(256) void k_owner_bounds(const uint64_t* ukeys, const int64_t* nuniq, int world,
-                                                      int shift, int64_t* bounds) {
+// Owner bounds and send buffers in one launch: every thread finds the owner boundaries at its
+// record and writes the record's row, if it is valid (dropped records, ~0, sort last) and inside the
+// caller's capacity (the host sees the count and grows the buffer when it was too small)
+__global__ __launch_bounds__(256) void k_bounds_strip(const uint64_t* ukeys, const Fx192* usums, const int64_t* nuniq,
+                                                      int world, int64_t cap, int shift, int64_t* bounds,
+                                                      uint64_t* out, Fx192* sums_out, int packed) {
   const int64_t nu = *nuniq;
-  auto owner = [&](int64_t u) -> int64_t {
-    const uint64_t k = ukeys[u];
-    return k == ~0ull ? (int64_t)world : (int64_t)(k >> shift);
-  };
-  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u <= nu; u += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t lo = u == 0 ? -1 : owner(u - 1), hi = u == nu ? (int64_t)world : owner(u);
-    for (int64_t o = lo + 1; o <= hi; ++o) bounds[o] = u;  // owners lo+1 .. hi start at u
-  }
-}
-
-// as k_strip_owner, before the host knows the count: n = bounds[world] on the device, and nothing
-// is written when it exceeds the caller's capacity
-// (packed = 1: one (key, sum) row of 4 words per record at out, sums_out unused)
-__global__ __launch_bounds__(256) void k_strip_owner_dev(const uint64_t* ukeys, const Fx192* usums, const int64_t* bounds,
-                                                         int world, int64_t cap, int shift, uint64_t* out,
-                                                         Fx192* sums_out, int packed) {
-  const int64_t n = bounds[world];
-  if (n > cap) return;
   const uint64_t mask = (1ull << shift) - 1;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint64_t k = ukeys[i] & mask;
-    const Fx192 v = usums[i];
-    if (packed) {
-      typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-      u64x2* row = reinterpret_cast<u64x2*>(out + 4 * i);  // 32-B rows: two 16-B stores
-      row[0] = u64x2{k, v.w0};
-      row[1] = u64x2{v.w1, v.w2};
-    } else {
-      out[i] = k;
-      sums_out[i] = v;
+  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u <= nu; u += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = u < nu ? ukeys[u] : ~0ull;
+    const int64_t hi = k == ~0ull ? (int64_t)world : (int64_t)(k >> shift);
+    const int64_t lo = u == 0 ? -1 : (ukeys[u - 1] == ~0ull ? (int64_t)world : (int64_t)(ukeys[u - 1] >> shift));
+    for (int64_t o = lo + 1; o <= hi; ++o) bounds[o] = u;  // owners lo+1 .. hi start at u
+    if (out && k != ~0ull && u < cap) {
+      const Fx192 v = usums[u];
+      if (packed) {
+        typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+        u64x2* row = reinterpret_cast<u64x2*>(out + 4 * u);  // 32-B rows: two 16-B stores
+        row[0] = u64x2{k & mask, v.w0};
+        row[1] = u64x2{v.w1, v.w2};
+      } else {
+        out[u] = k & mask;
+        sums_out[u] = v;
+      }
     }
   }
 }
+
 // the reduced records of a ray-sharded plan into the caller's send buffers: keys without the owner
 // field, and the exact sums (one launch for both)
 __global__ __launch_bounds__(256) void k_strip_owner(const uint64_t* ukeys, const Fx192* usums, int64_t n, int shift,
@@ -3121,12 +3113,10 @@ int trace_records_impl(rt_coverage* c, const float* tx_pos, double tx_power, dou
     const KeyBits kb = key_bits(c, n_bins);
     rc = cov_reduce(c, c->okeys, c->oamps, nlist, record_sort_bits(c, kb, n_bins), wide_key(c, kb), s);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_owner_bounds, dim3((unsigned)std::min<int64_t>((nlist + 255) / 256, 4096)), dim3(256), 0, s,
-                       c->ukeys, c->nuniq, world, own_shift(c), c->bounds);
-    if (keys_out)  // the send buffers are filled before the host synchronizes (no launch after it)
-      hipLaunchKernelGGL(k_strip_owner_dev, dim3((unsigned)std::min<int64_t>((nlist + 255) / 256, 4096)), dim3(256), 0,
-                         s, c->ukeys, plan_sums(c), c->bounds, world, max_out, own_shift(c), keys_out,
-                         (Fx192*)sums_out, packed ? 1 : 0);
+    // the send buffers are filled before the host synchronizes (no launch after it)
+    hipLaunchKernelGGL(k_bounds_strip, dim3((unsigned)std::min<int64_t>((nlist + 256) / 256, 4096)), dim3(256), 0, s,
+                       c->ukeys, plan_sums(c), c->nuniq, world, keys_out ? max_out : 0, own_shift(c), c->bounds,
+                       keys_out, (Fx192*)sums_out, packed ? 1 : 0);
     RT_HIP(hipGetLastError());
     prof_mark(c, 7, s);
     RT_HIP(hipMemcpyAsync(b.data(), c->bounds, sizeof(int64_t) * (world + 1), hipMemcpyDeviceToHost, s));
