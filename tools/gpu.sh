@@ -22,6 +22,7 @@
 #   k2var     tools/k2_fused_variants.py over LIBS                           -> ${TAG}_k2.jsonl
 #   k4write   rocprofv3 --pmc WRITE_SIZE / FETCH_SIZE over tools/k4_write_ab.py, per library in LIBS
 #   hashbench tools/hash_bench (build it first, hipcc line in its header)    -> ${TAG}_hash_bench.jsonl
+#   ossort    tools/os_sort_bench vs rocPRIM (build it first, header)         -> ${TAG}_os_sort.jsonl
 #   rehearse  bench.py N=2,4 on this one GPU (gloo, RFRT_BENCH_ONE_GPU=1)    -> ${TAG}_rehearse_<n>.log
 #   full      = tests smoke bench
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
@@ -106,6 +107,11 @@ run_task() {
         done
       done
       cat ${O}_hash_bench.jsonl ;;
+    ossort)
+      for a in "1048576 30 0.5" "786432 35 0.5" "7864320 31 0.3" "6291456 36 0.3" "200000 30 0.5"; do
+        timeout -k 10 60 tools/os_sort_bench $a >> ${O}_os_sort.jsonl 2>&1
+        rc=$?; tail -1 ${O}_os_sort.jsonl; step_rc $rc "ossort $a"
+      done ;;
     rehearse)
       for n in 2 4; do
         RFRT_BENCH_ONE_GPU=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
