@@ -65,7 +65,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-runs", type=int, default=5, help="timed CPU-baseline runs (median), after 1 warm-up")
     ap.add_argument("--cpu-rays", type=int, default=8_000_000, help="rays per CPU-baseline run (all threads)")
-    ap.add_argument("--cpu-cells", type=int, default=4, help="K3 cells per coverage CPU-baseline run")
+    ap.add_argument("--cpu-cells", type=int, default=8,
+                    help="K3 / K5 cells per coverage CPU-baseline run (SURVEY 8(d) D5: median of 5 after a warm-up)")
     ap.add_argument("--no-coverage", action="store_true", help="skip K3 (same as leaving it out of --legs)")
     ap.add_argument("--coverage-grid", type=int, default=256, help="K3: n x n receiver cells at z=5 on room.stl")
     ap.add_argument("--coverage-rays", type=int, default=1_000_000)
@@ -185,14 +186,14 @@ def cpu_baseline_k3(args, info):
                           nthreads=info["threads_used"])
             ir = orc.cir_from_paths(orc.clean_paths(o["received"], o["mask"]), 1, N, 2.998e8, 100e9, 100e-9)
             orc.signal_power(ir, 100e-9)
-    med, ts = _median_runs(run, max(1, args.cpu_runs // 2))
+    med, ts = _median_runs(run, args.cpu_runs)
     ir = np.zeros(10000)
     ir[[3000, 5000, 7000]] = 1e-6
     conv, _ = _median_runs(lambda: orc.signal_power(ir, 100e-9), 5)
     return {"value": len(cells) / med, "unit": "cells/s", "cores": info["threads_used"], "kind": "port",
             "sample": f"{len(cells)} seeded K3 cells ({', '.join(str(int(c)) for c in cells)}), each the reference "
                       f"loop body: {N}-ray trace with its icosphere + host CIR + np.convolve power; median of "
-                      f"{len(ts)} runs ({', '.join(f'{t:.2f}' for t in ts)} s)",
+                      f"{len(ts)} runs after 1 warm-up ({', '.join(f'{t:.2f}' for t in ts)} s)",
             "np_convolve_power_ms_per_cell": conv * 1e3, "host": info}
 
 
@@ -249,7 +250,7 @@ def cpu_baseline_k4(args, terr, info, build):
     return out
 
 
-def cpu_baseline_k5(args, terr, info, cells=3):
+def cpu_baseline_k5(args, terr, info):
     """coverage.py:38-57 literally on the host for seeded K5 cells of the terrain map: per cell a
     1M-ray trace with its icosphere (oracle BVH path), host CIR, np.convolve power."""
     from oracle import oracle as orc
@@ -258,7 +259,7 @@ def cpu_baseline_k5(args, terr, info, cells=3):
 
     E = orc.Mesh(terr.vertices, terr.faces)
     grid = CoverageGrid.square(args.k5_grid, 50.0, 2.0)
-    ids = np.random.default_rng(5).choice(grid.num_cells, cells, replace=False)
+    ids = np.random.default_rng(5).choice(grid.num_cells, args.cpu_cells, replace=False)
     cen = grid.centers().reshape(-1, 3)[ids]
     N, B, tx = args.k5_rays, 3, (10.0, 0.0, 4.5)
 
@@ -269,11 +270,12 @@ def cpu_baseline_k5(args, terr, info, cells=3):
                           nthreads=info["threads_used"])
             ir = orc.cir_from_paths(orc.clean_paths(o["received"], o["mask"]), 1, N, 2.998e8, 100e9, 200e-9)
             orc.signal_power(ir, 200e-9)
-    med, ts = _median_runs(run, max(1, args.cpu_runs // 2))
+    med, ts = _median_runs(run, args.cpu_runs)
     return {"value": len(ids) / med, "unit": "cells/s", "cores": info["threads_used"], "kind": "port",
             "sample": f"{len(ids)} seeded K5 cells ({', '.join(str(int(c)) for c in ids)}), each the reference loop "
                       f"body: {N}-ray trace over the terrain stand-in with its icosphere (oracle BVH path) + host "
-                      f"CIR + np.convolve power; median of {len(ts)} runs ({', '.join(f'{t:.2f}' for t in ts)} s)",
+                      f"CIR + np.convolve power; median of {len(ts)} runs after 1 warm-up "
+                      f"({', '.join(f'{t:.2f}' for t in ts)} s)",
             "host": info}
 
 
@@ -532,6 +534,34 @@ def terrain_legs(args, local, rank, world, dist):
     return k4, k5
 
 
+def summary(out):
+    """Every leg's headline figures in one compact block (printed last in the line)."""
+    def r(x, nd=4):
+        return None if x is None else float(f"{x:.{nd}g}")
+
+    def roof(leg):
+        rf = (leg or {}).get("roofline") or {}
+        return r(rf.get("frac"), 3), r(rf.get("kernel_ms"), 4)
+
+    s = {"k2": {"value": r(out["value"]), "ms_per_step": r(out["ms_per_step"]),
+                "roofline_frac": r(out["roofline"]["frac"], 3), "kernel_ms": r(out["roofline"]["kernel_ms"]),
+                "cpu": r((out.get("cpu_baseline") or {}).get("value"))}}
+    for key, name in (("k1_plumbing", "k1"), ("k4_terrain", "k4")):
+        leg = out.get(key)
+        if leg:
+            f, k = roof(leg)
+            s[name] = {"value": r(leg["value"]), "ms_per_step": r(leg["ms_per_step"]), "roofline_frac": f,
+                       "kernel_ms": k, "cpu": r((leg.get("cpu_baseline") or {}).get("value"))}
+    for key, name in (("coverage", "k3"), ("k5_terrain_coverage", "k5")):
+        leg = out.get(key)
+        if leg:
+            f, k = roof(leg)
+            s[name] = {"value": r(leg["value"]), "ms_per_map": r(leg["ms_per_map"]), "roofline_frac": f,
+                       "traj_ms": k, "replay_ms": r((leg.get("stage_ms") or {}).get("replay_ms")),
+                       "cpu": r((leg.get("cpu_baseline") or {}).get("value"))}
+    return s
+
+
 def main():
     args = parse()
     import torch
@@ -730,6 +760,7 @@ def main():
             if k1_out is not None:
                 cb1 = cpu_baseline_k1(args, info, build)
                 k1_out["cpu_baseline"], k1_out["cpu_baseline_1thread"] = cb1["all"], cb1["1thread"]
+        out["summary"] = summary(out)  # last key: survives a truncated tail of the line
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

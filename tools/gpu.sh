@@ -21,8 +21,7 @@
 #   tracevar  tools/trace_variants.py over LIBS (SCENE=room|terrain)         -> ${TAG}_trace.jsonl
 #   k2var     tools/k2_fused_variants.py over LIBS                           -> ${TAG}_k2.jsonl
 #   k4write   rocprofv3 --pmc WRITE_SIZE / FETCH_SIZE over tools/k4_write_ab.py, per library in LIBS
-#   hashbench tools/hash_bench (build it first, hipcc line in its header)    -> ${TAG}_hash_bench.jsonl
-#   ossort    tools/os_sort_bench vs rocPRIM (build it first, header)         -> ${TAG}_os_sort.jsonl
+#   ossort    tools/os_sort_bench vs rocPRIM (built on the box)               -> ${TAG}_os_sort.jsonl
 #   rehearse  bench.py N=2,4 on this one GPU (gloo, RFRT_BENCH_ONE_GPU=1)    -> ${TAG}_rehearse_<n>.log
 #   full      = tests smoke bench
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
@@ -99,17 +98,12 @@ run_task() {
           rc=$?; echo "k4write $b $c rc=$rc"; tail -1 gpurun_out/prof_${TAG}/k4w_${b}_$c.log | cut -c1-300; step_rc $rc "k4write $b"
         done
       done ;;
-    hashbench)
-      for n in 1048576 8388608; do
-        for h in 0.0 0.5; do
-          timeout -k 10 120 tools/hash_bench $n $h >> ${O}_hash_bench.jsonl 2>&1
-          rc=$?; step_rc $rc "hashbench $n $h"
-        done
-      done
-      cat ${O}_hash_bench.jsonl ;;
     ossort)
+      # tool binaries are not pushed (.gpurunignore): build on the box, same image
+      timeout -k 10 300 hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/os_sort_bench.hip -o /tmp/os_sort_bench
+      rc=$?; step_rc $rc "ossort build"
       for a in "1048576 30 0.5" "786432 35 0.5" "7864320 31 0.3" "6291456 36 0.3" "200000 30 0.5"; do
-        timeout -k 10 60 tools/os_sort_bench $a >> ${O}_os_sort.jsonl 2>&1
+        timeout -k 10 60 /tmp/os_sort_bench $a >> ${O}_os_sort.jsonl 2>&1
         rc=$?; tail -1 ${O}_os_sort.jsonl; step_rc $rc "ossort $a"
       done ;;
     rehearse)
