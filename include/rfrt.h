@@ -159,12 +159,19 @@ int rt_coverage_trace_records_packed(rt_coverage* cov, const float* tx_pos, doub
                                      int64_t max_out, int64_t* counts, int64_t* stats, void* stream);
 /* keys_out (cell << 32 | bin), sums_out (3 uint64 per record): device, max_out >= sum(counts). */
 int rt_coverage_records(rt_coverage* cov, uint64_t* keys_out, uint64_t* sums_out, int64_t max_out, void* stream);
+/* The last trace's records as rt_coverage_trace_records_packed's 32-B rows (device, 16-B aligned,
+ * max_out >= sum(counts)): fetches them when that call's rows_out was too small (stats[2] = 0),
+ * instead of tracing again. */
+int rt_coverage_records_packed(rt_coverage* cov, uint64_t* rows_out, int64_t max_out, void* stream);
 /* keys (cell << 32 | bin) and sums (3 uint64 per record) received from every rank, in any order. */
 int rt_coverage_power_records(rt_coverage* cov, const uint64_t* keys, const uint64_t* sums, int64_t n, int64_t n_bins,
                               double alpha, double* power, void* stream);
 /* rt_coverage_power_records for records that arrive as nseg (<= 64) segments of seg_counts[t]
  * records (host array), segment t from rank t, each in rt_coverage_records' order (ascending keys,
- * no repeated key): the segments are merged by rank instead of sorted (one launch). */
+ * no repeated key): the segments are merged by rank instead of sorted (one launch).
+ * PRECONDITION, not checked: every segment strictly ascending -- what rt_coverage_records /
+ * _trace_records_packed emit and an all-to-all delivers.  Records in any other order give a wrong
+ * map, not an error; send them through rt_coverage_power_records (which sorts) instead. */
 int rt_coverage_power_segments(rt_coverage* cov, const uint64_t* keys, const uint64_t* sums, const int64_t* seg_counts,
                                int nseg, int64_t n_bins, double alpha, double* power, void* stream);
 /* rt_coverage_power_segments on received (key, sum) rows of rt_coverage_trace_records_packed's

@@ -66,6 +66,7 @@ def lib():
     L.rt_coverage_trace_records.argtypes = [_vp, _vp, ctypes.c_double, ctypes.c_double, ctypes.c_double, _int, _i64,
                                             _vp, _vp, _vp]
     L.rt_coverage_records.argtypes = [_vp, _vp, _vp, _i64, _vp]
+    L.rt_coverage_records_packed.argtypes = [_vp, _vp, _i64, _vp]
     L.rt_coverage_trace_records_to.argtypes = [_vp, _vp, ctypes.c_double, ctypes.c_double, ctypes.c_double, _int,
                                                _i64, _vp, _vp, _i64, _vp, _vp, _vp]
     L.rt_coverage_power_records.argtypes = [_vp, _vp, _vp, _i64, _i64, ctypes.c_double, _vp, _vp]
@@ -89,6 +90,7 @@ def lib():
     for name in ("rt_mesh_create", "rt_mesh_create_ex", "rt_mesh_destroy", "rt_mesh_info", "rt_bvh_info", "rt_trace", "rt_compact", "rt_cir", "rt_trace_cir",
                  "rt_coverage_create", "rt_coverage_destroy", "rt_coverage_run", "rt_coverage_received",
                  "rt_coverage_create_rays", "rt_coverage_trace_records", "rt_coverage_trace_records_to", "rt_coverage_records",
+                 "rt_coverage_records_packed",
                  "rt_coverage_power_records", "rt_coverage_power_segments", "rt_coverage_trace_records_packed",
                  "rt_coverage_power_packed", "rt_coverage_amps_to_sums", "rt_coverage_profile", "rt_coverage_last_profile", "rt_debug_poison",
                  "rt_profile", "rt_trace_last_profile", "rt_trace_profile_stats",

@@ -194,29 +194,32 @@ class Coverage:
         stats = np.zeros(3, np.int64)
         dev = f"cuda:{self.device}"
         if getattr(self, "_rows", None) is None:
-            self._rows = torch.empty((max(self.ray_count * 4, 1 << 16), 4), dtype=torch.int64, device=dev)
-        for attempt in range(2):
-            rows = self._rows
-            check(lib().rt_coverage_trace_records_packed(
-                self._h, tx.ctypes.data, float(tx_power), float(self.light_speed_mps), float(self.sample_rate_hz),
-                cir_flags(self.light_speed_mps, self.sample_rate_hz), self.n_bins, ptr(rows), rows.shape[0],
-                counts.ctypes.data, stats.ctypes.data, _lib.stream_handle(self.device)),
-                "rt_coverage_trace_records_packed")
-            n = int(counts.sum())
-            if stats[2] or n == 0:
-                break
-            # more records than the buffer holds: grow it and trace again (the plan keeps no
-            # packed copy to fetch; this happens once per plan at most)
-            self._rows = torch.empty((n + n // 4 + 1024, 4), dtype=torch.int64, device=dev)
+            # grow-only; a first guess of 2 records per ray (K3 ranks send ~1.6, K5 ~3.7): an
+            # overflow fetches the records from the plan (rt_coverage_records_packed), no re-trace
+            self._rows = torch.empty((max(self.ray_count * 2, 1 << 16), 4), dtype=torch.int64, device=dev)
+        rows = self._rows
+        check(lib().rt_coverage_trace_records_packed(
+            self._h, tx.ctypes.data, float(tx_power), float(self.light_speed_mps), float(self.sample_rate_hz),
+            cir_flags(self.light_speed_mps, self.sample_rate_hz), self.n_bins, ptr(rows), rows.shape[0],
+            counts.ctypes.data, stats.ctypes.data, _lib.stream_handle(self.device)),
+            "rt_coverage_trace_records_packed")
+        n = int(counts.sum())
+        if n and not stats[2]:
+            self._rows = rows = torch.empty((n + n // 4 + 1024, 4), dtype=torch.int64, device=dev)
+            check(lib().rt_coverage_records_packed(self._h, ptr(rows), rows.shape[0], _lib.stream_handle(self.device)),
+                  "rt_coverage_records_packed")
         self.last_candidates = int(stats[0])
         return rows[:n], [int(c) for c in counts]
 
     def power_from_rows(self, rows, counts):
         """power_from_records for (n, 4) int64 rows of trace_rows' layout arriving as consecutive
-        segments, counts[t] rows from rank t (exchange_rows' output)."""
+        segments, counts[t] rows from rank t (exchange_rows' output).  Each segment must be in
+        trace_rows' order (strictly ascending keys): the segments are merged, not sorted, and other
+        orders give a wrong map, not an error (use power_from_records without counts for those)."""
+        import torch
         n = int(rows.shape[0]) if rows.dim() == 2 else 0
-        if n and (tuple(rows.shape) != (n, 4) or not rows.is_contiguous()):
-            raise ValueError(f"rows must be a contiguous (n, 4) int64 tensor, got {tuple(rows.shape)}")
+        if n and (tuple(rows.shape) != (n, 4) or not rows.is_contiguous() or rows.dtype != torch.int64):
+            raise ValueError(f"rows must be a contiguous (n, 4) int64 tensor, got {tuple(rows.shape)} {rows.dtype}")
         c = np.ascontiguousarray(np.asarray(counts, dtype=np.int64))
         if int(c.sum()) != n or (c < 0).any():
             raise ValueError(f"segment counts {c.tolist()} do not add up to the {n} rows")
@@ -229,9 +232,10 @@ class Coverage:
         """Ray mode, last stage: the power of this rank's cells from the records every rank sent it
         (keys and (n, 3) fixed-point sums); the (num_cells,) float64 device map, 0 elsewhere.
         counts: the number of records from each source rank, when they arrive as consecutive
-        segments in trace_records' order (ascending keys per segment, as exchange_records delivers
-        them): the segments are merged by rank (rt_coverage_power_segments).  Without counts the
-        records may come in any order and are sorted (rt_coverage_power_records)."""
+        segments in trace_records' order (strictly ascending keys per segment, as exchange_records
+        delivers them; not checked -- another order gives a wrong map): the segments are merged by
+        rank (rt_coverage_power_segments).  Without counts the records may come in any order and are
+        sorted (rt_coverage_power_records)."""
         n = int(keys.numel())
         if n and tuple(sums.shape) != (n, 3):
             raise ValueError(f"sums must be (n, 3) int64 fixed point, got {tuple(sums.shape)}")

@@ -556,11 +556,19 @@ __global__ __launch_bounds__(256, RT_TRAJ_SPLIT_WAVES) void k_traj_split(CovPara
     bool alive = valid;
     for (int k = 0; k < p.B; ++k) {
       const rt::Shear s = rt::make_shear(pos, dir);
+#if RT_BVH_WIDTH == 8
+      rt::Walk8 w;
+#else
       rt::Walk4 w;
+#endif
       rt::WalkStack st = rt::make_stack();
       bool active = false;
       if (alive) {
+#if RT_BVH_WIDTH == 8
+        rt::split_init8<G>(w, st, p.env_bvh, s, pos, dir, j);
+#else
         rt::split_init<G>(w, st, p.env_bvh, s, pos, dir, j);
+#endif
         active = true;
       } else {
         rt::hit_init(w.h);
@@ -1245,6 +1253,13 @@ __global__ __launch_bounds__(256) void k_sel_scatter(const uint8_t* flag, const 
 #ifndef RT_COV_BVH_DIRKEY
 #define RT_COV_BVH_DIRKEY 0
 #endif
+// RT_REPLAY_RAY_KEY (brute-force scenes): after the bounces left, the ray's trajectory slot
+// instead of direction and cell.  The LDS brute force tests every face whatever the direction, so
+// direction coherence buys little there, while slot order makes a wave's trajectory, key and trx
+// reads fall on shared lines (K3 k_replay<false> fetched 1.24 GB per launch at L2 hit 0.19).
+#ifndef RT_REPLAY_RAY_KEY
+#define RT_REPLAY_RAY_KEY 0
+#endif
 template <bool USE_BVH>
 __device__ __forceinline__ uint16_t replay_key(const CovParams& p, uint64_t key) {
   {
@@ -1268,6 +1283,10 @@ __device__ __forceinline__ uint16_t replay_key(const CovParams& p, uint64_t key)
     for (int b = 0; b < 5; ++b) mz |= ((cx >> b) & 1u) << (2 * b) | ((cy >> b) & 1u) << (2 * b + 1);
     if (USE_BVH && RT_COV_BVH_DIRKEY) return (uint16_t)((dy * 8 + dx) << 10 | mz);
     const uint32_t rem = (uint32_t)min(max(p.B - 1 - k0, 0), 3);
+    if (!USE_BVH && RT_REPLAY_RAY_KEY) {  // brute force: the ray's trajectory slot after the bounces left
+      const int sh = max(0, 32 - __clz((int)max(p.n - 1, (int64_t)1)) - 14);
+      return (uint16_t)(rem << 14 | ((uint32_t)(r >> sh) & 0x3FFFu));
+    }
     return (uint16_t)(rem << 14 | (dy * 8 + dx) << 8 | mz >> 2);
   }
 }
@@ -1289,7 +1308,7 @@ __global__ __launch_bounds__(256) void k_replay_keys(CovParams p, const uint64_t
 #define RT_REPLAY_WINDOW 1
 #endif
 #ifndef RT_REPLAY_WIN_ITEMS
-#define RT_REPLAY_WIN_ITEMS 8
+#define RT_REPLAY_WIN_ITEMS 4  // 4096-entry windows: twice the blocks for a rank's list; K5 rank of 8 1.088 -> 1.003 ms, K3 0.99 -> 0.92 (r4c)
 #endif
 constexpr int kReplayWin = 1024 * RT_REPLAY_WIN_ITEMS;
 // Larger lists (one GPU's whole map: K3 7.9M, K5 6.4M first wins) keep the device-wide sort: there
@@ -1406,6 +1425,53 @@ __global__ __launch_bounds__(256) void k_merge_segments(const uint64_t* keys, in
       }
       pos += a - so.off[t];
     }
+    keys_out[pos] = k;
+    idx_out[pos] = i;
+  }
+}
+// The same merge with the nseg - 1 binary searches of an element run in lockstep (NS >= nseg
+// segments, `steps` = the longest search): each step issues its loads for every segment at once,
+// so a thread waits `steps` memory latencies instead of (nseg - 1) x steps -- the searches over
+// L2-resident keys are a chain of dependent loads, and k_merge_segments' time was that chain
+// (52 us for a K5 owner's 465k records, profiles/r3zg_k5_rank_timeline.txt).
+#ifndef RT_MERGE_LOCKSTEP
+#define RT_MERGE_LOCKSTEP 1
+#endif
+template <int NS>
+__global__ __launch_bounds__(256) void k_merge_lockstep(const uint64_t* keys, int64_t kstride, SegOffsets so,
+                                                        int steps, uint64_t* keys_out, int64_t* idx_out) {
+  const int64_t n = so.off[so.nseg];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int sg = 0;
+    while (sg + 1 < so.nseg && so.off[sg + 1] <= i) ++sg;
+    const uint64_t k = keys[i * kstride];
+    int64_t a[NS], len[NS];
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+      a[t] = t < so.nseg ? so.off[t] : 0;
+      len[t] = (t < so.nseg && t != sg) ? so.off[t + 1] - so.off[t] : 0;
+    }
+    for (int st = 0; st < steps; ++st) {
+      uint64_t km[NS];
+#pragma unroll
+      for (int t = 0; t < NS; ++t) {  // every segment's probe first: independent loads
+        const int64_t m = a[t] + (len[t] >> 1);
+        km[t] = keys[(len[t] > 0 ? m : i) * kstride];
+      }
+#pragma unroll
+      for (int t = 0; t < NS; ++t) {  // first element > k (t < sg) or >= k (t > sg)
+        if (len[t] > 0) {
+          const int64_t half = len[t] >> 1;
+          const bool right = km[t] < k || (t < sg && km[t] == k);
+          a[t] = right ? a[t] + half + 1 : a[t];
+          len[t] = right ? len[t] - half - 1 : half;
+        }
+      }
+    }
+    int64_t pos = i - so.off[sg];
+#pragma unroll
+    for (int t = 0; t < NS; ++t)
+      if (t < so.nseg && t != sg) pos += a[t] - so.off[t];
     keys_out[pos] = k;
     idx_out[pos] = i;
   }
@@ -1648,9 +1714,11 @@ __global__ __launch_bounds__(64) void k_power_small(TermArrays G, const int32_t*
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int lane = threadIdx.x & 63;
   if (nshard > 1) {  // other ranks' cells: 0 (the map is sum-reduced), instead of a fill
-    const int64_t ncell = g.nx * g.ny * g.nz;
-    for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < ncell; c += stride)
-      if ((c % g.nx) % nshard != shard) power[c] = 0.0;
+    // 32-bit index arithmetic (cells < 2^32, rt_coverage_create): a 64-bit division by a run-time
+    // divisor is a ~100-instruction sequence, and this loop visits every cell of the map
+    const uint32_t ncell = (uint32_t)(g.nx * g.ny * g.nz), nx = (uint32_t)g.nx, ns = (uint32_t)nshard;
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < ncell; c += (uint32_t)stride)
+      if ((c % nx) % ns != (uint32_t)shard) power[c] = 0.0;
   }
   for (int64_t base = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); base < nown; base += stride) {
     const int64_t t = base + lane;
@@ -1906,6 +1974,7 @@ struct rt_coverage {
   int shard = 0, nshard = 1;
   // buffers
   float4* traj = nullptr;  // n * B * 2 float4
+  int32_t* ray_order = nullptr;  // BVH scenes: the plan's rays sorted by initial direction (first run)
   uint8_t* nseg = nullptr;
   uint64_t *keys = nullptr, *keys_sorted = nullptr, *okeys = nullptr, *okeys_sorted = nullptr, *ukeys = nullptr;
   double *oamps = nullptr, *oamps_sorted = nullptr, *uamps = nullptr;
@@ -2392,7 +2461,6 @@ hipError_t sort_records(void* tmp, size_t& bytes, const uint64_t* kin, uint64_t*
   return rocprim::radix_sort_pairs(tmp, bytes, kin, kout, vin, vout, (unsigned)n, 0u, (unsigned)end_bit, s);
 }
 
-
 int alloc_cands(rt_coverage* c, int64_t cap) {
   free_cands(c);
   RT_HIP(hipMalloc(&c->keys, cap * 8));
@@ -2639,9 +2707,18 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
   p.zero_ctr = c->counters;  // zeroed by the trajectory kernel (first attempt; retries use a fill)
   for (bool& r : c->ev_rec) r = false;
   if (bvh) {  // direction-sorted rows: coherent BVH traversal (as rt_trace)
-    void* ws = nullptr;
-    p.order = rt::dir_order(c->ray_offset, c->n, s, &ws);
-    if (!p.order) return RT_EHIP;
+    // The order depends only on the plan's ray ids (their initial directions, kernel.py:51-52), so
+    // the plan sorts once, on its first run, and keeps the permutation (rt_trace, which has no
+    // plan, sorts per call).  K5: ~0.1 ms per one-GPU map, a fixed ~30 us per rank of 8.
+    if (!c->ray_order) {
+      void* ws = nullptr;
+      const int32_t* o = rt::dir_order(c->ray_offset, c->n, s, &ws);
+      if (!o) return RT_EHIP;
+      RT_HIP(hipMalloc(&c->ray_order, sizeof(int32_t) * (size_t)c->n));
+      RT_HIP(hipMemcpyAsync(c->ray_order, o, sizeof(int32_t) * (size_t)c->n, hipMemcpyDeviceToDevice, s));
+      RT_HIP(hipFreeAsync(ws, s));
+    }
+    p.order = c->ray_order;
     prof_mark(c, 0, s);
     if (c->n <= traj_split_max_rays())  // too few rays to fill the GPU: four lanes per ray
       hipLaunchKernelGGL(k_traj_split<RT_TRAJ_SPLIT_G>,
@@ -2650,7 +2727,6 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
     else
       hipLaunchKernelGGL(k_traj<true>, dim3(grid_rays), dim3(256), lds, s, p);
     prof_mark(c, 1, s);
-    RT_HIP(hipFreeAsync(ws, s));
     p.order = nullptr;
   } else {
     prof_mark(c, 0, s);
@@ -2749,7 +2825,13 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
     // the list holds at most cap entries (one per candidate)
     RT_HIP(hipMemcpyAsync(c->hcnt, c->counters, 24, hipMemcpyDeviceToHost, s));
     RT_HIP(hipEventRecord(c->ev_cnt, s));
-    replayed = RT_REPLAY_EARLY && RT_REPLAY_WINDOW && (c->last_list > 0 ? c->last_list : c->cap) <= kReplayWindowMax;
+    // early (windowed) replay only for rank plans of a ray-sharded map, whose lists are a rank's
+    // share: a one-GPU or cell-sharded plan's whole-map list takes the device-wide sort,
+    // which needs the length on the host.  The previous run's length (or the cap) sizes the grid and
+    // vetoes the window order once a rank's list outgrows kReplayWindowMax; the kernels stride over
+    // the device count either way, so a stale length costs time, never correctness.
+    replayed = RT_REPLAY_EARLY && RT_REPLAY_WINDOW && c->ray_mode && c->nshard > 1 &&
+               (c->last_list > 0 ? c->last_list : c->cap) <= kReplayWindowMax;
     if (replayed) {
       int rc = launch_replay(c->cap, (const unsigned long long*)c->counters + 2, true,
                              c->last_list > 0 ? c->last_list + c->last_list / 8 : c->cap);
@@ -2966,6 +3048,7 @@ int rt_coverage_destroy(rt_coverage* c) {
   rt::DeviceGuard dg(c->device);
   free_cands(c);
   if (c->traj) (void)hipFree(c->traj);
+  if (c->ray_order) (void)hipFree(c->ray_order);
   if (c->nseg) (void)hipFree(c->nseg);
   if (c->counters) (void)hipFree(c->counters);
   if (c->nuniq) (void)hipFree(c->nuniq);
@@ -3148,6 +3231,25 @@ int rt_coverage_records(rt_coverage* c, uint64_t* keys_out, uint64_t* sums_out, 
   return RT_OK;
 }
 
+int rt_coverage_records_packed(rt_coverage* c, uint64_t* rows_out, int64_t max_out, void* stream) {
+  if (!c || !c->ray_mode || (c->n_out > 0 && !rows_out) || max_out < c->n_out ||
+      (reinterpret_cast<uintptr_t>(rows_out) & 15)) {
+    rt::set_error("rt_coverage_records_packed: invalid arguments (16-B aligned rows, max_out >= the sum of the counts)");
+    return RT_EINVAL;
+  }
+  if (c->n_out == 0) return RT_OK;
+  hipStream_t s = (hipStream_t)stream;
+  rt::DeviceGuard dg(c->device);
+  RT_HIP(dg.err);
+  // the reduced records are still in the plan (ukeys / sums, valid ones first): the same rows
+  // k_bounds_strip writes (its bounds are rewritten with the same values)
+  hipLaunchKernelGGL(k_bounds_strip, dim3((unsigned)std::min<int64_t>((c->n_out + 256) / 256, 4096)), dim3(256), 0, s,
+                     c->ukeys, plan_sums(c), c->nuniq, c->nshard, max_out, own_shift(c), c->bounds, rows_out,
+                     (Fx192*)nullptr, 1);
+  RT_HIP(hipGetLastError());
+  return RT_OK;
+}
+
 int rt_coverage_amps_to_sums(const double* amps, int64_t n, uint64_t* sums, void* stream) {
   if (n < 0 || (n > 0 && (!amps || !sums))) {
     rt::set_error("rt_coverage_amps_to_sums: invalid arguments");
@@ -3247,8 +3349,18 @@ int power_segments_impl(rt_coverage* c, const uint64_t* keys, const uint64_t* su
     int64_t* idx_sorted = reinterpret_cast<int64_t*>(c->oamps_sorted);
     // (G lanes per element, one binary search each, then a group sum: no faster on K3's 200k
     // records, 46 -> 76 us on K5's 465k -- the searches' loads, not their latency, set the time)
-    hipLaunchKernelGGL(k_merge_segments, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 8192)), dim3(256), 0, s, keys,
-                       stride, so, c->okeys_sorted, idx_sorted);
+    int64_t longest = 0;
+    for (int t = 0; t < nseg; ++t) longest = std::max<int64_t>(longest, seg_counts[t]);
+    const int steps = bits_for((uint64_t)longest);  // a search over len keys takes <= bits(len) halvings
+    const dim3 gm((unsigned)std::min<int64_t>((n + 255) / 256, 8192));
+    if (RT_MERGE_LOCKSTEP && nseg <= 2)
+      hipLaunchKernelGGL(k_merge_lockstep<2>, gm, dim3(256), 0, s, keys, stride, so, steps, c->okeys_sorted, idx_sorted);
+    else if (RT_MERGE_LOCKSTEP && nseg <= 4)
+      hipLaunchKernelGGL(k_merge_lockstep<4>, gm, dim3(256), 0, s, keys, stride, so, steps, c->okeys_sorted, idx_sorted);
+    else if (RT_MERGE_LOCKSTEP && nseg <= 8)
+      hipLaunchKernelGGL(k_merge_lockstep<8>, gm, dim3(256), 0, s, keys, stride, so, steps, c->okeys_sorted, idx_sorted);
+    else
+      hipLaunchKernelGGL(k_merge_segments, gm, dim3(256), 0, s, keys, stride, so, c->okeys_sorted, idx_sorted);
     RT_HIP(hipGetLastError());
     WideKey wk{};
     wk.identity = true;

@@ -417,7 +417,165 @@ __device__ __forceinline__ Hit group_hit(Hit h) {
   return h;
 }
 
-#if RT_BVH_WIDE
+// ---- Compressed 8-wide nodes (RT_BVH_WIDTH 8, bvh_wide.hip build_wide / emit_node8), 128 B each:
+//   dwords 0..2  grid origin (x, y, z) = the node box's low corner
+//   dword  3     per-axis step exponents: byte a = e_a + 127, step 2^e_a
+//   dwords 4..15 quantised child bounds, one byte per child: lo.x[8] hi.x[8] lo.y[8] hi.y[8] lo.z[8] hi.z[8]
+//   dwords 16..23 child refs (int): >= 0 wide node, -1 empty slot, <= -2 leaf ~(first << 3 | count)
+// A child's bound is origin + q * 2^e, rounded outward on the host in the same f32 arithmetic, so
+// the decoded box contains the binary tree's padded box and culling stays conservative.  Per child
+// 16 B instead of Walk4's 32 B, and three binary levels per node instead of two: fewer dependent
+// node fetches per query.  The slab test works relative to the ray origin: (origin - o) once per
+// node and axis, then fmaf(q, 2^e, origin - o) per bound -- within an ulp or two of the absolute
+// form, far inside the boxes' 1e-5 padding.
+#ifndef RT_BVH_WIDTH
+#define RT_BVH_WIDTH 4
+#endif
+__device__ __forceinline__ float byte_f(uint32_t w, int b) { return (float)((w >> (8 * b)) & 0xFFu); }
+__device__ __forceinline__ float exp_step(uint32_t e, int a) {
+  return __uint_as_float(((e >> (8 * a)) & 0xFFu) << 23);
+}
+
+// the 8 child boxes of a compressed node against the ray: entry t (INF on a miss) and refs
+struct Node8 {
+  float t[8];
+  int ref[8];
+};
+__device__ __forceinline__ void visit8(const BvhView& b, int node, const RayBox& r, Node8& out) {
+  const float4* w = b.wide + 8 * (int64_t)node;
+  const float4 h = w[0], qa = w[1], qb = w[2], qc = w[3], ra = w[4], rb = w[5];
+  const uint32_t eb = __float_as_uint(h.w);
+  const float sx = exp_step(eb, 0), sy = exp_step(eb, 1), sz = exp_step(eb, 2);
+  const float dx = h.x - r.ox, dy = h.y - r.oy, dz = h.z - r.oz;
+  const uint32_t lxw[2] = {__float_as_uint(qa.x), __float_as_uint(qa.y)};
+  const uint32_t hxw[2] = {__float_as_uint(qa.z), __float_as_uint(qa.w)};
+  const uint32_t lyw[2] = {__float_as_uint(qb.x), __float_as_uint(qb.y)};
+  const uint32_t hyw[2] = {__float_as_uint(qb.z), __float_as_uint(qb.w)};
+  const uint32_t lzw[2] = {__float_as_uint(qc.x), __float_as_uint(qc.y)};
+  const uint32_t hzw[2] = {__float_as_uint(qc.z), __float_as_uint(qc.w)};
+  const int refs[8] = {__float_as_int(ra.x), __float_as_int(ra.y), __float_as_int(ra.z), __float_as_int(ra.w),
+                       __float_as_int(rb.x), __float_as_int(rb.y), __float_as_int(rb.z), __float_as_int(rb.w)};
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const int wd = c >> 2, by = c & 3;
+    const float tx0 = fmaf(byte_f(lxw[wd], by), sx, dx) * r.ix, tx1 = fmaf(byte_f(hxw[wd], by), sx, dx) * r.ix;
+    const float ty0 = fmaf(byte_f(lyw[wd], by), sy, dy) * r.iy, ty1 = fmaf(byte_f(hyw[wd], by), sy, dy) * r.iy;
+    const float tz0 = fmaf(byte_f(lzw[wd], by), sz, dz) * r.iz, tz1 = fmaf(byte_f(hzw[wd], by), sz, dz) * r.iz;
+    const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+    const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+    out.ref[c] = refs[c];
+    out.t[c] = (refs[c] != -1 && tn <= tf * 1.00001f + 1e-6f) ? tn : INFINITY;
+  }
+}
+
+struct Walk8 {
+  Hit h;
+  RayBox r;
+  float tc;
+  int cur, sp;
+
+  __device__ __forceinline__ void init(float3 o, float3 d, float tcull = RT_MAX_T) {
+    hit_init(h);
+    tc = fminf(RT_MAX_T, tcull);
+    r = make_raybox(o, d);
+    cur = 0;
+    sp = 0;
+  }
+  __device__ __forceinline__ void push(WalkStack& st, int c, float t) {
+    if (sp < RT_BVH_STACK) {  // cannot overflow: bound checked on the host (build_wide)
+      st.set(sp, c, t);
+      ++sp;
+    }
+  }
+  // one visited node's children: hit leaves tested nearest first, then the nearest hit inner child
+  // is visited next and the others pushed far to near
+  __device__ __forceinline__ void expand(const BvhView& b, const Shear& s, WalkStack& st, const Node8& nd) {
+    uint32_t leaves = 0, inner = 0;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      leaves |= (nd.ref[c] < -1 && nd.t[c] < INFINITY) ? 1u << c : 0u;
+      inner |= (nd.ref[c] >= 0 && nd.t[c] < INFINITY) ? 1u << c : 0u;
+    }
+#pragma unroll 1
+    while (leaves) {
+      float bt = INFINITY;
+      int bref = 0, bc = 0;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const bool take = ((leaves >> c) & 1u) && nd.t[c] < bt;
+        bt = take ? nd.t[c] : bt;
+        bref = take ? nd.ref[c] : bref;
+        bc = take ? c : bc;
+      }
+      if (!(bt <= cull_limit(h, tc))) break;
+      const int pk = ~bref;
+      leaf4(b, s, pk >> 3, pk & 7, h);
+      leaves &= ~(1u << bc);
+    }
+    const float lim = cull_limit(h, tc);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) inner &= nd.t[c] <= lim ? ~0u : ~(1u << c);
+    cur = -1;
+#pragma unroll 1
+    while (inner) {
+      // the farthest remaining child is pushed; the last one left (the nearest) is visited next
+      float bt = -1.0f;
+      int bref = 0, bc = 0;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const bool take = ((inner >> c) & 1u) && nd.t[c] > bt;
+        bt = take ? nd.t[c] : bt;
+        bref = take ? nd.ref[c] : bref;
+        bc = take ? c : bc;
+      }
+      inner &= ~(1u << bc);
+      if (inner) push(st, bref, bt);
+      else cur = bref;
+    }
+  }
+  __device__ __forceinline__ bool step(const BvhView& b, const Shear& s, WalkStack& st) {
+    if (cur < 0) {  // pop
+      if (sp == 0) return false;
+      --sp;
+      if (!(st.get_t(sp) <= cull_limit(h, tc))) return true;
+      cur = st.get_node(sp);
+    }
+    Node8 nd;
+    visit8(b, cur, r, nd);
+    expand(b, s, st, nd);
+    return true;
+  }
+};
+
+// Walk8 over G lanes (G = 4 or 8) tracing ONE ray together: lane j takes the root's children
+// c = j, j + G, ... (a leaf child tested on the spot, an inner child pushed when hit); the group's
+// (t, face) minimum is the ray's closest hit (group_hit), each lane culling with the group's best t
+// (group_min_t), as split_init for Walk4.
+template <int G>
+__device__ __forceinline__ void split_init8(Walk8& w, WalkStack& st, const BvhView& b, const Shear& s, float3 o,
+                                            float3 d, int j, float tcull = RT_MAX_T) {
+  static_assert(G == 4 || G == 8, "split over 4 or 8 lanes");
+  w.init(o, d, tcull);
+  w.cur = -1;
+  Node8 nd;
+  visit8(b, 0, w.r, nd);
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    if ((c & (G - 1)) != j) {
+      nd.t[c] = INFINITY;
+      nd.ref[c] = -1;
+    }
+  }
+  w.expand(b, s, st, nd);
+  if (w.cur >= 0) {  // the lane's nearest inner child goes on the stack too: step() starts by popping
+    w.push(st, w.cur, 0.0f);
+    w.cur = -1;
+  }
+}
+
+#if RT_BVH_WIDTH == 8
+using Walk = Walk8;
+#elif RT_BVH_WIDE
 using Walk = Walk4;
 #else
 using Walk = Walk2;

@@ -118,6 +118,35 @@ __device__ __forceinline__ bool rx_maybe(const TraceArgs& a, float3 o, float3 d,
 #ifndef RT_XCD_WINDOWS
 #define RT_XCD_WINDOWS 0
 #endif
+#ifndef RT_SPARSE_RX
+#define RT_SPARSE_RX 1
+#endif
+// received rows = NaN, row_mask = 0, in row order with 16-B streaming stores (RT_SPARSE_RX)
+__global__ __launch_bounds__(256) void k_fill_received(float* received, int64_t nwords, uint32_t* mask, int64_t n) {
+  typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, str = (int64_t)gridDim.x * blockDim.x;
+  const uint32_t qn = 0x7FC00000u;
+  if (received) {
+    uint32_t* w = reinterpret_cast<uint32_t*>(received);
+    const int64_t head = (int64_t)((16 - (reinterpret_cast<uintptr_t>(w) & 15)) & 15) / 4;  // words to 16-B alignment
+    const int64_t h = head < nwords ? head : nwords;
+    const int64_t nv = (nwords - h) / 4;
+    u4v* v = reinterpret_cast<u4v*>(w + h);
+    for (int64_t i = tid; i < nv; i += str) __builtin_nontemporal_store(u4v{qn, qn, qn, qn}, v + i);
+    if (tid < h) w[tid] = qn;
+    for (int64_t i = h + 4 * nv + tid; i < nwords; i += str) w[i] = qn;
+  }
+  if (mask) {
+    const int64_t h = (int64_t)((16 - (reinterpret_cast<uintptr_t>(mask) & 15)) & 15) / 4;
+    const int64_t hh = h < n ? h : n;
+    const int64_t nv = (n - hh) / 4;
+    u4v* v = reinterpret_cast<u4v*>(mask + hh);
+    for (int64_t i = tid; i < nv; i += str) __builtin_nontemporal_store(u4v{0u, 0u, 0u, 0u}, v + i);
+    if (tid < hh) mask[tid] = 0u;
+    for (int64_t i = hh + 4 * nv + tid; i < n; i += str) mask[i] = 0u;
+  }
+}
+
 template <int P, bool NT = (RT_NT_ROWS != 0)>
 __device__ __forceinline__ void store_row_fixed(float* dst, const float (*pts)[3]) {
   if constexpr ((P * 3) % 4 == 0) {  // 16-B aligned rows (P = 4, 8): 16-byte stores
@@ -495,7 +524,12 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
         store_row_fixed<P, kNtRows>(a.traced + row * (P * 3), path);
       }
     }
-    if (a.received) {
+    // BVH kernels (RT_SPARSE_RX): launch_trace fills received (NaN) and row_mask (0) in row order
+    // first, as the reference does on the host (tracer.py:67-72), and only received rays store their
+    // row and mask word here (kernel.py:89-91): a direction-sorted burst scatters its rows, and
+    // writing every ray's NaN row and mask word cost ~0.2 GB of partial-line writes per K4 launch
+    constexpr bool kSparseRx = USE_BVH && RT_SPARSE_RX;
+    if (a.received && (!kSparseRx || last_rx >= 0)) {
       float rec[P][3];
 #pragma unroll
       for (int i = 0; i < P; ++i) {
@@ -511,7 +545,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
         store_row_fixed<P, kNtRows>(a.received + row * (P * 3), rec);
       }
     }
-    if (a.mask) {
+    if (a.mask && (!kSparseRx || last_rx >= 0)) {
       if constexpr (kNtRows) __builtin_nontemporal_store(last_rx >= 0 ? 1u : 0u, a.mask + row);
       else a.mask[row] = last_rx >= 0 ? 1u : 0u;
     }
@@ -1216,9 +1250,20 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
   // (hipExtLaunchKernelGGL), so timing adds no marker packets -- and no gaps -- to the stream
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   trace_events(&ev0, &ev1);
+  // BVH kernels store only the received rows (RT_SPARSE_RX): the fill comes first, inside the
+  // profiled span (its start event, the trace kernel's stop event)
+  const bool fill = RT_SPARSE_RX && bvh && B <= 8 && (received || mask);
+  if (fill) {
+    const unsigned gf = (unsigned)std::min<int64_t>((n * (B + 1) * 3 / 4 + 255) / 256, 4096);
+    if (ev0) hipExtLaunchKernelGGL(k_fill_received, dim3(gf), dim3(256), 0, stream, ev0, nullptr, 0, received,
+                                   (int64_t)n * (B + 1) * 3, mask, n);
+    else hipLaunchKernelGGL(k_fill_received, dim3(gf), dim3(256), 0, stream, received, (int64_t)n * (B + 1) * 3,
+                            mask, n);
+  }
+  hipEvent_t ev_start = fill ? nullptr : ev0;
 #define RT_LAUNCH(K, ...)                                                                                \
   do {                                                                                                   \
-    if (ev0) hipExtLaunchKernelGGL(K, dim3(grid), blk, lds, stream, ev0, ev1, 0, __VA_ARGS__);           \
+    if (ev0) hipExtLaunchKernelGGL(K, dim3(grid), blk, lds, stream, ev_start, ev1, 0, __VA_ARGS__);      \
     else hipLaunchKernelGGL(K, dim3(grid), blk, lds, stream, __VA_ARGS__);                              \
   } while (0)
   switch (B) {

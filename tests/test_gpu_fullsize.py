@@ -7,8 +7,11 @@ oracle (coverage.py:38-57: for that one centre a full 1M-ray trace with its icos
 of tracer.py:84-117 and the power of coverage.py:45-52): the cells whose receiver contains the
 transmitter (every ray is received), the cells with the most delay bins, cells on the wave-per-cell
 power path (> 16 bins) and the thread-per-cell one (<= 16), cells receiving a single bin, and
-random cells (mostly empty).  Bar as tests/test_gpu_coverage.py: identical bins, IR norm-wise 1e-5,
-power 1e-9 against the rounded-once arccos and 1e-5 plus the reference's own arccos spread.
+random cells (mostly empty); K5 also grid-edge and terrain-shadowed cells, 64 or more in all.  Bar:
+identical bins; every bin element-wise within 1e-9 of the reference computed with the arccos rounded
+once and within 1e-5 of the reference itself except where the reference's own float32 arccos moves
+the bin by > 1e-6 (counted and printed); power 1e-9 against the rounded-once arccos and 1e-5 plus
+the reference's own arccos spread.
 """
 import os
 import time
@@ -33,8 +36,10 @@ def _gpu(require_gpu):
     lib()
 
 
-def _sample_cells(power, cells, bins, grid, tx, r, rng, n_each=4):
-    """(cell ids, why) -- TX cells, most bins, >16 bins, <=16, single bin, random."""
+def _sample_cells(power, cells, bins, grid, tx, r, rng, n_each=4, edges=0, shadowed=0, at_least=0):
+    """(cell ids, why) -- TX cells, most bins, >16 bins, <=16, single bin, random; optionally cells
+    on the grid's edge and shadowed cells (receiving, but nothing at or before their line-of-sight
+    delay bin: the direct path is blocked by the terrain), then random cells up to at_least."""
     nb = np.bincount(cells, minlength=grid.num_cells)
     cen = grid.centers().reshape(-1, 3)
     picks = {}
@@ -55,12 +60,33 @@ def _sample_cells(power, cells, bins, grid, tx, r, rng, n_each=4):
     one = np.nonzero(nb == 1)[0]
     add(rng.choice(one, min(2, len(one)), replace=False) if len(one) else [], "single bin")
     add(rng.choice(grid.num_cells, n_each, replace=False), "random")
+    if edges:
+        ix, iy = np.arange(grid.num_cells) % grid.nx, (np.arange(grid.num_cells) // grid.nx) % grid.ny
+        edge = np.nonzero((ix == 0) | (ix == grid.nx - 1) | (iy == 0) | (iy == grid.ny - 1))[0]
+        recv = edge[nb[edge] > 0]
+        add(rng.choice(recv, min(edges // 2, len(recv)), replace=False) if len(recv) else [], "grid edge, receiving")
+        add(rng.choice(edge, edges - edges // 2, replace=False), "grid edge")
+    if shadowed:
+        first = np.full(grid.num_cells, np.iinfo(np.int64).max)
+        np.minimum.at(first, cells, bins)
+        los = ((np.linalg.norm(cen - np.asarray(tx), axis=1) - r) / 2.998e8 * 100e9).astype(np.int64)
+        sh = np.nonzero((nb > 0) & (first > los + 2))[0]
+        add(rng.choice(sh, min(shadowed, len(sh)), replace=False) if len(sh) else [], "shadowed (LOS blocked)")
+    while len(picks) < at_least:
+        add(rng.choice(grid.num_cells, at_least - len(picks), replace=False), "random")
     return picks
 
 
 def _check_cells(E, power, cells, bins, amps, grid, picks, tx, win, B):
+    """Per sampled cell: identical bins, power (1e-9 vs the rounded-once arccos; 1e-5 plus the
+    reference's own arccos spread vs the reference), and every impulse-response bin element-wise:
+    within 1e-9 relative of the rounded-once reference, and within 1e-5 relative of the reference
+    itself except where the reference's float32 np.arccos (65% correctly rounded)
+    moves the bin by more than 1e-6 -- a Fresnel factor near its zero, where one ulp of angle is a
+    large relative change.  Returns the counts of such bins."""
     cen = grid.centers().reshape(-1, 3)
     t0 = time.time()
+    n_bins_checked = n_outside = n_sensitive = 0
     for c, why in sorted(picks.items()):
         ref = orc.coverage_cell(E, tx, cen[c], B, N, win=win)
         sel = cells == c
@@ -73,8 +99,20 @@ def _check_cells(E, power, cells, bins, amps, grid, picks, tx, win, B):
             np.testing.assert_allclose(power[c], ref["power_cr"], rtol=1e-9, err_msg=f"cell {c} ({why})")
             allowed = 1e-5 * abs(ref["power"]) + 1.01 * abs(ref["power_cr"] - ref["power"])
             assert abs(power[c] - ref["power"]) <= allowed, f"cell {c} ({why})"
+            a, ir, ir_cr = amps[sel], ref["ir"][rb], ref["ir_cr"][rb]
+            np.testing.assert_allclose(a, ir_cr, rtol=1e-9, atol=0, err_msg=f"cell {c} ({why}) vs rounded-once")
+            outside = np.abs(a - ir) > 1e-5 * np.abs(ir)
+            sensitive = np.abs(ir_cr - ir) > 1e-6 * np.abs(ir)
+            assert not (outside & ~sensitive).any(), f"cell {c} ({why}): bins {rb[outside & ~sensitive]}"
+            assert (np.abs(a - ir) <= 1e-5 * np.abs(ir) + 1.01 * np.abs(ir_cr - ir)).all(), f"cell {c} ({why})"
+            n_bins_checked += len(rb)
+            n_outside += int(outside.sum())
+            n_sensitive += int(sensitive.sum())
         print(f"  cell {c:8d} {why:32s} paths {ref['paths']:8d} bins {len(rb):5d} ok ({time.time() - t0:.1f} s)",
               flush=True)
+    print(f"  {len(picks)} cells, {n_bins_checked} bins element-wise: {n_outside} outside 1e-5 relative of the "
+          f"reference, all among the {n_sensitive} bins its float32 arccos moves by > 1e-6", flush=True)
+    return n_bins_checked, n_outside, n_sensitive
 
 
 def test_k3_full_map_sampled_cells_vs_oracle():
@@ -108,8 +146,11 @@ def test_k5_full_map_sampled_cells_vs_oracle():
     receiving = int(np.isfinite(power).sum())
     assert receiving == len(np.unique(cells))
     print(f"\nK5: {receiving} cells receiving, {len(cells)} (cell, bin) entries", flush=True)
-    picks = _sample_cells(power, cells, bins, grid, tx, 0.1, np.random.default_rng(5), n_each=3)
-    assert len(picks) >= 14
+    picks = _sample_cells(power, cells, bins, grid, tx, 0.1, np.random.default_rng(5), n_each=8, edges=8,
+                          shadowed=8, at_least=64)
+    assert len(picks) >= 64
+    assert sum(w.startswith("shadowed") for w in picks.values()) >= 1
+    assert sum(w.startswith("grid edge") for w in picks.values()) >= 4
     _check_cells(orc.Mesh(terr.vertices, terr.faces), power, cells, bins, amps, grid, picks, tx, win, B)
 
 

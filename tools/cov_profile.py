@@ -3,7 +3,9 @@ estimates: K3 (room, 256^2) and K5 (terrain stand-in, 1024^2), each as the whole
 per-rank work of an S-GPU run.  MODE=cells: rank 0 of an S-way x-column cell shard.  MODE=rays
 (default): all S ray-shard plans run one after another on this GPU; per rank, the time of its
 trace + local reduce (stage 1) plus its owner stage on the records routed to it, and the slowest
-rank is reported (the all-to-all itself is not included).  Prints one JSON line per case."""
+rank is reported; "ms_per_map_with_collectives" adds the modelled all-to-all and all-gather
+(collective_model: bytes from the measured record counts over a stated xGMI rate, plus a stated
+latency per collective).  Prints one JSON line per case."""
 import json
 import os
 import sys
@@ -102,10 +104,37 @@ def rays_case(case, m, grid, tx, win, B, env, S, reps):
         if best is None or max(per_rank) < max(best[0]):
             best = (per_rank, t_trace, t_own, nrec, [sum(x[-1]) for x in sent])
     per_rank, t_trace, t_own, nrec, nsent = best
+    coll = collective_model(nsent, nrec, grid, S)
     print(json.dumps({"case": case, "mode": "rays", "shards": S, "ms_per_map_max_rank": max(per_rank) * 1e3,
+                      "ms_per_map_with_collectives": max(t_trace) * 1e3 + coll["ms_total"] + max(t_own) * 1e3,
+                      "collectives_model": coll,
                       "ms_trace_stage": [round(x * 1e3, 3) for x in t_trace],
                       "ms_owner_stage": [round(x * 1e3, 3) for x in t_own],
                       "records_sent": nsent, "records_received": nrec}), flush=True)
+
+
+# Cost model of the three collectives of a ray-sharded map (run() / bench.py: dist.exchange_rows =
+# an all-to-all of the send counts, then of the 32-B (key, sum) rows; dist.gather_power_map = an
+# all-gather of each owner's x columns, f64).  Stated constants, overridable: XGMI_GBS = bytes per
+# second one GPU moves out (and in) across its 7 xGMI links in an RCCL all-to-all / all-gather
+# (MI355X: 7 links x ~153 GB/s peak each; 300 GB/s assumed achieved), COLL_US = fixed latency per
+# collective (launch + RCCL protocol + the host read of the counts).  The trace stage of every rank
+# ends before the exchange, and the owner stage starts after it, so the map time is
+# max(trace) + collectives + max(owner) + the all-gather.
+def collective_model(nsent, nrec, grid, S):
+    gbs = float(os.environ.get("XGMI_GBS", "300"))
+    lat = float(os.environ.get("COLL_US", "25"))
+    row = 32
+    a2a_out = max(n * row * (S - 1) / S for n in nsent)  # a rank's own share stays local
+    a2a_in = max(n * row * (S - 1) / S for n in nrec)
+    a2a = max(a2a_out, a2a_in)
+    owned = (grid.nx + S - 1) // S * grid.ny * grid.nz * 8
+    ag_in = owned * (S - 1)  # every rank receives the other owners' columns
+    ms_a2a = 2 * lat / 1e3 + a2a / (gbs * 1e9) * 1e3
+    ms_ag = lat / 1e3 + ag_in / (gbs * 1e9) * 1e3
+    return {"xgmi_gbs_assumed": gbs, "latency_us_per_collective": lat, "a2a_bytes_max": int(a2a),
+            "allgather_bytes_in": int(ag_in), "ms_all_to_all": round(ms_a2a, 4), "ms_all_gather": round(ms_ag, 4),
+            "ms_total": round(ms_a2a + ms_ag, 4)}
     for p in plans:
         p.close()
 
