@@ -498,9 +498,11 @@ def terrain_legs(args, local, rank, world, dist):
         step(kind)
         # iterations that issued a query: every env / RX hit plus each ray's first miss
         active = int((kind != 0).sum().item()) + int((kind == 0).any(dim=1).sum().item())
-        roof = _roofline("k_trace_bvh<5>", float(pr[0]), N * B, B, "nominal N x B ray-bounces (D4), trace kernel "
-                         "alone (the ray-order sort is sort_ms); traffic: BVH node/leaf gathers (16-B lanes, FETCH_SIZE "
-                         "x2 not calibrated for gathers: the true bytes lie between traffic/2 and traffic)",
+        roof = _roofline("k_trace_bvh<5>", float(pr[0]), N * B, B, "nominal N x B ray-bounces (D4); kernel_ms spans "
+                         "the coalesced NaN / 0 fill of received and row_mask (k_fill_received) and the trace kernel, "
+                         "which stores only the received rows (the ray-order sort is sort_ms); traffic: both launches, "
+                         "BVH node/leaf gathers (16-B lanes, FETCH_SIZE x2 not calibrated for gathers: the true bytes "
+                         "lie between traffic/2 and traffic)",
                          N == 2_097_152 and world == 1)
         if roof:
             roof["sort_ms"] = float(pr[1])

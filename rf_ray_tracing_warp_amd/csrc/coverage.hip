@@ -711,12 +711,33 @@ __device__ __forceinline__ void owned_strips(const CovParams& p, const Seg& s, i
 }
 
 // pass A: per ray, the (segment, layer, column) items.  item = r<<40 | k<<36 | kz<<24 | ia
+// Each lane finds its ray's column spans (<= B segments x nz layers) and keeps them in LDS, the block
+// reserves its range with one atomic, and then all 256 threads write the block's items together:
+// item q of the block belongs to the lane whose exclusive prefix is the last one <= q (a binary
+// search over the lanes' prefixes in LDS) and to that lane's span whose start is the last one <= q.
+// (Each lane writing its own items serially made a wave last as long as its longest ray: up to ~770
+// stores for a segment across the whole room; K3 rank of 8 49 us for 125k rays.)  Plans with more
+// than kColSpans spans per ray (B x nz) keep the serial writes.
+#ifndef RT_COLS_SPANS
+#define RT_COLS_SPANS 1
+#endif
+constexpr int kColSpans = 4;
+struct ColSpan {
+  int32_t ia0;   // first column
+  uint32_t n;    // columns
+  uint32_t tag;  // step << 16 | k << 12 | kz
+};
 __global__ __launch_bounds__(256) void k_cols(CovParams p) {
+  __shared__ uint32_t s_pre[256];  // the lanes' exclusive item prefixes in the block
+  __shared__ uint32_t s_tot;
+  __shared__ ColSpan s_span[kColSpans][256];
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const bool spans_ok = RT_COLS_SPANS && (int64_t)p.B * p.g.nz <= kColSpans && p.g.nz <= 4096 && p.nshard < 65536;
   for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < p.n; base += stride) {
     const int64_t r = base + threadIdx.x;
     const bool active = r < p.n;
     unsigned c = 0;
+    int nsp = 0;
     const int ns = active ? p.nseg[r] : 0;
     for (int k = 0; k < ns; ++k) {
       const Seg s = load_seg(p, r, k);
@@ -726,25 +747,56 @@ __global__ __launch_bounds__(256) void k_cols(CovParams p) {
         seg_columns(p, s, kz, ta, tb, ia0, ia1);
         int64_t step;
         owned_strips(p, s, ia0, step);
-        if (ia1 >= ia0) c += (unsigned)((ia1 - ia0) / step + 1);
+        if (ia1 >= ia0) {
+          const unsigned n = (unsigned)((ia1 - ia0) / step + 1);
+          if (spans_ok) s_span[nsp++][threadIdx.x] = ColSpan{(int32_t)ia0, n, (uint32_t)(step << 16 | k << 12 | kz)};
+          c += n;
+        }
       }
     }
+    if (spans_ok)
+      for (int j = nsp; j < kColSpans; ++j) s_span[j][threadIdx.x].n = 0u;
     unsigned pre;
     const unsigned long long at = block_append(p.item_count, c, pre);
-    int64_t w = (int64_t)(at + pre);
-    for (int k = 0; k < ns; ++k) {
-      const Seg s = load_seg(p, r, k);
-      for (int64_t kz = 0; kz < p.g.nz; ++kz) {
-        double ta, tb;
-        int64_t ia0, ia1;
-        seg_columns(p, s, kz, ta, tb, ia0, ia1);
-        int64_t step;
-        owned_strips(p, s, ia0, step);
-        for (int64_t ia = ia0; ia <= ia1; ia += step, ++w)
-          if (w < p.item_cap)
-            p.items[w] = ((uint64_t)r << 40) | ((uint64_t)k << 36) | ((uint64_t)kz << 24) | (uint64_t)ia;
+    if (!spans_ok) {
+      int64_t w = (int64_t)(at + pre);
+      for (int k = 0; k < ns; ++k) {
+        const Seg s = load_seg(p, r, k);
+        for (int64_t kz = 0; kz < p.g.nz; ++kz) {
+          double ta, tb;
+          int64_t ia0, ia1;
+          seg_columns(p, s, kz, ta, tb, ia0, ia1);
+          int64_t step;
+          owned_strips(p, s, ia0, step);
+          for (int64_t ia = ia0; ia <= ia1; ia += step, ++w)
+            if (w < p.item_cap)
+              p.items[w] = ((uint64_t)r << 40) | ((uint64_t)k << 36) | ((uint64_t)kz << 24) | (uint64_t)ia;
+        }
+      }
+      continue;
+    }
+    s_pre[threadIdx.x] = pre;
+    if (threadIdx.x == 255) s_tot = pre + c;
+    __syncthreads();
+    const uint32_t tot = s_tot;
+    for (uint32_t q = threadIdx.x; q < tot; q += blockDim.x) {
+      int lo = 0, hi = 255;  // last lane with s_pre <= q
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s_pre[mid] <= q) lo = mid;
+        else hi = mid - 1;
+      }
+      uint32_t off = q - s_pre[lo];  // the item's index in lane lo's list
+      int j = 0;
+      while (j + 1 < kColSpans && off >= s_span[j][lo].n) off -= s_span[j++][lo].n;
+      const ColSpan sp = s_span[j][lo];
+      const int64_t w = (int64_t)at + q;
+      if (w < p.item_cap) {
+        const uint64_t k = (sp.tag >> 12) & 15u, kz = sp.tag & 0xFFFu, step = sp.tag >> 16;
+        p.items[w] = ((uint64_t)(base + lo) << 40) | (k << 36) | (kz << 24) | (uint64_t)(sp.ia0 + (int64_t)off * step);
       }
     }
+    __syncthreads();  // s_pre, s_tot and the spans are rewritten by the next block-row
   }
 }
 
@@ -1200,6 +1252,16 @@ __global__ __launch_bounds__(256, RT_WIN_WAVES) void k_win(CovParams p, const ui
 // one contiguous tile.  k_sel_count counts a tile's flags; k_sel_scatter adds the counts of the
 // tiles before it (<= G values from L2) and writes its indices in order.  (One atomic per wave on
 // a single counter instead measured 1.4 ms on K3: 123k contended atomics.)
+// A first win as the replay reads it: its candidate key (cell, ray slot, bounce) and receiver t,
+// gathered once in candidate order by k_sel_scatter (coherent reads: the candidates are in ray
+// order) instead of through list -> keys / trx at every replayed record (three scattered 8-B / 4-B
+// reads, each a line: K3 k_replay fetched 1.24 GB per launch at L2 hit 0.19).  The window order
+// writes the items themselves in processing order, so a rank's replay reads them sequentially.
+struct ReplayItem {
+  uint64_t key;
+  float trx;
+  int32_t pad;
+};
 __device__ __forceinline__ int64_t sel_tile(int64_t n, int G) { return ((n + G - 1) / G + 255) / 256 * 256; }
 __device__ __forceinline__ int block_sum(int v, int* s4) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -1219,7 +1281,8 @@ __global__ __launch_bounds__(256) void k_sel_count(const uint8_t* flag, const un
   if (threadIdx.x == 0) counts[blockIdx.x] = c;
 }
 __global__ __launch_bounds__(256) void k_sel_scatter(const uint8_t* flag, const unsigned long long* n_dev, int64_t cap,
-                                                     const int32_t* counts, int64_t* list, unsigned long long* nlist) {
+                                                     const int32_t* counts, const uint64_t* keys, const float* trx,
+                                                     ReplayItem* items, unsigned long long* nlist) {
   __shared__ int s4[4];
   __shared__ int w4[4];
   const int64_t n = min((int64_t)*n_dev, cap), tile = sel_tile(n, gridDim.x);
@@ -1238,7 +1301,10 @@ __global__ __launch_bounds__(256) void k_sel_scatter(const uint8_t* flag, const 
     int off = 0;
     for (int w = 0; w < wave; ++w) off += w4[w];
     const int step = w4[0] + w4[1] + w4[2] + w4[3];
-    if (f) list[base + off + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = i;
+    if (f) {
+      const int64_t k = base + off + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      items[k] = ReplayItem{keys[i], trx[i], 0};
+    }
     base += step;
     __syncthreads();  // w4 is rewritten by the next step
   }
@@ -1291,10 +1357,10 @@ __device__ __forceinline__ uint16_t replay_key(const CovParams& p, uint64_t key)
   }
 }
 template <bool USE_BVH>
-__global__ __launch_bounds__(256) void k_replay_keys(CovParams p, const uint64_t* keys, const int64_t* list, int64_t nl,
+__global__ __launch_bounds__(256) void k_replay_keys(CovParams p, const ReplayItem* items, int64_t nl,
                                                      uint16_t* okey, int32_t* oval) {
   for (int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; li < nl; li += (int64_t)gridDim.x * blockDim.x) {
-    okey[li] = replay_key<USE_BVH>(p, keys[list[li]]);
+    okey[li] = replay_key<USE_BVH>(p, items[li].key);
     oval[li] = (int32_t)li;
   }
 }
@@ -1323,8 +1389,8 @@ constexpr int64_t kReplayWindowMax = RT_REPLAY_WINDOW_MAX;
 #define RT_REPLAY_EARLY 1
 #endif
 template <bool USE_BVH>
-__global__ __launch_bounds__(1024) void k_replay_order(CovParams p, const uint64_t* keys, const int64_t* list,
-                                                       int64_t nl, const unsigned long long* nl_dev, int32_t* order) {
+__global__ __launch_bounds__(1024) void k_replay_order(CovParams p, const ReplayItem* items, int64_t nl,
+                                                       const unsigned long long* nl_dev, ReplayItem* sorted) {
   using Sort = rocprim::block_radix_sort<uint16_t, 1024, RT_REPLAY_WIN_ITEMS, int32_t>;
   __shared__ typename Sort::storage_type st;
   if (nl_dev) nl = min(nl, (int64_t)*nl_dev);  // launched before the host knows the list length
@@ -1335,18 +1401,18 @@ __global__ __launch_bounds__(1024) void k_replay_order(CovParams p, const uint64
 #pragma unroll
   for (int i = 0; i < RT_REPLAY_WIN_ITEMS; ++i) {
     const int64_t li = base + i;
-    k[i] = li < nl ? replay_key<USE_BVH>(p, keys[list[li]]) : (uint16_t)0xFFFF;
+    k[i] = li < nl ? replay_key<USE_BVH>(p, items[li].key) : (uint16_t)0xFFFF;
     v[i] = (int32_t)li;
   }
   Sort().sort(k, v, st);
 #pragma unroll
-  for (int i = 0; i < RT_REPLAY_WIN_ITEMS; ++i)
-    if (base + i < nl) order[base + i] = v[i];
+  for (int i = 0; i < RT_REPLAY_WIN_ITEMS; ++i)  // the window's items, just read: L2-resident
+    if (base + i < nl) sorted[base + i] = items[v[i]];
 }
 
 template <bool USE_BVH, bool RX_FIRST>
-__global__ __launch_bounds__(256, USE_BVH ? RT_COV_REPLAY_WAVES_BVH : RT_COV_REPLAY_WAVES) void k_replay(CovParams p, const uint64_t* keys, const float* trx,
-                                                const int64_t* list, int64_t nl, const unsigned long long* nl_dev,
+__global__ __launch_bounds__(256, USE_BVH ? RT_COV_REPLAY_WAVES_BVH : RT_COV_REPLAY_WAVES) void k_replay(CovParams p, const ReplayItem* items,
+                                                int64_t nl, const unsigned long long* nl_dev,
                                                 const int32_t* order, uint64_t* out_key, double* out_amp) {
   extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
   __shared__ RxLds L;
@@ -1355,14 +1421,13 @@ __global__ __launch_bounds__(256, USE_BVH ? RT_COV_REPLAY_WAVES_BVH : RT_COV_REP
   stage_rx(L, p.r_rx);
   stage_env<USE_BVH>(p, lds_tab);
   for (int64_t jl = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; jl < nl; jl += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t li = order ? (int64_t)order[jl] : jl;
-    const int64_t i = list[li];
-    const uint64_t key = keys[i];
+    const ReplayItem it = items[order ? (int64_t)order[jl] : jl];
+    const uint64_t key = it.key;
     const int64_t cell = (int64_t)(key >> 28), r = (int64_t)((key >> 4) & 0xFFFFFF);
     // records at the processing position jl: their order is irrelevant (they are sorted by key
     // and summed exactly), and consecutive lanes then write consecutive 8-B words instead of
     // scattering them (K3 k_replay wrote 445 MB for 126 MB of records, r2zm)
-    replay<USE_BVH, RX_FIRST>(p, lds_tab, L, cell, r, (int)(key & 15), trx[i], out_key[jl], out_amp[jl]);
+    replay<USE_BVH, RX_FIRST>(p, lds_tab, L, cell, r, (int)(key & 15), it.trx, out_key[jl], out_amp[jl]);
   }
 }
 
@@ -1985,10 +2050,18 @@ struct rt_coverage {
   int32_t range_epoch = 0;
   int32_t* bigcells = nullptr;  // per cell slot: the cells k_power sweeps (more than kPowSmall terms)
   int32_t* runs = nullptr;  // exact run sums: [cap] head flags, [cap] their scan, [cap] run starts, [64] counters
+  // k_owner_runs' look-back: [cap / kOwnTile + 1] state words, [ticket counter, error count]; host:
+  // tickets issued so far, the call's tag
+  uint64_t* own_states = nullptr;
+  unsigned long long* own_aux = nullptr;
+  uint64_t own_tickets = 0, own_tag = 0;
+  int32_t* segcells = nullptr;  // k_seg_cells: [3][kOcSegs][nown] (start, count, epoch) of ray-mode owners
+  bool ukeys_unsorted = false;  // the last owner stage left ukeys in reservation order
   uint8_t* win = nullptr;
   uint8_t* first_flag = nullptr;
   float* trx = nullptr;
   int64_t* list = nullptr;
+  ReplayItem *ritems = nullptr, *ritems_sorted = nullptr;  // first wins (candidate order / processing order)
   uint64_t* items = nullptr;
   int64_t item_cap = 0;
   unsigned long long* counters = nullptr;  // [0] candidates, [1] column items, [2] replay list (int64)
@@ -2386,6 +2459,393 @@ __global__ __launch_bounds__(256) void k_cross_tiles(int64_t ntiles, TileMeta tm
   }
 }
 
+// ---- Owner stage, runs + terms + cell ranges in one launch (RT_OWNER_FUSED).  After the segment
+// merge, a run of equal keys holds at most one record per source rank (each rank's segment has
+// unique keys), so it is at most nseg long: the record that heads a run sums it on its own, reading
+// on past its tile's end when the run crosses it (a run that began in an earlier tile is its head's).
+// The unique index of a head is the number of heads before it: per tile of kOwnTile records a
+// count, combined across tiles by decoupled look-back (tiles taken in order from a ticket counter;
+// every state word carries the call's tag, so nothing is reset between calls).  Each head then
+// writes its key and f64 sum, its power-sweep terms (k_terms) and, at cell boundaries, the cell's
+// range (k_cell_ranges).  Replaces k_tile_heads, k_tile_sums, k_cross_tiles, k_terms and
+// k_cell_ranges (five launches) on merged segments.
+#ifndef RT_OWNER_FUSED
+#define RT_OWNER_FUSED 1
+#endif
+#ifndef RT_OWN_ITEMS
+#define RT_OWN_ITEMS 4
+#endif
+constexpr int kOwnItems = RT_OWN_ITEMS, kOwnTile = 256 * kOwnItems;
+// RT_OWNER_LOOKBACK 0: the tiles' head counts come from k_tile_heads and every block sums the
+// counts before it (no ticket, no waiting on other blocks)
+#ifndef RT_OWNER_LOOKBACK
+#define RT_OWNER_LOOKBACK 1
+#endif
+constexpr uint64_t kOwnAgg = 1ull << 38, kOwnInc = 2ull << 38, kOwnCount = (1ull << 38) - 1;
+constexpr uint64_t kOwnTagMask = ~(kOwnInc | kOwnAgg | kOwnCount);
+struct OwnerRuns {
+  const uint64_t* keys;  // merged wide keys [n]
+  SumVal val;            // the record sums in merged order
+  int64_t n;
+  uint64_t* states;      // [tiles] look-back words
+  unsigned long long* ticket;
+  uint64_t ticket_base, tag;
+  unsigned* errors;
+  uint64_t* ukeys;
+  double *uamps, *tcos, *tsin, *ev;
+  int64_t* nuniq;
+  int64_t ncell;
+  int32_t *cstart, *cend, *cepoch;
+  int32_t epoch;
+  unsigned* nbig;
+  PowerParams P;
+  const int32_t* heads;  // RT_OWNER_LOOKBACK 0: head count of every tile
+};
+__global__ __launch_bounds__(256) void k_owner_runs(OwnerRuns a) {
+  __shared__ uint32_t s_tile;
+  __shared__ int s_w[4];
+  __shared__ int64_t s_prefix;
+  if (threadIdx.x == 0) s_tile = RT_OWNER_LOOKBACK ? (uint32_t)(atomicAdd(a.ticket, 1ull) - a.ticket_base) : blockIdx.x;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *a.nbig = 0u;  // k_power_small lists the big cells afresh
+  __syncthreads();
+  const int64_t tile = s_tile;
+  const int64_t i0 = tile * kOwnTile + (int64_t)threadIdx.x * kOwnItems;
+  uint64_t k[kOwnItems];
+  bool head[kOwnItems];
+  int c = 0;
+  uint64_t prev = i0 > 0 && i0 - 1 < a.n ? a.keys[i0 - 1] : ~0ull;
+#pragma unroll
+  for (int j = 0; j < kOwnItems; ++j) {
+    const int64_t i = i0 + j;
+    k[j] = i < a.n ? a.keys[i] : ~0ull;
+    head[j] = i < a.n && (i == 0 || k[j] != prev);
+    prev = k[j];
+    c += head[j] ? 1 : 0;
+  }
+  // block exclusive scan of the heads
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int x = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s_w[w] = x;
+  __syncthreads();
+  int before = 0;
+  for (int q = 0; q < w; ++q) before += s_w[q];
+  const int total = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+#if !RT_OWNER_LOOKBACK
+  {  // the heads of the tiles before this one, summed by the block
+    int64_t hb = 0;
+    for (int64_t j = threadIdx.x; j < tile; j += blockDim.x) hb += a.heads[j];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) hb += __shfl_xor(hb, o, 64);
+    __shared__ int64_t s_hb[4];
+    __syncthreads();
+    if (lane == 0) s_hb[w] = hb;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      s_prefix = s_hb[0] + s_hb[1] + s_hb[2] + s_hb[3];
+      if (i0 + kOwnTile >= a.n) *a.nuniq = s_prefix + total;
+    }
+  }
+  if (false) {
+#else
+  if (threadIdx.x == 0) {
+#endif
+    uint64_t* st = a.states + tile;
+    __hip_atomic_store(st, a.tag | (tile == 0 ? kOwnInc : kOwnAgg) | (uint64_t)total, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t excl = 0;
+    if (tile > 0) {
+      int spins = 0;
+      for (int64_t j = tile - 1; j >= 0;) {
+        const uint64_t sv = __hip_atomic_load(a.states + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((sv & kOwnTagMask) != a.tag) {  // not published yet
+          if (++spins > (1 << 22)) {
+            atomicAdd(a.errors, 1u);
+            break;
+          }
+          continue;
+        }
+        excl += sv & kOwnCount;
+        if (sv & kOwnInc) break;
+        --j;
+      }
+      __hip_atomic_store(st, a.tag | kOwnInc | (excl + (uint64_t)total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    s_prefix = (int64_t)excl;
+    if (i0 + kOwnTile >= a.n) *a.nuniq = (int64_t)excl + total;  // the last tile
+  }
+  __syncthreads();
+  int64_t u = s_prefix + before + x - c;  // unique index of this thread's first head
+  const PowerParams& P = a.P;
+#pragma unroll
+  for (int j = 0; j < kOwnItems; ++j) {
+    if (!head[j]) continue;
+    const int64_t i = i0 + j;
+    const uint64_t key = k[j];
+    Fx192 acc = a.val(i);
+    int64_t e = i + 1;
+    for (; e < a.n; ++e) {  // <= nseg records
+      const uint64_t ke = a.keys[e];
+      if (ke != key) break;
+      acc = FxPlus()(acc, a.val(e));
+    }
+    const double amp = fx_to_double(acc);
+    a.ukeys[u] = key;
+    a.uamps[u] = amp;
+    const int64_t m = (int64_t)(key & 0xFFFFFFFFull);
+    double sp, cp;
+    sincos_turns(P.turns * (double)(P.half - m), sp, cp);
+    a.tcos[u] = amp * cp;
+    a.tsin[u] = amp * sp;
+    const int64_t st = m - P.half > 0 ? m - P.half : 0;
+    const int64_t en = m + (P.n_bins - 1 - P.half), e1 = (en < P.n_bins - 1 ? en : P.n_bins - 1) + 1;
+    sincos_turns(P.turns * (double)st, a.ev[4 * u], a.ev[4 * u + 1]);
+    sincos_turns(P.turns * (double)e1, a.ev[4 * u + 2], a.ev[4 * u + 3]);
+    const uint64_t cell = key >> 32;
+    if (cell < (uint64_t)a.ncell) {  // (a ~0 key never arrives from another rank)
+      const uint64_t pk = i > 0 ? a.keys[i - 1] : ~0ull;
+      if (i == 0 || (pk >> 32) != cell) {
+        a.cstart[cell] = (int32_t)u;
+        a.cepoch[cell] = a.epoch;
+      }
+      if (e >= a.n || (a.keys[e] >> 32) != cell) a.cend[cell] = (int32_t)(u + 1);
+    }
+    ++u;
+  }
+}
+
+// ---- Owner stage per cell (RT_OWNER_CELLS, default): no merge of the received segments.
+// k_seg_cells: every received record that starts its cell's run within its segment stamps the
+//   cell's (first record, count) for that segment (epoch-tagged, so nothing is cleared);
+// k_owner_cells: one thread per owned cell merges its <= nseg runs (a few records each), adds the
+//   equal keys' fixed-point sums, keeps the cell's unique (bin, f64 amplitude) terms in LDS and, for
+//   up to kPowSmall terms, sweeps the power at once (power_sparse with the terms' phases computed as
+//   k_terms does, so the same bits as the one-GPU map); larger cells get their terms written to the
+//   global term arrays and are listed for k_power, unchanged.  Every cell's unique keys and
+//   amplitudes also go to ukeys / uamps (rt_coverage_received), at a range reserved with one
+//   atomic per wave -- so not in key order there (rt_coverage_received sorts on demand).
+// Replaces the merge, run sums, terms, cell ranges and small-cell sweep (five launches, each a
+// latency-bound pass over all records: ~130-180 us per owner of 8 on K3 / K5).
+#ifndef RT_OWNER_CELLS
+#define RT_OWNER_CELLS 1
+#endif
+constexpr int kOcSegs = 8;
+struct SegCells {  // [kOcSegs][nown]: a cell's run in each segment (valid when ep == epoch)
+  int32_t *start, *cnt, *ep;
+  int64_t nown;
+};
+__device__ __forceinline__ uint32_t owned_index(uint32_t c, const rt_grid& g, int shard, int nshard) {
+  const uint32_t nx = (uint32_t)g.nx, ns = (uint32_t)nshard;
+  const uint32_t nxo = (nx - (uint32_t)shard + ns - 1) / ns;
+  const uint32_t row = c / nx, ix = c - row * nx;
+  return row * nxo + (ix - (uint32_t)shard) / ns;
+}
+__global__ __launch_bounds__(256) void k_seg_cells(const uint64_t* keys, int64_t kstride, SegOffsets so, rt_grid g,
+                                                   int shard, int nshard, SegCells sc, int32_t epoch,
+                                                   int64_t* nuniq_ctr, unsigned* nbig) {
+  const int64_t n = so.off[so.nseg];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *nuniq_ctr = 0;  // k_owner_cells reserves its cells' ranges from it
+    *nbig = 0u;
+  }
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int sg = 0;
+    while (sg + 1 < so.nseg && so.off[sg + 1] <= i) ++sg;
+    const uint64_t cell = keys[i * kstride] >> 32;
+    if (i > so.off[sg] && (keys[(i - 1) * kstride] >> 32) == cell) continue;  // not the first of its run
+    int64_t a = i + 1, b = so.off[sg + 1];  // first record of a later cell (keys ascend)
+    while (a < b) {
+      const int64_t m = (a + b) >> 1;
+      if ((keys[m * kstride] >> 32) == cell) a = m + 1;
+      else b = m;
+    }
+    const int64_t slot = (int64_t)sg * sc.nown + owned_index((uint32_t)cell, g, shard, nshard);
+    sc.start[slot] = (int32_t)i;
+    sc.cnt[slot] = (int32_t)(a - i);
+    sc.ep[slot] = epoch;
+  }
+}
+// a cell's terms from its (bin, amplitude) pairs in LDS, the phases computed as k_terms does
+struct FlyTerms {
+  const int32_t (*sm)[64];
+  const double (*sa)[64];
+  int lane;
+  PowerParams P;
+  __device__ __forceinline__ int64_t m(int64_t k) const { return sm[k][lane]; }
+  __device__ __forceinline__ void cs(int64_t k, double& c, double& s) const {
+    double sp, cp;
+    sincos_turns(P.turns * (double)(P.half - m(k)), sp, cp);
+    const double a = sa[k][lane];
+    c = a * cp;
+    s = a * sp;
+  }
+  __device__ __forceinline__ void start(int64_t k, double& s, double& c) const {
+    const int64_t mk = m(k), st = mk - P.half > 0 ? mk - P.half : 0;
+    sincos_turns(P.turns * (double)st, s, c);
+  }
+  __device__ __forceinline__ void stop(int64_t k, double& s, double& c) const {
+    const int64_t mk = m(k), e = mk + (P.n_bins - 1 - P.half), e1 = (e < P.n_bins - 1 ? e : P.n_bins - 1) + 1;
+    sincos_turns(P.turns * (double)e1, s, c);
+  }
+};
+struct OwnerCells {
+  const uint64_t* keys;  // received keys at keys[i * kstride]
+  int64_t kstride;
+  const uint64_t* words;  // received sums at words[i * vstride .. + 2]
+  int64_t vstride;
+  int nseg;
+  SegCells sc;
+  int32_t epoch;
+  rt_grid g;
+  int shard, nshard;
+  PowerParams P;
+  double* power;
+  int64_t* nuniq;  // reservation counter, then the unique count
+  uint64_t* ukeys;
+  double *uamps, *tcos, *tsin, *ev;
+  int32_t *cstart, *cend, *cepoch;
+  int32_t* big;
+  unsigned* nbig;
+};
+__global__ __launch_bounds__(64) void k_owner_cells(OwnerCells a) {
+  __shared__ int32_t s_m[kPowSmall][64];
+  __shared__ double s_a[kPowSmall][64];
+  const rt_grid& g = a.g;
+  const int lane = threadIdx.x & 63;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  {  // other ranks' cells: 0 (the map is sum-reduced), 32-bit index arithmetic
+    const uint32_t ncell = (uint32_t)(g.nx * g.ny * g.nz), nx = (uint32_t)g.nx, ns = (uint32_t)a.nshard;
+    if (a.nshard > 1)
+      for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < ncell; c += (uint32_t)stride)
+        if ((c % nx) % ns != (uint32_t)a.shard) a.power[c] = 0.0;
+  }
+  const int64_t nxo = g.nx > a.shard ? (g.nx - a.shard + a.nshard - 1) / a.nshard : 0;
+  const int64_t nown = nxo * g.ny * g.nz;
+  auto val = [&](int64_t i) {
+    const uint64_t* q = a.words + i * a.vstride;
+    return Fx192{q[0], q[1], q[2]};
+  };
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); base < nown; base += stride) {
+    const int64_t t = base + lane;
+    const bool valid = t < nown;
+    int64_t cell = 0;
+    int32_t pos[kOcSegs], end[kOcSegs];
+    uint64_t hk[kOcSegs];
+    if (valid) {
+      const int64_t jx = t % nxo, rest = t / nxo;
+      cell = rest * g.nx + a.shard + jx * a.nshard;
+    }
+#pragma unroll
+    for (int s = 0; s < kOcSegs; ++s) {
+      pos[s] = end[s] = 0;
+      if (valid && s < a.nseg) {
+        const int64_t slot = (int64_t)s * a.sc.nown + t;
+        if (a.sc.ep[slot] == a.epoch) {
+          pos[s] = a.sc.start[slot];
+          end[s] = pos[s] + a.sc.cnt[slot];
+        }
+      }
+    }
+    // merge the runs: unique keys ascending, equal keys' sums added exactly
+    int K = 0;
+#pragma unroll
+    for (int s = 0; s < kOcSegs; ++s) hk[s] = pos[s] < end[s] ? a.keys[(int64_t)pos[s] * a.kstride] : ~0ull;
+    while (true) {
+      uint64_t km = ~0ull;
+#pragma unroll
+      for (int s = 0; s < kOcSegs; ++s) km = hk[s] < km ? hk[s] : km;
+      if (km == ~0ull) break;
+      Fx192 acc{0, 0, 0};
+#pragma unroll
+      for (int s = 0; s < kOcSegs; ++s)
+        if (hk[s] == km) {
+          acc = FxPlus()(acc, val(pos[s]));
+          ++pos[s];
+          hk[s] = pos[s] < end[s] ? a.keys[(int64_t)pos[s] * a.kstride] : ~0ull;
+        }
+      if (K < kPowSmall) {
+        s_m[K][lane] = (int32_t)(km & 0xFFFFFFFFull);
+        s_a[K][lane] = fx_to_double(acc);
+      }
+      ++K;
+    }
+    // this cell's range of the unique arrays: one atomic per wave
+    int64_t x = K;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    int64_t u0 = 0;
+    if (lane == 63 && x > 0) u0 = (int64_t)atomicAdd((unsigned long long*)a.nuniq, (unsigned long long)x);
+    u0 = __shfl(u0, 63, 64) + x - K;
+    const bool is_big = valid && K > kPowSmall;
+    if (valid && !is_big) {
+      for (int k = 0; k < K; ++k) {
+        a.ukeys[u0 + k] = (uint64_t)cell << 32 | (uint32_t)s_m[k][lane];
+        a.uamps[u0 + k] = s_a[k][lane];
+      }
+      a.power[cell] = power_sparse(0, K, a.P, FlyTerms{s_m, s_a, lane, a.P});  // NaN when empty
+    }
+    if (is_big) {  // the terms to the global arrays for k_power (the runs merged again)
+#pragma unroll
+      for (int s = 0; s < kOcSegs; ++s) {
+        pos[s] = end[s] = 0;
+        if (s < a.nseg) {
+          const int64_t slot = (int64_t)s * a.sc.nown + t;
+          if (a.sc.ep[slot] == a.epoch) {
+            pos[s] = a.sc.start[slot];
+            end[s] = pos[s] + a.sc.cnt[slot];
+          }
+        }
+        hk[s] = pos[s] < end[s] ? a.keys[(int64_t)pos[s] * a.kstride] : ~0ull;
+      }
+      const PowerParams& P = a.P;
+      for (int64_t u = u0;; ++u) {
+        uint64_t km = ~0ull;
+#pragma unroll
+        for (int s = 0; s < kOcSegs; ++s) km = hk[s] < km ? hk[s] : km;
+        if (km == ~0ull) break;
+        Fx192 acc{0, 0, 0};
+#pragma unroll
+        for (int s = 0; s < kOcSegs; ++s)
+          if (hk[s] == km) {
+            acc = FxPlus()(acc, val(pos[s]));
+            ++pos[s];
+            hk[s] = pos[s] < end[s] ? a.keys[(int64_t)pos[s] * a.kstride] : ~0ull;
+          }
+        const double amp = fx_to_double(acc);
+        const int64_t m = (int64_t)(km & 0xFFFFFFFFull);
+        a.ukeys[u] = km;
+        a.uamps[u] = amp;
+        double sp, cp;
+        sincos_turns(P.turns * (double)(P.half - m), sp, cp);
+        a.tcos[u] = amp * cp;
+        a.tsin[u] = amp * sp;
+        const int64_t st = m - P.half > 0 ? m - P.half : 0;
+        const int64_t e = m + (P.n_bins - 1 - P.half), e1 = (e < P.n_bins - 1 ? e : P.n_bins - 1) + 1;
+        sincos_turns(P.turns * (double)st, a.ev[4 * u], a.ev[4 * u + 1]);
+        sincos_turns(P.turns * (double)e1, a.ev[4 * u + 2], a.ev[4 * u + 3]);
+      }
+      a.cstart[cell] = (int32_t)u0;
+      a.cend[cell] = (int32_t)(u0 + K);
+      a.cepoch[cell] = a.epoch;
+    }
+    const uint64_t mb = __ballot(is_big);
+    if (mb) {
+      unsigned b0 = 0;
+      if (lane == 0) b0 = atomicAdd(a.nbig, (unsigned)__popcll(mb));
+      b0 = __shfl(b0, 0, 64);
+      if (is_big) a.big[b0 + (unsigned)__builtin_amdgcn_mbcnt_hi((uint32_t)(mb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mb, 0u))] =
+          (int32_t)cell;
+    }
+  }
+}
+
 hipError_t scan_flags(void* tmp, size_t& bytes, const int32_t* flags, int32_t* scan, int64_t n, hipStream_t s) {
   return rocprim::inclusive_scan(tmp, bytes, flags, scan, (size_t)n, rocprim::plus<int32_t>(), s);
 }
@@ -2408,7 +2868,8 @@ void free_cands(rt_coverage* c) {
   for (void* q : {(void*)c->keys, (void*)c->keys_sorted, (void*)c->okeys, (void*)c->okeys_sorted, (void*)c->ukeys,
                   (void*)c->oamps, (void*)c->oamps_sorted, (void*)c->uamps, (void*)c->tcos, (void*)c->tsin, (void*)c->ev,
                   (void*)c->win, (void*)c->trx,
-                  (void*)c->list, (void*)c->first_flag, c->tmp, c->rord, (void*)c->runs})
+                  (void*)c->list, (void*)c->first_flag, c->tmp, c->rord, (void*)c->runs, (void*)c->ritems,
+                  (void*)c->ritems_sorted})
     if (q) (void)hipFree(q);
   c->keys = c->keys_sorted = c->okeys = c->okeys_sorted = c->ukeys = nullptr;
   c->oamps = c->oamps_sorted = c->uamps = c->tcos = c->tsin = c->ev = nullptr;
@@ -2416,7 +2877,10 @@ void free_cands(rt_coverage* c) {
   c->first_flag = nullptr;
   c->trx = nullptr;
   c->list = nullptr;
+  c->ritems = c->ritems_sorted = nullptr;
   c->runs = nullptr;
+  if (c->own_states) (void)hipFree(c->own_states);
+  c->own_states = nullptr;
   c->tmp = nullptr;
   c->tmp_bytes = 0;
   c->rord = nullptr;
@@ -2477,7 +2941,12 @@ int alloc_cands(rt_coverage* c, int64_t cap) {
   RT_HIP(hipMalloc(&c->first_flag, cap));
   RT_HIP(hipMalloc(&c->trx, cap * 4));
   RT_HIP(hipMalloc(&c->list, cap * 8));
+  RT_HIP(hipMalloc(&c->ritems, cap * sizeof(ReplayItem)));
+  RT_HIP(hipMalloc(&c->ritems_sorted, cap * sizeof(ReplayItem)));
   RT_HIP(hipMalloc(&c->runs, (cap * 3 + 64) * 4));  // run flags, their scan, run starts, long-run list
+  // k_owner_runs' states: zero = no tag (tags start at 1 << 40)
+  RT_HIP(hipMalloc(&c->own_states, ((size_t)cap / kOwnTile + 2) * 8));
+  RT_HIP(hipMemset(c->own_states, 0, ((size_t)cap / kOwnTile + 2) * 8));
   size_t b1 = 0, b2 = 0, b3 = 0;
   RT_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, b1, c->keys, c->keys_sorted, (int)cap, 0, 64));
   size_t b2m = 0;  // both sort_records paths: Onesweep at cap, the merge sort below its threshold
@@ -2523,7 +2992,8 @@ int poison_plan(rt_coverage* c, hipStream_t s) {
               {c->okeys_sorted, (size_t)c->cap * 8}, {c->ukeys, (size_t)c->cap * 8}, {c->oamps, (size_t)c->cap * 8},
               {c->oamps_sorted, (size_t)c->cap * 8}, {c->uamps, (size_t)c->cap * 8}, {c->tcos, (size_t)c->cap * 8},
               {c->tsin, (size_t)c->cap * 8}, {c->ev, (size_t)c->cap * 32}, {c->first_flag, (size_t)c->cap},
-              {c->trx, (size_t)c->cap * 4}, {c->list, (size_t)c->cap * 8}, {c->items, (size_t)c->item_cap * 8},
+              {c->trx, (size_t)c->cap * 4}, {c->list, (size_t)c->cap * 8},
+              {c->ritems, (size_t)c->cap * sizeof(ReplayItem)}, {c->ritems_sorted, (size_t)c->cap * sizeof(ReplayItem)}, {c->items, (size_t)c->item_cap * 8},
               {c->tmp, c->tmp_bytes}, {c->rord, c->rord_bytes}, {c->counters, 32}, {c->nuniq, 8},
               {c->cstart, sizeof(int32_t) * (size_t)nc}, {c->cend, sizeof(int32_t) * (size_t)nc},
               {c->bigcells, sizeof(int32_t) * (size_t)nc}, {c->cepoch, sizeof(int32_t) * (size_t)nc},
@@ -2549,11 +3019,11 @@ __global__ __launch_bounds__(256) void k_count_segments(const uint8_t* nseg, int
   for (int o = 32; o >= 1; o >>= 1) acc += __shfl_down(acc, o, 64);
   if ((threadIdx.x & 63) == 0 && acc) atomicAdd(out, acc);
 }
-__global__ __launch_bounds__(256) void k_count_replay(const uint64_t* keys, const int64_t* list, int64_t nl, int B,
+__global__ __launch_bounds__(256) void k_count_replay(const ReplayItem* items, int64_t nl, int B,
                                                       unsigned long long* out) {
   unsigned long long acc = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nl; i += (int64_t)gridDim.x * blockDim.x)
-    acc += (unsigned long long)(B - (int)(keys[list[i]] & 15));
+    acc += (unsigned long long)(B - (int)(items[i].key & 15));
   for (int o = 32; o >= 1; o >>= 1) acc += __shfl_down(acc, o, 64);
   if ((threadIdx.x & 63) == 0 && acc) atomicAdd(out, acc);
 }
@@ -2767,33 +3237,36 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
     if (windows) {
       const unsigned grid_w = (unsigned)((nl + kReplayWin - 1) / kReplayWin);
       if (bvh)
-        hipLaunchKernelGGL(k_replay_order<true>, dim3(grid_w), dim3(1024), 0, s, p, c->keys, c->list, nl, nl_dev,
-                           v_out);
+        hipLaunchKernelGGL(k_replay_order<true>, dim3(grid_w), dim3(1024), 0, s, p, c->ritems, nl, nl_dev,
+                           c->ritems_sorted);
       else
-        hipLaunchKernelGGL(k_replay_order<false>, dim3(grid_w), dim3(1024), 0, s, p, c->keys, c->list, nl, nl_dev,
-                           v_out);
+        hipLaunchKernelGGL(k_replay_order<false>, dim3(grid_w), dim3(1024), 0, s, p, c->ritems, nl, nl_dev,
+                           c->ritems_sorted);
     } else {
       if (bvh)
-        hipLaunchKernelGGL(k_replay_keys<true>, dim3(grid_l), dim3(256), 0, s, p, c->keys, c->list, nl, k_in, v_in);
+        hipLaunchKernelGGL(k_replay_keys<true>, dim3(grid_l), dim3(256), 0, s, p, c->ritems, nl, k_in, v_in);
       else
-        hipLaunchKernelGGL(k_replay_keys<false>, dim3(grid_l), dim3(256), 0, s, p, c->keys, c->list, nl, k_in, v_in);
+        hipLaunchKernelGGL(k_replay_keys<false>, dim3(grid_l), dim3(256), 0, s, p, c->ritems, nl, k_in, v_in);
       RT_HIP(hipcub::DeviceRadixSort::SortPairs((char*)ws + 2 * kbs + 2 * rbs, cub_bytes, k_in, k_out, v_in, v_out,
                                                 (int)nl, 0, 16, s));
     }
     prof_mark(c, 4, s);
+    // the window order wrote the items in processing order; the device-wide sort gives an order
+    const ReplayItem* rit = windows ? c->ritems_sorted : c->ritems;
+    const int32_t* rord = windows ? nullptr : v_out;
     // BVH scenes: receiver first, the traversal culled at its t (K5 replay 3.47 -> 2.7 ms); the
     // LDS brute force tests every face anyway (a plane-culled variant measured 5% slower on K3,
     // a receiver-first one skipping faces beyond the receiver's t 5% slower too: 2.50 vs 2.63 ms,
     // profiles/r2x_cov_rxfirst_lds_ab.jsonl)
     if (bvh && replay_rx_first())
-      hipLaunchKernelGGL((k_replay<true, true>), dim3(grid_l), dim3(256), lds_replay, s, p, c->keys, c->trx, c->list, nl,
-                         nl_dev, v_out, c->okeys, c->oamps);
+      hipLaunchKernelGGL((k_replay<true, true>), dim3(grid_l), dim3(256), lds_replay, s, p, rit, nl, nl_dev, rord,
+                         c->okeys, c->oamps);
     else if (bvh)
-      hipLaunchKernelGGL((k_replay<true, false>), dim3(grid_l), dim3(256), lds_replay, s, p, c->keys, c->trx, c->list, nl,
-                         nl_dev, v_out, c->okeys, c->oamps);
+      hipLaunchKernelGGL((k_replay<true, false>), dim3(grid_l), dim3(256), lds_replay, s, p, rit, nl, nl_dev, rord,
+                         c->okeys, c->oamps);
     else
-      hipLaunchKernelGGL((k_replay<false, false>), dim3(grid_l), dim3(256), lds_replay, s, p, c->keys, c->trx, c->list, nl,
-                         nl_dev, v_out, c->okeys, c->oamps);
+      hipLaunchKernelGGL((k_replay<false, false>), dim3(grid_l), dim3(256), lds_replay, s, p, rit, nl, nl_dev, rord,
+                         c->okeys, c->oamps);
     prof_mark(c, 5, s);
     RT_HIP(hipGetLastError());
     return 0;
@@ -2818,7 +3291,8 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
       hipLaunchKernelGGL(k_sel_count, dim3(G), dim3(256), 0, s, c->first_flag, (const unsigned long long*)c->counters,
                          c->cap, tiles);
       hipLaunchKernelGGL(k_sel_scatter, dim3(G), dim3(256), 0, s, c->first_flag,
-                         (const unsigned long long*)c->counters, c->cap, tiles, c->list, c->counters + 2);
+                         (const unsigned long long*)c->counters, c->cap, tiles, c->keys, c->trx, c->ritems,
+                         c->counters + 2);
     }
     RT_HIP(hipGetLastError());
     // the counters go to pinned memory ahead of the replay, and the host waits for that copy only;
@@ -2869,7 +3343,7 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
         if (rc) return rc;
       }
       if (c->profile)
-        hipLaunchKernelGGL(k_count_replay, dim3(1024), dim3(256), 0, s, c->keys, c->list, nlist, p.B, c->work + 1);
+        hipLaunchKernelGGL(k_count_replay, dim3(1024), dim3(256), 0, s, c->ritems, nlist, p.B, c->work + 1);
     }
     nrec = nlist;
   }
@@ -2956,8 +3430,7 @@ int cov_reduce_sums(rt_coverage* c, const uint64_t* keys, const Fx192* sums, int
 
 // Closed-form signal power of this plan's cells from the reduced records in c->ukeys / c->uamps
 // (nrec: host upper bound of their count); other ranks' cells are zero-filled.
-int cov_power(rt_coverage* c, int64_t nrec, int64_t n_bins, double alpha, double* power, hipStream_t s) {
-  const int64_t ncell = cov_ncell(c);
+PowerParams power_params(int64_t n_bins, double alpha) {
   PowerParams P;
   P.n_bins = n_bins;
   P.half = (n_bins - 1) / 2;
@@ -2965,6 +3438,15 @@ int cov_power(rt_coverage* c, int64_t nrec, int64_t n_bins, double alpha, double
   P.turns = alpha / 6.283185307179586;
   P.sin_a = sin(alpha);
   P.cos_a = cos(alpha);
+  return P;
+}
+// ranges_done: the terms, cell ranges (epoch c->range_epoch) and nbig reset were already written
+// (k_owner_runs)
+int cov_power(rt_coverage* c, int64_t nrec, int64_t n_bins, double alpha, double* power, hipStream_t s,
+              bool ranges_done = false) {
+  c->ukeys_unsorted = false;
+  const int64_t ncell = cov_ncell(c);
+  const PowerParams P = power_params(n_bins, alpha);
   // one wave per owned cell, 4 per block
   const unsigned grid_cells = (unsigned)std::min<int64_t>((ncell / c->nshard + 4) / 4, 4096);
   // one thread per small cell, 64 per block: each thread's sweep is a chain of dependent loads,
@@ -2974,12 +3456,16 @@ int cov_power(rt_coverage* c, int64_t nrec, int64_t n_bins, double alpha, double
   // cells with more than kPowSmall terms, listed by k_power_small for k_power (count reset by k_cell_ranges)
   int32_t* big = c->bigcells;
   unsigned* nbig = reinterpret_cast<unsigned*>(c->runs + 3 * c->cap + 1);
-  const int32_t epoch = ++c->range_epoch;  // cells not stamped with it have no keys (k_cell_ranges)
-  const unsigned grid_u = (unsigned)std::max<int64_t>(1, std::min<int64_t>((nrec + 255) / 256, 8192));
-  if (nrec > 0)
-    hipLaunchKernelGGL(k_terms, dim3(grid_u), dim3(256), 0, s, c->ukeys, c->uamps, c->nuniq, P, c->tcos, c->tsin, c->ev);
-  hipLaunchKernelGGL(k_cell_ranges, dim3(grid_u), dim3(256), 0, s, c->ukeys, c->nuniq, ncell, c->cstart, c->cend,
-                     c->cepoch, epoch, nbig);
+  if (!ranges_done) {
+    const int32_t epoch = ++c->range_epoch;  // cells not stamped with it have no keys (k_cell_ranges)
+    const unsigned grid_u = (unsigned)std::max<int64_t>(1, std::min<int64_t>((nrec + 255) / 256, 8192));
+    if (nrec > 0)
+      hipLaunchKernelGGL(k_terms, dim3(grid_u), dim3(256), 0, s, c->ukeys, c->uamps, c->nuniq, P, c->tcos, c->tsin,
+                         c->ev);
+    hipLaunchKernelGGL(k_cell_ranges, dim3(grid_u), dim3(256), 0, s, c->ukeys, c->nuniq, ncell, c->cstart, c->cend,
+                       c->cepoch, epoch, nbig);
+  }
+  const int32_t epoch = c->range_epoch;
   hipLaunchKernelGGL(k_power_small, dim3(grid_small), dim3(64), 0, s, terms, c->cstart, c->cend, c->cepoch, epoch,
                      c->grid, c->shard, c->nshard, P, power, big, nbig);
   if (nrec > 0)
@@ -3027,6 +3513,8 @@ int rt_coverage_create(int device, const rt_mesh* env, int max_bounces, int64_t 
   if (e == hipSuccess) e = hipMalloc(&c->bigcells, sizeof(int32_t) * nc);
   if (e == hipSuccess) e = hipMalloc(&c->cepoch, sizeof(int32_t) * nc);
   if (e == hipSuccess) e = hipMemset(c->cepoch, 0, sizeof(int32_t) * nc);  // epochs start at 1
+  if (e == hipSuccess) e = hipMalloc(&c->own_aux, 16);
+  if (e == hipSuccess) e = hipMemset(c->own_aux, 0, 16);
   if (e == hipSuccess) e = hipHostMalloc((void**)&c->hcnt, 32, hipHostMallocDefault);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_cnt, hipEventDisableTiming);
   if (e != hipSuccess) {
@@ -3056,6 +3544,8 @@ int rt_coverage_destroy(rt_coverage* c) {
   if (c->cend) (void)hipFree(c->cend);
   if (c->bigcells) (void)hipFree(c->bigcells);
   if (c->cepoch) (void)hipFree(c->cepoch);
+  if (c->own_aux) (void)hipFree(c->own_aux);
+  if (c->segcells) (void)hipFree(c->segcells);
   if (c->items) (void)hipFree(c->items);
   if (c->bounds) (void)hipFree(c->bounds);
   if (c->work) (void)hipFree(c->work);
@@ -3344,8 +3834,57 @@ int power_segments_impl(rt_coverage* c, const uint64_t* keys, const uint64_t* su
   if (rc) return rc;
   c->ev_rec[6] = c->ev_rec[7] = false;
   prof_mark(c, 6, s);
+  bool fused = false;
   if (n > 0) {
     if ((rc = grow_for(c, n))) return rc;
+    const int64_t nxo = c->grid.nx > c->shard ? (c->grid.nx - c->shard + c->nshard - 1) / c->nshard : 0;
+    const int64_t nown = nxo * c->grid.ny * c->grid.nz;
+    if (RT_OWNER_CELLS && nseg <= kOcSegs && !c->segcells) {
+      const size_t b = (size_t)3 * kOcSegs * (size_t)std::max<int64_t>(nown, 1) * sizeof(int32_t);
+      RT_HIP(hipMalloc(&c->segcells, b));
+      RT_HIP(hipMemset(c->segcells, 0, b));  // epoch 0 is never a run's
+    }
+    if (RT_OWNER_CELLS && nseg <= kOcSegs) {
+      SegCells sc{c->segcells, c->segcells + kOcSegs * nown, c->segcells + 2 * kOcSegs * nown, nown};
+      const int32_t epoch = ++c->range_epoch;
+      unsigned* nbig = reinterpret_cast<unsigned*>(c->runs + 3 * c->cap + 1);
+      hipLaunchKernelGGL(k_seg_cells, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 8192)), dim3(256), 0, s, keys,
+                         stride, so, c->grid, c->shard, c->nshard, sc, epoch, c->nuniq, nbig);
+      OwnerCells oc{};
+      oc.keys = keys;
+      oc.kstride = stride;
+      oc.words = sums;
+      oc.vstride = stride == 1 ? 3 : stride;
+      oc.nseg = nseg;
+      oc.sc = sc;
+      oc.epoch = epoch;
+      oc.g = c->grid;
+      oc.shard = c->shard;
+      oc.nshard = c->nshard;
+      oc.P = power_params(n_bins, alpha);
+      oc.power = power;
+      oc.nuniq = c->nuniq;
+      oc.ukeys = c->ukeys;
+      oc.uamps = c->uamps;
+      oc.tcos = c->tcos;
+      oc.tsin = c->tsin;
+      oc.ev = c->ev;
+      oc.cstart = c->cstart;
+      oc.cend = c->cend;
+      oc.cepoch = c->cepoch;
+      oc.big = c->bigcells;
+      oc.nbig = nbig;
+      hipLaunchKernelGGL(k_owner_cells, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((nown + 63) / 64, 16384))),
+                         dim3(64), 0, s, oc);
+      const unsigned grid_cells = (unsigned)std::max<int64_t>(1, std::min<int64_t>((cov_ncell(c) / c->nshard + 4) / 4, 4096));
+      const TermArrays terms{c->ukeys, c->tcos, c->tsin, c->ev};
+      hipLaunchKernelGGL(k_power, dim3(grid_cells), dim3(256), 0, s, terms, c->cstart, c->cend, c->bigcells, nbig, oc.P,
+                         power);
+      RT_HIP(hipGetLastError());
+      c->ukeys_unsorted = true;
+      prof_mark(c, 7, s);
+      return RT_OK;
+    }
     int64_t* idx_sorted = reinterpret_cast<int64_t*>(c->oamps_sorted);
     // (G lanes per element, one binary search each, then a group sum: no faster on K3's 200k
     // records, 46 -> 76 us on K5's 465k -- the searches' loads, not their latency, set the time)
@@ -3362,13 +3901,47 @@ int power_segments_impl(rt_coverage* c, const uint64_t* keys, const uint64_t* su
     else
       hipLaunchKernelGGL(k_merge_segments, gm, dim3(256), 0, s, keys, stride, so, c->okeys_sorted, idx_sorted);
     RT_HIP(hipGetLastError());
-    WideKey wk{};
-    wk.identity = true;
-    rc = run_sums(c, SumVal{sums, idx_sorted, stride == 1 ? 3 : stride}, n, wk, s);
+    if (RT_OWNER_FUSED && nseg <= 8) {
+      OwnerRuns a{};
+      a.keys = c->okeys_sorted;
+      a.val = SumVal{sums, idx_sorted, stride == 1 ? 3 : stride};
+      a.n = n;
+      a.states = c->own_states;
+      a.ticket = c->own_aux;
+      a.errors = reinterpret_cast<unsigned*>(c->own_aux + 1);
+      const int64_t ntiles = (n + kOwnTile - 1) / kOwnTile;
+      a.ticket_base = c->own_tickets;
+      c->own_tickets += (uint64_t)ntiles;
+      a.tag = (c->own_tag++ % 0xFFFFFEull + 1ull) << 40;
+      a.ukeys = c->ukeys;
+      a.uamps = c->uamps;
+      a.tcos = c->tcos;
+      a.tsin = c->tsin;
+      a.ev = c->ev;
+      a.nuniq = c->nuniq;
+      a.ncell = cov_ncell(c);
+      a.cstart = c->cstart;
+      a.cend = c->cend;
+      a.cepoch = c->cepoch;
+      a.epoch = ++c->range_epoch;
+      a.nbig = reinterpret_cast<unsigned*>(c->runs + 3 * c->cap + 1);
+      a.P = power_params(n_bins, alpha);
+      a.heads = c->runs;
+      if (!RT_OWNER_LOOKBACK)
+        hipLaunchKernelGGL(k_tile_heads, dim3((unsigned)ntiles), dim3(256), 0, s, c->okeys_sorted, n, (int64_t)kOwnTile,
+                           c->runs);
+      hipLaunchKernelGGL(k_owner_runs, dim3((unsigned)ntiles), dim3(256), 0, s, a);
+      RT_HIP(hipGetLastError());
+      fused = true;
+    } else {
+      WideKey wk{};
+      wk.identity = true;
+      rc = run_sums(c, SumVal{sums, idx_sorted, stride == 1 ? 3 : stride}, n, wk, s);
+    }
   } else {
     RT_HIP(hipMemsetAsync(c->nuniq, 0, 8, s));
   }
-  if (!rc) rc = cov_power(c, n, n_bins, alpha, power, s);
+  if (!rc) rc = cov_power(c, n, n_bins, alpha, power, s, fused);
   if (!rc) prof_mark(c, 7, s);
   return rc;
 }
@@ -3440,8 +4013,16 @@ int rt_coverage_received(rt_coverage* c, uint64_t* keys_out, double* amps_out, i
   }
   *n_out = nu;
   const int64_t m = std::min(nu, max_out);
-  if (m > 0 && keys_out) RT_HIP(hipMemcpyAsync(keys_out, c->ukeys, m * 8, hipMemcpyDeviceToDevice, s));
-  if (m > 0 && amps_out) RT_HIP(hipMemcpyAsync(amps_out, c->uamps, m * 8, hipMemcpyDeviceToDevice, s));
+  const uint64_t* uk = c->ukeys;
+  const double* ua = c->uamps;
+  if (c->ukeys_unsorted && nu > 1 && (keys_out || amps_out)) {  // the per-cell owner stage: sort on demand
+    size_t tb = c->tmp_bytes;
+    RT_HIP(sort_records(c->tmp, tb, c->ukeys, c->okeys_sorted, c->uamps, c->oamps_sorted, nu, 64, s));
+    uk = c->okeys_sorted;
+    ua = c->oamps_sorted;
+  }
+  if (m > 0 && keys_out) RT_HIP(hipMemcpyAsync(keys_out, uk, m * 8, hipMemcpyDeviceToDevice, s));
+  if (m > 0 && amps_out) RT_HIP(hipMemcpyAsync(amps_out, ua, m * 8, hipMemcpyDeviceToDevice, s));
   return RT_OK;
 }
 

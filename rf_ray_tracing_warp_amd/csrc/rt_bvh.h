@@ -69,7 +69,39 @@ __device__ __forceinline__ float slab(const RayBox& r, float lx, float ly, float
 // leaf faces [first, first + count), count <= 4: the four 48-B records are fetched together
 // (indices clamped into the table, the results of q >= count ignored), so a leaf costs one
 // memory latency instead of one per face
+// RT_LEAF_PAIRS: a leaf's faces fetched two at a time instead of all four (24 instead of 48 VGPRs
+// in flight; a second latency only for leaves of more than two faces)
+#ifndef RT_LEAF_PAIRS
+#define RT_LEAF_PAIRS 0
+#endif
+__device__ __forceinline__ void leaf_face(const Shear& s, float4 a, float4 m, float4 c, Hit& h) {
+  const float4 q0 = make_float4(pick(a.x, a.y, a.z, s.kx), pick(a.x, a.y, a.z, s.ky), pick(a.x, a.y, a.z, s.kz),
+                                pick(a.w, m.x, m.y, s.kx));
+  const float4 q1 = make_float4(pick(a.w, m.x, m.y, s.ky), pick(a.w, m.x, m.y, s.kz), pick(m.z, m.w, c.x, s.kx),
+                                pick(m.z, m.w, c.x, s.ky));
+  const float c2 = pick(m.z, m.w, c.x, s.kz);
+  float T, det;
+  if (tri_test(s, q0, q1, c2, T, det)) hit_consider(h, T, det, __float_as_int(c.y));
+}
 __device__ __forceinline__ void leaf4(const BvhView& b, const Shear& s, int first, int count, Hit& h) {
+#if RT_LEAF_PAIRS
+#pragma unroll
+  for (int q0 = 0; q0 < 4; q0 += 2) {
+    if (q0 >= count) break;
+    float4 A[2], M[2], C[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const float4* p = b.lcomp + (int64_t)min(first + q0 + q, b.nf - 1) * 3;
+      A[q] = p[0];
+      M[q] = p[1];
+      C[q] = p[2];
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      if (q0 + q < count) leaf_face(s, A[q], M[q], C[q], h);
+  }
+  return;
+#endif
   float4 A[4], M[4], C[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {

@@ -32,6 +32,9 @@ KERNELS = {  # short name -> substring of the demangled rocprofv3 name
     "k_cols": "k_cols(",
     "k_power": "k_power(",
     "k_power_small": "k_power_small(",
+    "k_fill_received": "k_fill_received(",
+    "k_owner_cells": "k_owner_cells(",
+    "k_seg_cells": "k_seg_cells(",
 }
 
 
@@ -94,6 +97,12 @@ def main(tag, note=""):
     legs = {k: {"hbm_bytes_per_launch": v["hbm_bytes_per_launch"], "l2_hit_rate": v.get("l2_hit_rate"),
                 "avg_us": v["avg_us"], "source": f"profiles/{tag}_pmc.json", "note": note}
             for k, v in out["kernels"].items() if "hbm_bytes_per_launch" in v}
+    # a K4 step is the coalesced NaN / 0 fill of received and row_mask, then the trace kernel (which
+    # stores only the received rows): the leg's traffic is both launches' bytes
+    if "k_trace_bvh<5>" in legs and "k_fill_received" in legs:
+        t, f = legs["k_trace_bvh<5>"], legs["k_fill_received"]
+        t["hbm_bytes_per_launch"] += f["hbm_bytes_per_launch"]
+        t["note"] = (t["note"] + "; " if t["note"] else "") + "k_trace_bvh<5> + k_fill_received"
     json.dump(legs, open(os.path.join(ROOT, "profiles", "traffic_legs.json"), "w"), indent=1)
     k2 = out["kernels"].get("k_trace_bf<3>", {})
     if "hbm_bytes_per_launch" in k2:
