@@ -604,6 +604,85 @@ __global__ __launch_bounds__(256, RT_TRAJ_SPLIT_WAVES) void k_traj_split(CovPara
   }
 }
 
+// k_traj for brute-force scenes with few rays (a ray-sharded rank's share, RT_TRAJ_LDS_SPLIT): G
+// lanes per ray, lane j testing the faces f = j, j + G, ... of the LDS table (ascending, so the
+// deferred division's order rule holds within the lane); the lexicographic (t, face) minimum of the
+// G lanes (group_hit) is the ray's closest hit, bit for bit the one-lane loop's.  A K3 rank of 8
+// has 125k rays: one lane per ray is ~490 waves for 1024 SIMDs, and the kernel took as long as one
+// wave's 3 x 44 face tests (41 us against 20 for an eighth of the one-GPU pass).
+#ifndef RT_TRAJ_LDS_SPLIT
+#define RT_TRAJ_LDS_SPLIT 4
+#endif
+template <int G>
+__global__ __launch_bounds__(256) void k_traj_lds_split(CovParams p) {
+  extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
+  constexpr int LG = G == 8 ? 3 : (G == 4 ? 2 : 1);
+  static_assert(G == 2 || G == 4 || G == 8, "2, 4 or 8 lanes per ray");
+  if (p.zero_ctr && blockIdx.x == 0 && threadIdx.x < 4) p.zero_ctr[threadIdx.x] = 0ull;
+  stage_env<false>(p, lds_tab);
+  const int j = threadIdx.x & (G - 1);
+  const int64_t stride = ((int64_t)gridDim.x * blockDim.x) >> LG;
+  const int64_t nit = (p.n + stride - 1) / stride;  // every lane of a wave runs the same iterations
+  for (int64_t it = 0; it < nit; ++it) {
+    const int64_t ir = it * stride + (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> LG);
+    const bool valid = ir < p.n;
+    float3 dir = rt::ray_dir(p.ray_offset + (valid ? ir : 0));
+    float3 pos = make_float3(p.tx[0], p.tx[1], p.tx[2]);
+    int nseg = 0;
+    bool alive = valid;
+    for (int k = 0; k < p.B; ++k) {
+      const rt::Shear s = rt::make_shear(pos, dir);
+#if RT_LAZY_HIT
+      rt::LazyHit lh;
+      rt::lazy_init(lh);
+#else
+      rt::Hit lh;
+      rt::hit_init(lh);
+#endif
+      if (alive) {
+        const int off = s.kcase * 3;
+        for (int f = j; f < p.env_nf; f += G) {
+          const float4 q0 = lds_tab[f * 18 + off + 0];
+          const float4 q1 = lds_tab[f * 18 + off + 1];
+          const float c2 = lds_tab[f * 18 + off + 2].x;
+          float T, det;
+#if RT_LAZY_HIT
+          if (rt::tri_test(s, q0, q1, c2, T, det)) rt::lazy_consider(lh, T, det, f);
+#else
+          if (rt::tri_test(s, q0, q1, c2, T, det)) rt::hit_consider(lh, T, det, f);
+#endif
+        }
+      }
+#if RT_LAZY_HIT
+      const rt::Hit he = rt::group_hit<G>(rt::lazy_finish(lh));
+#else
+      const rt::Hit he = rt::group_hit<G>(lh);
+#endif
+      if (!alive) continue;
+      if (j == 0) {
+        float4* tp = p.traj + 2 * (ir * p.B + k);  // slot ir, as k_traj
+        tp[0] = make_float4(pos.x, pos.y, pos.z, he.face < 0 ? INFINITY : he.t);
+        tp[1] = make_float4(dir.x, dir.y, dir.z, 0.0f);
+      }
+      nseg = k + 1;
+      if (he.face < 0) {
+        alive = false;  // escapes: this segment is infinite, later iterations repeat the miss
+        continue;
+      }
+      pos.x = fmaf(dir.x, he.t, pos.x);
+      pos.y = fmaf(dir.y, he.t, pos.y);
+      pos.z = fmaf(dir.z, he.t, pos.z);
+      const float4 n4 = p.env_nrm[he.face];
+      const float3 n = make_float3(n4.x, n4.y, n4.z);
+      const float sc = 2.0f * rt::dot3(dir, n);
+      dir.x = fmaf(-sc, n.x, dir.x);
+      dir.y = fmaf(-sc, n.y, dir.y);
+      dir.z = fmaf(-sc, n.z, dir.z);
+    }
+    if (valid && j == 0) p.nseg[ir] = (uint8_t)nseg;
+  }
+}
+
 // ------------------------------------------------------------------ 2. candidate cells per segment
 // One atomic per 256-thread block: exclusive prefix of the threads' counts (wave scan + LDS),
 // thread 0 reserves the block's total.  Every thread of the block must call it (inactive: c = 0);
@@ -3200,7 +3279,12 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
     p.order = nullptr;
   } else {
     prof_mark(c, 0, s);
-    hipLaunchKernelGGL(k_traj<false>, dim3(grid_rays), dim3(256), lds, s, p);
+    if (RT_TRAJ_LDS_SPLIT > 1 && c->n <= traj_split_max_rays())  // few rays: G lanes per ray
+      hipLaunchKernelGGL(k_traj_lds_split<RT_TRAJ_LDS_SPLIT>,
+                         dim3((unsigned)std::min<int64_t>((RT_TRAJ_LDS_SPLIT * c->n + 255) / 256, 8192)), dim3(256),
+                         lds, s, p);
+    else
+      hipLaunchKernelGGL(k_traj<false>, dim3(grid_rays), dim3(256), lds, s, p);
     prof_mark(c, 1, s);
   }
   RT_HIP(hipGetLastError());
@@ -3839,12 +3923,13 @@ int power_segments_impl(rt_coverage* c, const uint64_t* keys, const uint64_t* su
     if ((rc = grow_for(c, n))) return rc;
     const int64_t nxo = c->grid.nx > c->shard ? (c->grid.nx - c->shard + c->nshard - 1) / c->nshard : 0;
     const int64_t nown = nxo * c->grid.ny * c->grid.nz;
-    if (RT_OWNER_CELLS && nseg <= kOcSegs && !c->segcells) {
+    const bool per_cell = RT_OWNER_CELLS && nseg <= kOcSegs && n_bins <= INT32_MAX;  // bins kept as int32
+    if (per_cell && !c->segcells) {
       const size_t b = (size_t)3 * kOcSegs * (size_t)std::max<int64_t>(nown, 1) * sizeof(int32_t);
       RT_HIP(hipMalloc(&c->segcells, b));
       RT_HIP(hipMemset(c->segcells, 0, b));  // epoch 0 is never a run's
     }
-    if (RT_OWNER_CELLS && nseg <= kOcSegs) {
+    if (per_cell) {
       SegCells sc{c->segcells, c->segcells + kOcSegs * nown, c->segcells + 2 * kOcSegs * nown, nown};
       const int32_t epoch = ++c->range_epoch;
       unsigned* nbig = reinterpret_cast<unsigned*>(c->runs + 3 * c->cap + 1);

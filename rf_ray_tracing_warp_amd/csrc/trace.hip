@@ -121,6 +121,9 @@ __device__ __forceinline__ bool rx_maybe(const TraceArgs& a, float3 o, float3 d,
 #ifndef RT_SPARSE_RX
 #define RT_SPARSE_RX 1
 #endif
+#ifndef RT_PATH_LDS
+#define RT_PATH_LDS 0
+#endif
 // received rows = NaN, row_mask = 0, in row order with 16-B streaming stores (RT_SPARSE_RX)
 __global__ __launch_bounds__(256) void k_fill_received(float* received, int64_t nwords, uint32_t* mask, int64_t n) {
   typedef uint32_t u4v __attribute__((ext_vector_type(4)));
@@ -461,7 +464,32 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
     const int64_t gid = a.ray_offset + row;
     float3 dir = rt::ray_dir(gid);
     float3 pos = make_float3(a.tx[0], a.tx[1], a.tx[2]);
+#if RT_PATH_LDS
+    // BVH kernels: the path's points 1..B wait in this thread's LDS column instead of 3B VGPRs
+    // live through every walk (K4: 5 waves per SIMD instead of 4), and come back for the row stores
+    __shared__ float s_path[USE_BVH ? 3 * B : 1][256];
     float path[P][3];
+    int npts = 0;
+    auto set_pt = [&](int i, float3 q) {
+      if constexpr (USE_BVH) {
+        s_path[3 * (i - 1) + 0][threadIdx.x] = q.x;
+        s_path[3 * (i - 1) + 1][threadIdx.x] = q.y;
+        s_path[3 * (i - 1) + 2][threadIdx.x] = q.z;
+        npts = i;
+      } else {
+        path[i][0] = q.x;
+        path[i][1] = q.y;
+        path[i][2] = q.z;
+      }
+    };
+#else
+    float path[P][3];
+    auto set_pt = [&](int i, float3 q) {
+      path[i][0] = q.x;
+      path[i][1] = q.y;
+      path[i][2] = q.z;
+    };
+#endif
 #pragma unroll
     for (int i = 0; i < P; ++i) path[i][0] = path[i][1] = path[i][2] = qnan;
     path[0][0] = pos.x;
@@ -486,9 +514,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
           pos.x = fmaf(dir.x, hr.t, pos.x);
           pos.y = fmaf(dir.y, hr.t, pos.y);
           pos.z = fmaf(dir.z, hr.t, pos.z);
-          path[b + 1][0] = pos.x;
-          path[b + 1][1] = pos.y;
-          path[b + 1][2] = pos.z;
+          set_pt(b + 1, pos);
           last_rx = b + 1;
           kind = 2;
           face = hr.face;
@@ -496,9 +522,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
           pos.x = fmaf(dir.x, he.t, pos.x);
           pos.y = fmaf(dir.y, he.t, pos.y);
           pos.z = fmaf(dir.z, he.t, pos.z);
-          path[b + 1][0] = pos.x;
-          path[b + 1][1] = pos.y;
-          path[b + 1][2] = pos.z;
+          set_pt(b + 1, pos);
           const float4 n4 = a.env_nrm[he.face];
           const float3 n = make_float3(n4.x, n4.y, n4.z);
           const float sc = 2.0f * rt::dot3(dir, n);
@@ -514,6 +538,17 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
       if (a.hit_kind) a.hit_kind[row * B + b] = kind;
       if (a.hit_face) a.hit_face[row * B + b] = face;
     }
+#if RT_PATH_LDS
+    if constexpr (USE_BVH) {
+#pragma unroll
+      for (int i = 1; i < P; ++i)
+        if (i <= npts) {
+          path[i][0] = s_path[3 * (i - 1) + 0][threadIdx.x];
+          path[i][1] = s_path[3 * (i - 1) + 1][threadIdx.x];
+          path[i][2] = s_path[3 * (i - 1) + 2][threadIdx.x];
+        }
+    }
+#endif
     // a full wave of consecutive rows (brute force, no row order): transposed 1-KB stores
     const bool wave_rows = RT_ROW_PERMUTE && P == 4 && !a.order && chunk * 256 + (threadIdx.x | 63) < a.n;
     if (a.traced) {

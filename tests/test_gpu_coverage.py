@@ -356,3 +356,76 @@ def test_trace_records_into_small_buffers_falls_back(room):
     assert k1.cpu().numpy().tobytes() == k2.cpu().numpy().tobytes()
     assert s1.cpu().numpy().tobytes() == s2.cpu().numpy().tobytes()
     p.close()
+
+
+def test_trace_rows_into_small_buffer_fetches_packed(room):
+    """Coverage.trace_rows with a too-small row buffer: rt_coverage_trace_records_packed reports it,
+    and the rows come from rt_coverage_records_packed (no second trace) -- the same rows, in the
+    same order, as with a buffer that was large enough; and the same rows as trace_records' keys
+    and sums."""
+    grid, tx, B, N = CoverageGrid(8.0, -2.5, 4.6, 0.37, 0.41, 0.4, 13, 12, 2), (10, 0, 5), 3, 60_000
+    p = Coverage(room, 2.998e8, 100e9, 100e-9, B, N, grid, shard_index=0, shard_count=2, shard_mode="rays")
+    r1, c1 = p.trace_rows(tx, 1)
+    r1 = r1.clone()
+    assert sum(c1) > 100
+    p._rows = torch.empty((1, 4), dtype=torch.int64, device="cuda")
+    r2, c2 = p.trace_rows(tx, 1)
+    assert c1 == c2 and p._rows.shape[0] >= sum(c1)
+    assert r1.cpu().numpy().tobytes() == r2.cpu().numpy().tobytes()
+    k, s, c3 = p.trace_records(tx, 1)
+    assert c3 == c1
+    assert np.array_equal(r1[:, 0].cpu().numpy(), k.cpu().numpy())
+    assert np.array_equal(r1[:, 1:].cpu().numpy(), s.cpu().numpy())
+    p.close()
+
+
+@pytest.mark.parametrize("nseg", [1, 3, 8, 9])
+def test_owner_segments_every_sweep_path(room, nseg):
+    """The owner stage on segments (rt_coverage_power_segments: the per-cell path for <= 8 sources,
+    the merge path above that) against the sorted path (rt_coverage_power_records) on the same
+    records: cells of 0 .. 9999 bins (every sweep: thread, wave, range-split), each (cell, bin)'s
+    fixed-point amplitude split over up to nseg source segments, each segment in key order.  Maps
+    and impulse responses bit for bit."""
+    rng = np.random.default_rng(21 + nseg)
+    sizes = [0, 1, 2, 5, 16, 17, 64, 191, 192, 193, 400, 2500, 9999]
+    grid = CoverageGrid(0.0, 0.0, 5.0, 1.0, 1.0, 1.0, len(sizes), 1, 1)
+    n, win = 10000, 100e-9
+    keys, sums = [], []
+    for c, K in enumerate(sizes):
+        for b in np.sort(rng.choice(n, K, replace=False)) if K else []:
+            keys.append((c << 32) | int(b))
+    keys = np.array(keys, np.uint64)
+    cov = Coverage(room, 2.998e8, 100e9, win, 3, 1000, grid, shard_mode="rays")
+    amps = torch.from_numpy(rng.uniform(1e-9, 1e-5, len(keys))).cuda()
+    from rf_ray_tracing_warp_amd.coverage import amps_to_sums
+    full = amps_to_sums(amps).cpu().numpy().view(np.uint64)  # (n, 3) fixed point, w0 least significant
+    # split each record's fixed point into parts on distinct random segments (exact: integer limbs)
+    seg_rows = [[] for _ in range(nseg)]
+    for i, k in enumerate(keys):
+        parts = int(rng.integers(1, min(nseg, 3) + 1))
+        segs = rng.choice(nseg, parts, replace=False)
+        rest = full[i].copy()
+        for j, sg in enumerate(segs):
+            if j == parts - 1:
+                piece = rest.copy()
+            else:  # take the low word's low half: no borrow across words
+                piece = np.array([rest[0] & np.uint64(0xFFFFFFFF), 0, 0], np.uint64)
+                rest = rest - piece
+            seg_rows[sg].append((k, piece))
+    k_all, s_all, counts = [], [], []
+    for rows in seg_rows:
+        rows.sort(key=lambda r: int(r[0]))
+        counts.append(len(rows))
+        k_all += [r[0] for r in rows]
+        s_all += [r[1] for r in rows]
+    kt = torch.from_numpy(np.array(k_all, np.uint64).view(np.int64)).cuda()
+    st = torch.from_numpy(np.array(s_all, np.uint64).reshape(-1, 3).view(np.int64)).cuda()
+    got = cov.power_from_records(kt, st, counts).cpu().numpy().copy()
+    gi = cov.impulse_responses()
+    ref = cov.power_from_records(kt, st).cpu().numpy().copy()
+    ri = cov.impulse_responses()
+    cov.close()
+    assert got.tobytes() == ref.tobytes()
+    assert np.isfinite(ref).sum() == sum(1 for K in sizes if K)
+    for x, y in zip(gi, ri):
+        assert x.tobytes() == y.tobytes()

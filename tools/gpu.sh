@@ -99,12 +99,14 @@ run_task() {
         done
       done ;;
     ossort)
-      # tool binaries are not pushed (.gpurunignore): build on the box, same image
-      timeout -k 10 300 hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/os_sort_bench.hip -o /tmp/os_sort_bench
-      rc=$?; step_rc $rc "ossort build"
-      for a in "1048576 30 0.5" "786432 35 0.5" "7864320 31 0.3" "6291456 36 0.3" "200000 30 0.5"; do
-        timeout -k 10 60 /tmp/os_sort_bench $a >> ${O}_os_sort.jsonl 2>&1
-        rc=$?; tail -1 ${O}_os_sort.jsonl; step_rc $rc "ossort $a"
+      # tool binaries are not pushed (.gpurunignore): build on the box, same image; one per digit width
+      for b in ${OS_BITS_LIST:-8 10 12}; do
+        timeout -k 10 300 hipcc -O3 --offload-arch=gfx950 -std=c++17 -DOS_BITS=$b tools/os_sort_bench.hip -o /tmp/os_sort_bench$b
+        rc=$?; step_rc $rc "ossort build $b"
+        for a in "786432 35 0.5" "1048576 30 0.5" "200000 30 0.5" "6291456 36 0.3"; do
+          timeout -k 10 60 /tmp/os_sort_bench$b $a >> ${O}_os_sort.jsonl 2>&1
+          rc=$?; tail -1 ${O}_os_sort.jsonl; step_rc $rc "ossort $b $a"
+        done
       done ;;
     rehearse)
       for n in 2 4; do

@@ -39,7 +39,10 @@
   } while (0)
 
 constexpr int kOsThreads = 256, kOsItems = 16, kOsWaveItems = 64 * kOsItems, kOsTile = kOsThreads * kOsItems;
-constexpr int kOsMaxBits = 12, kOsMaxBins = 1 << kOsMaxBits, kOsMaxPasses = 4;
+#ifndef OS_BITS
+#define OS_BITS 12  // digit bits per pass (-DOS_BITS=8 / 10 for the narrower-digit variants)
+#endif
+constexpr int kOsMaxBits = OS_BITS, kOsMaxBins = 1 << kOsMaxBits, kOsMaxPasses = (48 + OS_BITS - 1) / OS_BITS;
 constexpr uint64_t kOsAgg = 1ull << 38, kOsInc = 2ull << 38, kOsCount = (1ull << 38) - 1;
 constexpr uint64_t kOsTagMask = ~(kOsInc | kOsAgg | kOsCount);
 constexpr size_t kOsHistWords = (size_t)kOsMaxPasses * kOsMaxBins;  // u32 per histogram buffer
@@ -239,7 +242,7 @@ int main(int argc, char** argv) {
   const int64_t n = argc > 1 ? atoll(argv[1]) : 1048576;
   const int bits = argc > 2 ? atoi(argv[2]) : 30;
   const double hot = argc > 3 ? atof(argv[3]) : 0.5;
-  if (n < 1 || n > (1ll << 30) || bits < 1 || bits > kOsMaxPasses * kOsMaxBits) {
+  if (n < 1 || n > (1ll << 30) || bits < 1 || bits > 48) {
     fprintf(stderr, "usage: os_sort_bench [N <= 2^30] [bits 1..48] [hot]\n");
     return 2;
   }
@@ -292,9 +295,9 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(c.data(), vo1, n * 8, hipMemcpyDeviceToHost));
   CK(hipMemcpy(d.data(), vo2, n * 8, hipMemcpyDeviceToHost));
   const bool same = a == b && c == d;
-  printf("{\"n\": %lld, \"bits\": %d, \"hot\": %.2f, \"passes\": %d, \"rocprim_us\": %.1f, \"os_us\": %.1f, "
+  printf("{\"digit_bits\": %d, \"n\": %lld, \"bits\": %d, \"hot\": %.2f, \"passes\": %d, \"rocprim_us\": %.1f, \"os_us\": %.1f, "
          "\"bit_identical\": %s, \"spin_or_range_errors\": %u}\n",
-         (long long)n, bits, hot, (bits + kOsMaxBits - 1) / kOsMaxBits, us_rocprim, us_os, same ? "true" : "false",
+         OS_BITS, (long long)n, bits, hot, (bits + kOsMaxBits - 1) / kOsMaxBits, us_rocprim, us_os, same ? "true" : "false",
          errors);
   return same && errors == 0 ? 0 : 1;
 }
