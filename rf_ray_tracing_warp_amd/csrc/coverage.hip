@@ -2134,8 +2134,6 @@ struct rt_coverage {
   uint64_t* own_states = nullptr;
   unsigned long long* own_aux = nullptr;
   uint64_t own_tickets = 0, own_tag = 0;
-  int32_t* segcells = nullptr;  // k_seg_cells: [3][kOcSegs][nown] (start, count, epoch) of ray-mode owners
-  bool ukeys_unsorted = false;  // the last owner stage left ukeys in reservation order
   uint8_t* win = nullptr;
   uint8_t* first_flag = nullptr;
   float* trx = nullptr;
@@ -2694,234 +2692,6 @@ __global__ __launch_bounds__(256) void k_owner_runs(OwnerRuns a) {
       if (e >= a.n || (a.keys[e] >> 32) != cell) a.cend[cell] = (int32_t)(u + 1);
     }
     ++u;
-  }
-}
-
-// ---- Owner stage per cell (RT_OWNER_CELLS, default): no merge of the received segments.
-// k_seg_cells: every received record that starts its cell's run within its segment stamps the
-//   cell's (first record, count) for that segment (epoch-tagged, so nothing is cleared);
-// k_owner_cells: one thread per owned cell merges its <= nseg runs (a few records each), adds the
-//   equal keys' fixed-point sums, keeps the cell's unique (bin, f64 amplitude) terms in LDS and, for
-//   up to kPowSmall terms, sweeps the power at once (power_sparse with the terms' phases computed as
-//   k_terms does, so the same bits as the one-GPU map); larger cells get their terms written to the
-//   global term arrays and are listed for k_power, unchanged.  Every cell's unique keys and
-//   amplitudes also go to ukeys / uamps (rt_coverage_received), at a range reserved with one
-//   atomic per wave -- so not in key order there (rt_coverage_received sorts on demand).
-// Replaces the merge, run sums, terms, cell ranges and small-cell sweep (five launches, each a
-// latency-bound pass over all records: ~130-180 us per owner of 8 on K3 / K5).
-#ifndef RT_OWNER_CELLS
-#define RT_OWNER_CELLS 1
-#endif
-constexpr int kOcSegs = 8;
-struct SegCells {  // [kOcSegs][nown]: a cell's run in each segment (valid when ep == epoch)
-  int32_t *start, *cnt, *ep;
-  int64_t nown;
-};
-__device__ __forceinline__ uint32_t owned_index(uint32_t c, const rt_grid& g, int shard, int nshard) {
-  const uint32_t nx = (uint32_t)g.nx, ns = (uint32_t)nshard;
-  const uint32_t nxo = (nx - (uint32_t)shard + ns - 1) / ns;
-  const uint32_t row = c / nx, ix = c - row * nx;
-  return row * nxo + (ix - (uint32_t)shard) / ns;
-}
-__global__ __launch_bounds__(256) void k_seg_cells(const uint64_t* keys, int64_t kstride, SegOffsets so, rt_grid g,
-                                                   int shard, int nshard, SegCells sc, int32_t epoch,
-                                                   int64_t* nuniq_ctr, unsigned* nbig) {
-  const int64_t n = so.off[so.nseg];
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    *nuniq_ctr = 0;  // k_owner_cells reserves its cells' ranges from it
-    *nbig = 0u;
-  }
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    int sg = 0;
-    while (sg + 1 < so.nseg && so.off[sg + 1] <= i) ++sg;
-    const uint64_t cell = keys[i * kstride] >> 32;
-    if (i > so.off[sg] && (keys[(i - 1) * kstride] >> 32) == cell) continue;  // not the first of its run
-    int64_t a = i + 1, b = so.off[sg + 1];  // first record of a later cell (keys ascend)
-    while (a < b) {
-      const int64_t m = (a + b) >> 1;
-      if ((keys[m * kstride] >> 32) == cell) a = m + 1;
-      else b = m;
-    }
-    const int64_t slot = (int64_t)sg * sc.nown + owned_index((uint32_t)cell, g, shard, nshard);
-    sc.start[slot] = (int32_t)i;
-    sc.cnt[slot] = (int32_t)(a - i);
-    sc.ep[slot] = epoch;
-  }
-}
-// a cell's terms from its (bin, amplitude) pairs in LDS, the phases computed as k_terms does
-struct FlyTerms {
-  const int32_t (*sm)[64];
-  const double (*sa)[64];
-  int lane;
-  PowerParams P;
-  __device__ __forceinline__ int64_t m(int64_t k) const { return sm[k][lane]; }
-  __device__ __forceinline__ void cs(int64_t k, double& c, double& s) const {
-    double sp, cp;
-    sincos_turns(P.turns * (double)(P.half - m(k)), sp, cp);
-    const double a = sa[k][lane];
-    c = a * cp;
-    s = a * sp;
-  }
-  __device__ __forceinline__ void start(int64_t k, double& s, double& c) const {
-    const int64_t mk = m(k), st = mk - P.half > 0 ? mk - P.half : 0;
-    sincos_turns(P.turns * (double)st, s, c);
-  }
-  __device__ __forceinline__ void stop(int64_t k, double& s, double& c) const {
-    const int64_t mk = m(k), e = mk + (P.n_bins - 1 - P.half), e1 = (e < P.n_bins - 1 ? e : P.n_bins - 1) + 1;
-    sincos_turns(P.turns * (double)e1, s, c);
-  }
-};
-struct OwnerCells {
-  const uint64_t* keys;  // received keys at keys[i * kstride]
-  int64_t kstride;
-  const uint64_t* words;  // received sums at words[i * vstride .. + 2]
-  int64_t vstride;
-  int nseg;
-  SegCells sc;
-  int32_t epoch;
-  rt_grid g;
-  int shard, nshard;
-  PowerParams P;
-  double* power;
-  int64_t* nuniq;  // reservation counter, then the unique count
-  uint64_t* ukeys;
-  double *uamps, *tcos, *tsin, *ev;
-  int32_t *cstart, *cend, *cepoch;
-  int32_t* big;
-  unsigned* nbig;
-};
-__global__ __launch_bounds__(64) void k_owner_cells(OwnerCells a) {
-  __shared__ int32_t s_m[kPowSmall][64];
-  __shared__ double s_a[kPowSmall][64];
-  const rt_grid& g = a.g;
-  const int lane = threadIdx.x & 63;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  {  // other ranks' cells: 0 (the map is sum-reduced), 32-bit index arithmetic
-    const uint32_t ncell = (uint32_t)(g.nx * g.ny * g.nz), nx = (uint32_t)g.nx, ns = (uint32_t)a.nshard;
-    if (a.nshard > 1)
-      for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < ncell; c += (uint32_t)stride)
-        if ((c % nx) % ns != (uint32_t)a.shard) a.power[c] = 0.0;
-  }
-  const int64_t nxo = g.nx > a.shard ? (g.nx - a.shard + a.nshard - 1) / a.nshard : 0;
-  const int64_t nown = nxo * g.ny * g.nz;
-  auto val = [&](int64_t i) {
-    const uint64_t* q = a.words + i * a.vstride;
-    return Fx192{q[0], q[1], q[2]};
-  };
-  for (int64_t base = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); base < nown; base += stride) {
-    const int64_t t = base + lane;
-    const bool valid = t < nown;
-    int64_t cell = 0;
-    int32_t pos[kOcSegs], end[kOcSegs];
-    uint64_t hk[kOcSegs];
-    if (valid) {
-      const int64_t jx = t % nxo, rest = t / nxo;
-      cell = rest * g.nx + a.shard + jx * a.nshard;
-    }
-#pragma unroll
-    for (int s = 0; s < kOcSegs; ++s) {
-      pos[s] = end[s] = 0;
-      if (valid && s < a.nseg) {
-        const int64_t slot = (int64_t)s * a.sc.nown + t;
-        if (a.sc.ep[slot] == a.epoch) {
-          pos[s] = a.sc.start[slot];
-          end[s] = pos[s] + a.sc.cnt[slot];
-        }
-      }
-    }
-    // merge the runs: unique keys ascending, equal keys' sums added exactly
-    int K = 0;
-#pragma unroll
-    for (int s = 0; s < kOcSegs; ++s) hk[s] = pos[s] < end[s] ? a.keys[(int64_t)pos[s] * a.kstride] : ~0ull;
-    while (true) {
-      uint64_t km = ~0ull;
-#pragma unroll
-      for (int s = 0; s < kOcSegs; ++s) km = hk[s] < km ? hk[s] : km;
-      if (km == ~0ull) break;
-      Fx192 acc{0, 0, 0};
-#pragma unroll
-      for (int s = 0; s < kOcSegs; ++s)
-        if (hk[s] == km) {
-          acc = FxPlus()(acc, val(pos[s]));
-          ++pos[s];
-          hk[s] = pos[s] < end[s] ? a.keys[(int64_t)pos[s] * a.kstride] : ~0ull;
-        }
-      if (K < kPowSmall) {
-        s_m[K][lane] = (int32_t)(km & 0xFFFFFFFFull);
-        s_a[K][lane] = fx_to_double(acc);
-      }
-      ++K;
-    }
-    // this cell's range of the unique arrays: one atomic per wave
-    int64_t x = K;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int64_t y = __shfl_up(x, o, 64);
-      if (lane >= o) x += y;
-    }
-    int64_t u0 = 0;
-    if (lane == 63 && x > 0) u0 = (int64_t)atomicAdd((unsigned long long*)a.nuniq, (unsigned long long)x);
-    u0 = __shfl(u0, 63, 64) + x - K;
-    const bool is_big = valid && K > kPowSmall;
-    if (valid && !is_big) {
-      for (int k = 0; k < K; ++k) {
-        a.ukeys[u0 + k] = (uint64_t)cell << 32 | (uint32_t)s_m[k][lane];
-        a.uamps[u0 + k] = s_a[k][lane];
-      }
-      a.power[cell] = power_sparse(0, K, a.P, FlyTerms{s_m, s_a, lane, a.P});  // NaN when empty
-    }
-    if (is_big) {  // the terms to the global arrays for k_power (the runs merged again)
-#pragma unroll
-      for (int s = 0; s < kOcSegs; ++s) {
-        pos[s] = end[s] = 0;
-        if (s < a.nseg) {
-          const int64_t slot = (int64_t)s * a.sc.nown + t;
-          if (a.sc.ep[slot] == a.epoch) {
-            pos[s] = a.sc.start[slot];
-            end[s] = pos[s] + a.sc.cnt[slot];
-          }
-        }
-        hk[s] = pos[s] < end[s] ? a.keys[(int64_t)pos[s] * a.kstride] : ~0ull;
-      }
-      const PowerParams& P = a.P;
-      for (int64_t u = u0;; ++u) {
-        uint64_t km = ~0ull;
-#pragma unroll
-        for (int s = 0; s < kOcSegs; ++s) km = hk[s] < km ? hk[s] : km;
-        if (km == ~0ull) break;
-        Fx192 acc{0, 0, 0};
-#pragma unroll
-        for (int s = 0; s < kOcSegs; ++s)
-          if (hk[s] == km) {
-            acc = FxPlus()(acc, val(pos[s]));
-            ++pos[s];
-            hk[s] = pos[s] < end[s] ? a.keys[(int64_t)pos[s] * a.kstride] : ~0ull;
-          }
-        const double amp = fx_to_double(acc);
-        const int64_t m = (int64_t)(km & 0xFFFFFFFFull);
-        a.ukeys[u] = km;
-        a.uamps[u] = amp;
-        double sp, cp;
-        sincos_turns(P.turns * (double)(P.half - m), sp, cp);
-        a.tcos[u] = amp * cp;
-        a.tsin[u] = amp * sp;
-        const int64_t st = m - P.half > 0 ? m - P.half : 0;
-        const int64_t e = m + (P.n_bins - 1 - P.half), e1 = (e < P.n_bins - 1 ? e : P.n_bins - 1) + 1;
-        sincos_turns(P.turns * (double)st, a.ev[4 * u], a.ev[4 * u + 1]);
-        sincos_turns(P.turns * (double)e1, a.ev[4 * u + 2], a.ev[4 * u + 3]);
-      }
-      a.cstart[cell] = (int32_t)u0;
-      a.cend[cell] = (int32_t)(u0 + K);
-      a.cepoch[cell] = a.epoch;
-    }
-    const uint64_t mb = __ballot(is_big);
-    if (mb) {
-      unsigned b0 = 0;
-      if (lane == 0) b0 = atomicAdd(a.nbig, (unsigned)__popcll(mb));
-      b0 = __shfl(b0, 0, 64);
-      if (is_big) a.big[b0 + (unsigned)__builtin_amdgcn_mbcnt_hi((uint32_t)(mb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mb, 0u))] =
-          (int32_t)cell;
-    }
   }
 }
 
@@ -3528,7 +3298,6 @@ PowerParams power_params(int64_t n_bins, double alpha) {
 // (k_owner_runs)
 int cov_power(rt_coverage* c, int64_t nrec, int64_t n_bins, double alpha, double* power, hipStream_t s,
               bool ranges_done = false) {
-  c->ukeys_unsorted = false;
   const int64_t ncell = cov_ncell(c);
   const PowerParams P = power_params(n_bins, alpha);
   // one wave per owned cell, 4 per block
@@ -3629,7 +3398,6 @@ int rt_coverage_destroy(rt_coverage* c) {
   if (c->bigcells) (void)hipFree(c->bigcells);
   if (c->cepoch) (void)hipFree(c->cepoch);
   if (c->own_aux) (void)hipFree(c->own_aux);
-  if (c->segcells) (void)hipFree(c->segcells);
   if (c->items) (void)hipFree(c->items);
   if (c->bounds) (void)hipFree(c->bounds);
   if (c->work) (void)hipFree(c->work);
@@ -3921,55 +3689,6 @@ int power_segments_impl(rt_coverage* c, const uint64_t* keys, const uint64_t* su
   bool fused = false;
   if (n > 0) {
     if ((rc = grow_for(c, n))) return rc;
-    const int64_t nxo = c->grid.nx > c->shard ? (c->grid.nx - c->shard + c->nshard - 1) / c->nshard : 0;
-    const int64_t nown = nxo * c->grid.ny * c->grid.nz;
-    const bool per_cell = RT_OWNER_CELLS && nseg <= kOcSegs && n_bins <= INT32_MAX;  // bins kept as int32
-    if (per_cell && !c->segcells) {
-      const size_t b = (size_t)3 * kOcSegs * (size_t)std::max<int64_t>(nown, 1) * sizeof(int32_t);
-      RT_HIP(hipMalloc(&c->segcells, b));
-      RT_HIP(hipMemset(c->segcells, 0, b));  // epoch 0 is never a run's
-    }
-    if (per_cell) {
-      SegCells sc{c->segcells, c->segcells + kOcSegs * nown, c->segcells + 2 * kOcSegs * nown, nown};
-      const int32_t epoch = ++c->range_epoch;
-      unsigned* nbig = reinterpret_cast<unsigned*>(c->runs + 3 * c->cap + 1);
-      hipLaunchKernelGGL(k_seg_cells, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 8192)), dim3(256), 0, s, keys,
-                         stride, so, c->grid, c->shard, c->nshard, sc, epoch, c->nuniq, nbig);
-      OwnerCells oc{};
-      oc.keys = keys;
-      oc.kstride = stride;
-      oc.words = sums;
-      oc.vstride = stride == 1 ? 3 : stride;
-      oc.nseg = nseg;
-      oc.sc = sc;
-      oc.epoch = epoch;
-      oc.g = c->grid;
-      oc.shard = c->shard;
-      oc.nshard = c->nshard;
-      oc.P = power_params(n_bins, alpha);
-      oc.power = power;
-      oc.nuniq = c->nuniq;
-      oc.ukeys = c->ukeys;
-      oc.uamps = c->uamps;
-      oc.tcos = c->tcos;
-      oc.tsin = c->tsin;
-      oc.ev = c->ev;
-      oc.cstart = c->cstart;
-      oc.cend = c->cend;
-      oc.cepoch = c->cepoch;
-      oc.big = c->bigcells;
-      oc.nbig = nbig;
-      hipLaunchKernelGGL(k_owner_cells, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((nown + 63) / 64, 16384))),
-                         dim3(64), 0, s, oc);
-      const unsigned grid_cells = (unsigned)std::max<int64_t>(1, std::min<int64_t>((cov_ncell(c) / c->nshard + 4) / 4, 4096));
-      const TermArrays terms{c->ukeys, c->tcos, c->tsin, c->ev};
-      hipLaunchKernelGGL(k_power, dim3(grid_cells), dim3(256), 0, s, terms, c->cstart, c->cend, c->bigcells, nbig, oc.P,
-                         power);
-      RT_HIP(hipGetLastError());
-      c->ukeys_unsorted = true;
-      prof_mark(c, 7, s);
-      return RT_OK;
-    }
     int64_t* idx_sorted = reinterpret_cast<int64_t*>(c->oamps_sorted);
     // (G lanes per element, one binary search each, then a group sum: no faster on K3's 200k
     // records, 46 -> 76 us on K5's 465k -- the searches' loads, not their latency, set the time)
@@ -4098,16 +3817,8 @@ int rt_coverage_received(rt_coverage* c, uint64_t* keys_out, double* amps_out, i
   }
   *n_out = nu;
   const int64_t m = std::min(nu, max_out);
-  const uint64_t* uk = c->ukeys;
-  const double* ua = c->uamps;
-  if (c->ukeys_unsorted && nu > 1 && (keys_out || amps_out)) {  // the per-cell owner stage: sort on demand
-    size_t tb = c->tmp_bytes;
-    RT_HIP(sort_records(c->tmp, tb, c->ukeys, c->okeys_sorted, c->uamps, c->oamps_sorted, nu, 64, s));
-    uk = c->okeys_sorted;
-    ua = c->oamps_sorted;
-  }
-  if (m > 0 && keys_out) RT_HIP(hipMemcpyAsync(keys_out, uk, m * 8, hipMemcpyDeviceToDevice, s));
-  if (m > 0 && amps_out) RT_HIP(hipMemcpyAsync(amps_out, ua, m * 8, hipMemcpyDeviceToDevice, s));
+  if (m > 0 && keys_out) RT_HIP(hipMemcpyAsync(keys_out, c->ukeys, m * 8, hipMemcpyDeviceToDevice, s));
+  if (m > 0 && amps_out) RT_HIP(hipMemcpyAsync(amps_out, c->uamps, m * 8, hipMemcpyDeviceToDevice, s));
   return RT_OK;
 }
 

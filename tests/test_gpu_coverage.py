@@ -379,18 +379,15 @@ def test_trace_rows_into_small_buffer_fetches_packed(room):
     p.close()
 
 
-@pytest.mark.parametrize("nseg", [1, 3, 8, 9])
-def test_owner_segments_every_sweep_path(room, nseg):
-    """The owner stage on segments (rt_coverage_power_segments: the per-cell path for <= 8 sources,
-    the merge path above that) against the sorted path (rt_coverage_power_records) on the same
-    records: cells of 0 .. 9999 bins (every sweep: thread, wave, range-split), each (cell, bin)'s
-    fixed-point amplitude split over up to nseg source segments, each segment in key order.  Maps
-    and impulse responses bit for bit."""
-    rng = np.random.default_rng(21 + nseg)
-    sizes = [0, 1, 2, 5, 16, 17, 64, 191, 192, 193, 400, 2500, 9999]
+def _owner_segments_case(room, nseg, sizes, seed):
+    """rt_coverage_power_segments on `sizes[c]` random bins per cell c of an nx x 1 x 1 grid, each
+    (cell, bin)'s fixed-point amplitude split over up to 3 of nseg source segments (each segment in
+    key order), against the sorted path (rt_coverage_power_records) on the same records: maps and
+    impulse responses bit for bit."""
+    rng = np.random.default_rng(seed)
     grid = CoverageGrid(0.0, 0.0, 5.0, 1.0, 1.0, 1.0, len(sizes), 1, 1)
     n, win = 10000, 100e-9
-    keys, sums = [], []
+    keys = []
     for c, K in enumerate(sizes):
         for b in np.sort(rng.choice(n, K, replace=False)) if K else []:
             keys.append((c << 32) | int(b))
@@ -429,3 +426,22 @@ def test_owner_segments_every_sweep_path(room, nseg):
     assert np.isfinite(ref).sum() == sum(1 for K in sizes if K)
     for x, y in zip(gi, ri):
         assert x.tobytes() == y.tobytes()
+
+
+@pytest.mark.parametrize("nseg", [1, 3, 8, 9])
+def test_owner_segments_every_sweep_path(room, nseg):
+    """The owner stage on segments (lockstep merge for <= 8 sources, the general merge above that)
+    on cells of 0 .. 9999 bins (every sweep: thread, wave, range-split)."""
+    _owner_segments_case(room, nseg, [0, 1, 2, 5, 16, 17, 64, 191, 192, 193, 400, 2500, 9999], 21 + nseg)
+
+
+@pytest.mark.parametrize("nseg", [2, 8])
+def test_owner_segments_many_cells(room, nseg):
+    """The segment merge on a 1500-cell map of mostly small cells (0-16 bins: thread sweeps), some
+    of 17-200 bins (wave sweeps) and two of 2500 / 3000."""
+    rng = np.random.default_rng(5 + nseg)
+    sizes = [int(x) for x in rng.choice([0, 0, 1, 2, 3, 5, 8, 16], 1500)]
+    for c, K in zip(rng.choice(1500, 40, replace=False), rng.integers(17, 200, 40)):
+        sizes[int(c)] = int(K)
+    sizes[700], sizes[1201] = 2500, 3000
+    _owner_segments_case(room, nseg, sizes, 77 + nseg)

@@ -33,8 +33,6 @@ KERNELS = {  # short name -> substring of the demangled rocprofv3 name
     "k_power": "k_power(",
     "k_power_small": "k_power_small(",
     "k_fill_received": "k_fill_received(",
-    "k_owner_cells": "k_owner_cells(",
-    "k_seg_cells": "k_seg_cells(",
 }
 
 
