@@ -2134,6 +2134,7 @@ struct rt_coverage {
   uint64_t* own_states = nullptr;
   unsigned long long* own_aux = nullptr;
   uint64_t own_tickets = 0, own_tag = 0;
+  uint64_t* send_tails = nullptr;  // k_send_runs' look-back payloads: [2][cap / kOwnTile + 2][5] tagged words
   uint8_t* win = nullptr;
   uint8_t* first_flag = nullptr;
   float* trx = nullptr;
@@ -2558,6 +2559,12 @@ constexpr int kOwnItems = RT_OWN_ITEMS, kOwnTile = 256 * kOwnItems;
 #ifndef RT_OWNER_LOOKBACK
 #define RT_OWNER_LOOKBACK 1
 #endif
+// RT_LOOKBACK_TICKET 1: tiles taken in order from a ticket counter (one same-address atomic per
+// block); 0: tile = block index -- the dispatcher issues workgroups in index order, so every
+// predecessor a block waits on is already resident and makes progress
+#ifndef RT_LOOKBACK_TICKET
+#define RT_LOOKBACK_TICKET 0
+#endif
 constexpr uint64_t kOwnAgg = 1ull << 38, kOwnInc = 2ull << 38, kOwnCount = (1ull << 38) - 1;
 constexpr uint64_t kOwnTagMask = ~(kOwnInc | kOwnAgg | kOwnCount);
 struct OwnerRuns {
@@ -2582,7 +2589,8 @@ __global__ __launch_bounds__(256) void k_owner_runs(OwnerRuns a) {
   __shared__ uint32_t s_tile;
   __shared__ int s_w[4];
   __shared__ int64_t s_prefix;
-  if (threadIdx.x == 0) s_tile = RT_OWNER_LOOKBACK ? (uint32_t)(atomicAdd(a.ticket, 1ull) - a.ticket_base) : blockIdx.x;
+  if (threadIdx.x == 0)
+    s_tile = RT_OWNER_LOOKBACK && RT_LOOKBACK_TICKET ? (uint32_t)(atomicAdd(a.ticket, 1ull) - a.ticket_base) : blockIdx.x;
   if (blockIdx.x == 0 && threadIdx.x == 0) *a.nbig = 0u;  // k_power_small lists the big cells afresh
   __syncthreads();
   const int64_t tile = s_tile;
@@ -2629,31 +2637,43 @@ __global__ __launch_bounds__(256) void k_owner_runs(OwnerRuns a) {
   }
   if (false) {
 #else
-  if (threadIdx.x == 0) {
+  if (w == 0) {  // the look-back, by wave 0: lane L reads the state of tile jbase - L
 #endif
     uint64_t* st = a.states + tile;
-    __hip_atomic_store(st, a.tag | (tile == 0 ? kOwnInc : kOwnAgg) | (uint64_t)total, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0)
+      __hip_atomic_store(st, a.tag | (tile == 0 ? kOwnInc : kOwnAgg) | (uint64_t)total, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
     uint64_t excl = 0;
     if (tile > 0) {
       int spins = 0;
-      for (int64_t j = tile - 1; j >= 0;) {
-        const uint64_t sv = __hip_atomic_load(a.states + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((sv & kOwnTagMask) != a.tag) {  // not published yet
+      for (int64_t jbase = tile - 1;;) {  // windows of 64 predecessors: the nearest inclusive one
+        const int64_t j = jbase - lane;
+        const uint64_t sv = j >= 0 ? __hip_atomic_load(a.states + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+        const bool ready = j < 0 || (sv & kOwnTagMask) == a.tag;
+        const uint64_t incm = __ballot(j >= 0 && ready && (sv & kOwnInc) != 0);
+        const int stop = incm ? __builtin_ctzll(incm) : 63;
+        const uint64_t used = stop == 63 ? ~0ull : ((2ull << stop) - 1);
+        if (__ballot(!ready) & used) {  // a tile up to the inclusive one has not published yet
           if (++spins > (1 << 22)) {
-            atomicAdd(a.errors, 1u);
+            if (lane == 0) atomicAdd(a.errors, 1u);
             break;
           }
           continue;
         }
-        excl += sv & kOwnCount;
-        if (sv & kOwnInc) break;
-        --j;
+        uint64_t cnt = (j >= 0 && lane <= stop) ? (sv & kOwnCount) : 0ull;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+        excl += cnt;
+        if (incm || jbase < 64) break;  // tile 0 always publishes an inclusive state
+        jbase -= 64;
       }
-      __hip_atomic_store(st, a.tag | kOwnInc | (excl + (uint64_t)total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0)
+        __hip_atomic_store(st, a.tag | kOwnInc | (excl + (uint64_t)total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    s_prefix = (int64_t)excl;
-    if (i0 + kOwnTile >= a.n) *a.nuniq = (int64_t)excl + total;  // the last tile
+    if (lane == 0) {
+      s_prefix = (int64_t)excl;
+      if (i0 + kOwnTile >= a.n) *a.nuniq = (int64_t)excl + total;  // the last tile
+    }
   }
   __syncthreads();
   int64_t u = s_prefix + before + x - c;  // unique index of this thread's first head
@@ -2695,6 +2715,254 @@ __global__ __launch_bounds__(256) void k_owner_runs(OwnerRuns a) {
   }
 }
 
+// ---- Trace-stage reduce in one launch (RT_SEND_FUSED): the sorted replay records of a ray-sharded
+// rank -> its unique (owner, cell, bin) keys with their exact sums, the send rows and the owner
+// bounds.  Tiles of kSendTile records in ticket order; each thread holds 4 consecutive records.  A
+// run of equal keys may be any length (a K3 rank's transmitter cell: ~125k records in one bin), so
+// the sums are a segmented scan: per tile its head count and its segmented tail (the sum after its
+// last head, or of the whole tile if it has none), combined across tiles by decoupled look-back --
+// the state word carries the call's tag, the head bit and the count; the Fx192 tails sit beside it
+// as five words of 40 bits, each carrying the tag too, so every word validates itself and no fence
+// orders them (an agent-scope release / acquire pair per tile -- L2 write-back and invalidate across
+// the XCDs -- made the kernel 0.28-0.32 ms, profiles/r4i_sendruns_fenced_k3_rank_timeline.txt).
+// Every run is written by its last
+// record: key, exact sum, f64, its row (packed 32 B or key + sum) and, at owner changes, the bounds.
+// Replaces k_tile_heads, k_tile_sums, k_cross_tiles and k_bounds_strip (four launches, ~50 us per
+// rank of 8, profiles/r4h_k5.timeline.txt).  Integer sums: the same bits in any grouping.
+#ifndef RT_SEND_FUSED
+#define RT_SEND_FUSED 1
+#endif
+constexpr int kSendItems = 4, kSendTile = 256 * kSendItems;
+static_assert(kSendTile == kOwnTile, "k_send_runs shares k_owner_runs' tile states");
+constexpr uint64_t kSendHead = 1ull << 37, kSendCount = (1ull << 37) - 1;
+struct SegFx {  // segmented sum of a stretch of records: h = it holds a head, t = the sum after its last head
+  bool h;
+  Fx192 t;
+};
+__device__ __forceinline__ SegFx seg_op(const SegFx& a, const SegFx& b) {  // a, then b
+  return SegFx{a.h || b.h, b.h ? b.t : FxPlus()(a.t, b.t)};
+}
+__device__ __forceinline__ SegFx shfl_up_seg(const SegFx& x, int o) {
+  return SegFx{__shfl_up(x.h ? 1 : 0, o, 64) != 0, shfl_up_fx(x.t, o)};
+}
+// an Fx192 as five tagged words (tag24 << 40 | 40 payload bits), stored and loaded one by one
+__device__ __forceinline__ void put_tail(uint64_t* q, const Fx192& t, uint64_t tag24) {
+  const uint64_t M = (1ull << 40) - 1, tg = tag24 << 40;
+  const uint64_t c[5] = {t.w0 & M, (t.w0 >> 40 | t.w1 << 24) & M, (t.w1 >> 16) & M, (t.w1 >> 56 | t.w2 << 8) & M,
+                         t.w2 >> 32};
+#pragma unroll
+  for (int i = 0; i < 5; ++i) __hip_atomic_store(q + i, tg | c[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+struct SendRuns {
+  const uint64_t* keys;  // sorted compact record keys [n], dropped records (~0) last
+  const double* amps;
+  int64_t n;
+  uint64_t* states;
+  uint64_t *agg_tail, *inc_tail;  // [tiles][5] tagged words
+  unsigned long long* ticket;
+  uint64_t ticket_base, tag;
+  unsigned* errors;
+  WideKey wk;
+  int world, own_shift;
+  uint64_t* ukeys;
+  Fx192* usums;
+  double* uamps;
+  int64_t* nuniq;
+  int64_t* bounds;
+  uint64_t* out;     // packed: 32-B rows; else keys (owner stripped), sums in sums_out
+  Fx192* sums_out;
+  int packed;
+  int64_t cap;       // rows the caller's buffers hold
+};
+__global__ __launch_bounds__(256) void k_send_runs(SendRuns a) {
+  __shared__ uint32_t s_tile;
+  __shared__ int s_wc[4];
+  __shared__ SegFx s_ws[4];
+  __shared__ int64_t s_prefix;
+  __shared__ Fx192 s_carry;
+  if (threadIdx.x == 0) s_tile = RT_LOOKBACK_TICKET ? (uint32_t)(atomicAdd(a.ticket, 1ull) - a.ticket_base) : blockIdx.x;
+  __syncthreads();
+  const int64_t tile = s_tile;
+  const int64_t i0 = tile * kSendTile + (int64_t)threadIdx.x * kSendItems;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const Fx192 zero{0, 0, 0};
+  uint64_t k[kSendItems];
+  Fx192 v[kSendItems];
+  bool head[kSendItems];
+  const uint64_t key_before = i0 > 0 && i0 - 1 < a.n ? a.keys[i0 - 1] : ~0ull;
+  const uint64_t key_after = i0 + kSendItems < a.n ? a.keys[i0 + kSendItems] : ~0ull;
+  uint64_t prev = key_before;
+  int c = 0;
+  SegFx th{false, zero};
+#pragma unroll
+  for (int j = 0; j < kSendItems; ++j) {
+    const int64_t i = i0 + j;
+    k[j] = i < a.n ? a.keys[i] : ~0ull;
+    head[j] = i < a.n && (i == 0 || k[j] != prev);
+    prev = k[j];
+    v[j] = i < a.n ? fx_from_double(a.amps[i]) : zero;
+    c += head[j] ? 1 : 0;
+    th = seg_op(th, SegFx{head[j], v[j]});
+  }
+  // inclusive wave scans of the head counts and of the segmented sums
+  int x = c;
+  SegFx sx = th;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    const SegFx sy = shfl_up_seg(sx, o);
+    if (lane >= o) {
+      x += y;
+      sx = seg_op(sy, sx);
+    }
+  }
+  if (lane == 63) {
+    s_wc[w] = x;
+    s_ws[w] = sx;
+  }
+  SegFx lx = shfl_up_seg(sx, 1);  // the lanes before this one
+  if (lane == 0) lx = SegFx{false, zero};
+  __syncthreads();
+  int before = x - c;
+  SegFx pre{false, zero};
+  for (int q = 0; q < w; ++q) {
+    before += s_wc[q];
+    pre = seg_op(pre, s_ws[q]);
+  }
+  pre = seg_op(pre, lx);  // this tile's records before this thread
+  if (w == 0) {  // the look-back, by wave 0: one round trip per predecessor tile
+    const int total = s_wc[0] + s_wc[1] + s_wc[2] + s_wc[3];
+    SegFx T = s_ws[0];
+    for (int q = 1; q < 4; ++q) T = seg_op(T, s_ws[q]);
+    uint64_t* st = a.states + tile;
+    const uint64_t hb = T.h ? kSendHead : 0ull, tag24 = a.tag >> 40;
+    if (lane == 0) {
+      if (tile == 0) {
+        put_tail(a.inc_tail, T.t, tag24);
+        __hip_atomic_store(st, a.tag | kOwnInc | hb | (uint64_t)total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        put_tail(a.agg_tail + 5 * tile, T.t, tag24);
+        __hip_atomic_store(st, a.tag | kOwnAgg | hb | (uint64_t)total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    uint64_t excl = 0;
+    SegFx carry{false, zero};  // the tiles before this one, segmented
+    if (tile > 0) {
+      // windows of 64 predecessors, lane L reading tile jbase - L (state word and both tails): the
+      // nearest inclusive tile and the aggregates after it in one round trip
+      const uint64_t M40 = (1ull << 40) - 1;
+      int spins = 0;
+      for (int64_t jbase = tile - 1;;) {
+        const int64_t j = jbase - lane;
+        bool ready = true, inc = false;
+        SegFx x{false, zero};
+        uint64_t cnt = 0;
+        if (j >= 0) {
+          const uint64_t sv = __hip_atomic_load(a.states + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          uint64_t wa[5], wi[5];
+#pragma unroll
+          for (int i = 0; i < 5; ++i) {
+            wa[i] = __hip_atomic_load(a.agg_tail + 5 * j + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            wi[i] = __hip_atomic_load(a.inc_tail + 5 * j + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          inc = (sv & kOwnInc) != 0;
+          ready = (sv & kOwnTagMask) == a.tag;
+          const uint64_t* wq = inc ? wi : wa;
+#pragma unroll
+          for (int i = 0; i < 5; ++i) ready = ready && (wq[i] >> 40) == tag24;
+          inc = inc && ready;
+          uint64_t c5[5];
+#pragma unroll
+          for (int i = 0; i < 5; ++i) c5[i] = wq[i] & M40;
+          x = SegFx{inc || (sv & kSendHead) != 0,
+                    Fx192{c5[0] | c5[1] << 40, c5[1] >> 24 | c5[2] << 16 | c5[3] << 56, c5[3] >> 8 | c5[4] << 32}};
+          cnt = sv & kSendCount;
+        }
+        const uint64_t incm = __ballot(j >= 0 && inc);
+        const int stop = incm ? __builtin_ctzll(incm) : 63;  // the lanes 0 .. stop are combined
+        const uint64_t used = stop == 63 ? ~0ull : ((2ull << stop) - 1);
+        if (__ballot(j >= 0 && !ready) & used) {  // a tile in the window has not published yet
+          if (++spins > (1 << 22)) {
+            if (lane == 0) atomicAdd(a.errors, 1u);
+            break;
+          }
+          continue;
+        }
+        if (lane > stop || j < 0) {
+          x = SegFx{false, zero};
+          cnt = 0;
+        }
+        // older tiles (higher lanes) first: lane i takes lane i + o's stretch as the one before its own
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const SegFx y{__shfl_down(x.h ? 1 : 0, o, 64) != 0,
+                        Fx192{__shfl_down(x.t.w0, o, 64), __shfl_down(x.t.w1, o, 64), __shfl_down(x.t.w2, o, 64)}};
+          const uint64_t cy = __shfl_down(cnt, o, 64);
+          if (lane + o < 64) {
+            x = seg_op(y, x);
+            cnt += cy;
+          }
+        }
+        const SegFx W{__shfl(x.h ? 1 : 0, 0, 64) != 0, shfl_fx(x.t, 0)};
+        excl += __shfl(cnt, 0, 64);
+        carry = seg_op(W, carry);
+        if (incm || jbase < 64) break;  // an inclusive tile reached (tile 0 always publishes one)
+        jbase -= 64;
+      }
+      if (lane == 0) {
+        put_tail(a.inc_tail + 5 * tile, seg_op(carry, T).t, tag24);
+        __hip_atomic_store(st, a.tag | kOwnInc | hb | (excl + (uint64_t)total), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (lane == 0) {
+      s_prefix = (int64_t)excl;
+      s_carry = carry.t;
+      if (tile * kSendTile + kSendTile >= a.n) *a.nuniq = (int64_t)excl + total;  // the last tile
+    }
+  }
+  __syncthreads();
+  int64_t u = s_prefix + before - 1;               // the run open before this thread's first record
+  Fx192 acc = seg_op(SegFx{true, s_carry}, pre).t;  // its sum so far
+  const uint64_t mask = (1ull << a.own_shift) - 1;
+#pragma unroll
+  for (int j = 0; j < kSendItems; ++j) {
+    const int64_t i = i0 + j;
+    if (i >= a.n) break;
+    if (head[j]) {
+      ++u;
+      acc = v[j];
+      const uint64_t kp = j ? k[j - 1] : key_before;
+      const int lo = i == 0 ? -1 : (kp == ~0ull ? a.world : (int)(a.wk(kp) >> a.own_shift));
+      const int hi = k[j] == ~0ull ? a.world : (int)(a.wk(k[j]) >> a.own_shift);
+      for (int o = lo + 1; o <= hi; ++o) a.bounds[o] = u;  // owners lo+1 .. hi start at u
+    } else {
+      acc = FxPlus()(acc, v[j]);
+    }
+    const uint64_t next = j + 1 < kSendItems ? k[j + 1] : key_after;
+    if (i + 1 < a.n && next == k[j]) continue;  // the run goes on
+    const uint64_t wkey = a.wk(k[j]);
+    a.ukeys[u] = wkey;
+    a.usums[u] = acc;
+    a.uamps[u] = fx_to_double(acc);
+    if (a.out && k[j] != ~0ull && u < a.cap) {
+      if (a.packed) {
+        typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+        u64x2* row = reinterpret_cast<u64x2*>(a.out + 4 * u);  // 32-B rows: two 16-B stores
+        row[0] = u64x2{wkey & mask, acc.w0};
+        row[1] = u64x2{acc.w1, acc.w2};
+      } else {
+        a.out[u] = wkey & mask;
+        a.sums_out[u] = acc;
+      }
+    }
+    if (i + 1 == a.n) {  // the owners after the last record's start at the end
+      const int hi = k[j] == ~0ull ? a.world : (int)(wkey >> a.own_shift);
+      for (int o = hi + 1; o <= a.world; ++o) a.bounds[o] = u + 1;
+    }
+  }
+}
+
 hipError_t scan_flags(void* tmp, size_t& bytes, const int32_t* flags, int32_t* scan, int64_t n, hipStream_t s) {
   return rocprim::inclusive_scan(tmp, bytes, flags, scan, (size_t)n, rocprim::plus<int32_t>(), s);
 }
@@ -2730,6 +2998,8 @@ void free_cands(rt_coverage* c) {
   c->runs = nullptr;
   if (c->own_states) (void)hipFree(c->own_states);
   c->own_states = nullptr;
+  if (c->send_tails) (void)hipFree(c->send_tails);
+  c->send_tails = nullptr;
   c->tmp = nullptr;
   c->tmp_bytes = 0;
   c->rord = nullptr;
@@ -2796,6 +3066,8 @@ int alloc_cands(rt_coverage* c, int64_t cap) {
   // k_owner_runs' states: zero = no tag (tags start at 1 << 40)
   RT_HIP(hipMalloc(&c->own_states, ((size_t)cap / kOwnTile + 2) * 8));
   RT_HIP(hipMemset(c->own_states, 0, ((size_t)cap / kOwnTile + 2) * 8));
+  RT_HIP(hipMalloc(&c->send_tails, ((size_t)cap / kOwnTile + 2) * 2 * 5 * 8));
+  RT_HIP(hipMemset(c->send_tails, 0, ((size_t)cap / kOwnTile + 2) * 2 * 5 * 8));  // tag 0: never a call's
   size_t b1 = 0, b2 = 0, b3 = 0;
   RT_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, b1, c->keys, c->keys_sorted, (int)cap, 0, 64));
   size_t b2m = 0;  // both sort_records paths: Onesweep at cap, the merge sort below its threshold
@@ -3536,12 +3808,45 @@ int trace_records_impl(rt_coverage* c, const float* tx_pos, double tx_power, dou
   prof_mark(c, 6, s);
   if (nlist > 0) {
     const KeyBits kb = key_bits(c, n_bins);
-    rc = cov_reduce(c, c->okeys, c->oamps, nlist, record_sort_bits(c, kb, n_bins), wide_key(c, kb), s);
-    if (rc) return rc;
     // the send buffers are filled before the host synchronizes (no launch after it)
-    hipLaunchKernelGGL(k_bounds_strip, dim3((unsigned)std::min<int64_t>((nlist + 256) / 256, 4096)), dim3(256), 0, s,
-                       c->ukeys, plan_sums(c), c->nuniq, world, keys_out ? max_out : 0, own_shift(c), c->bounds,
-                       keys_out, (Fx192*)sums_out, packed ? 1 : 0);
+    if (RT_SEND_FUSED) {
+      if ((rc = grow_for(c, nlist))) return rc;
+      size_t tb = c->tmp_bytes;
+      const int sb = record_sort_bits(c, kb, n_bins);
+      RT_HIP(sort_records(c->tmp, tb, c->okeys, c->okeys_sorted, c->oamps, c->oamps_sorted, nlist, sb < 64 ? sb : 64, s));
+      SendRuns a{};
+      a.keys = c->okeys_sorted;
+      a.amps = c->oamps_sorted;
+      a.n = nlist;
+      a.states = c->own_states;
+      const int64_t ntiles = (nlist + kSendTile - 1) / kSendTile;
+      a.agg_tail = c->send_tails;
+      a.inc_tail = a.agg_tail + 5 * (c->cap / kOwnTile + 2);
+      a.ticket = c->own_aux;
+      a.errors = reinterpret_cast<unsigned*>(c->own_aux + 1);
+      a.ticket_base = c->own_tickets;
+      c->own_tickets += (uint64_t)ntiles;
+      a.tag = (c->own_tag++ % 0xFFFFFEull + 1ull) << 40;
+      a.wk = wide_key(c, kb);
+      a.world = world;
+      a.own_shift = own_shift(c);
+      a.ukeys = c->ukeys;
+      a.usums = plan_sums(c);
+      a.uamps = c->uamps;
+      a.nuniq = c->nuniq;
+      a.bounds = c->bounds;
+      a.out = keys_out;
+      a.sums_out = (Fx192*)sums_out;
+      a.packed = packed ? 1 : 0;
+      a.cap = keys_out ? max_out : 0;
+      hipLaunchKernelGGL(k_send_runs, dim3((unsigned)ntiles), dim3(256), 0, s, a);
+    } else {
+      rc = cov_reduce(c, c->okeys, c->oamps, nlist, record_sort_bits(c, kb, n_bins), wide_key(c, kb), s);
+      if (rc) return rc;
+      hipLaunchKernelGGL(k_bounds_strip, dim3((unsigned)std::min<int64_t>((nlist + 256) / 256, 4096)), dim3(256), 0,
+                         s, c->ukeys, plan_sums(c), c->nuniq, world, keys_out ? max_out : 0, own_shift(c), c->bounds,
+                         keys_out, (Fx192*)sums_out, packed ? 1 : 0);
+    }
     RT_HIP(hipGetLastError());
     prof_mark(c, 7, s);
     RT_HIP(hipMemcpyAsync(b.data(), c->bounds, sizeof(int64_t) * (world + 1), hipMemcpyDeviceToHost, s));
