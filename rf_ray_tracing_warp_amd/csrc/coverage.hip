@@ -1621,85 +1621,6 @@ __global__ __launch_bounds__(256) void k_merge_lockstep(const uint64_t* keys, in
   }
 }
 
-// RT_MERGE_SAMPLED: the lockstep merge with its searches started from a sample of every segment
-// (every S-th key, S a power of two) that each block stages in LDS: the search over the samples runs
-// in LDS, and only the last log2(S) halvings -- inside one S-key window -- load from global memory
-// (a full search over a K5 owner's ~58k-record segments took 16-17 dependent global loads).
-#ifndef RT_MERGE_SAMPLED
-#define RT_MERGE_SAMPLED 1
-#endif
-constexpr int kMergeSampCap = 4096;  // samples per block (32 KB of LDS)
-template <int NS>
-__global__ __launch_bounds__(256) void k_merge_sampled(const uint64_t* keys, int64_t kstride, SegOffsets so,
-                                                       int sshift, uint64_t* keys_out, int64_t* idx_out) {
-  __shared__ uint64_t s_samp[kMergeSampCap];
-  __shared__ int s_base[NS + 1];
-  const int64_t n = so.off[so.nseg];
-  const int64_t S = (int64_t)1 << sshift;
-  if (threadIdx.x == 0) {
-    int b = 0;
-    for (int t = 0; t < NS; ++t) {
-      s_base[t] = b;
-      b += t < so.nseg ? (int)((so.off[t + 1] - so.off[t] + S - 1) >> sshift) : 0;
-    }
-    s_base[NS] = b;
-  }
-  __syncthreads();
-  for (int q = threadIdx.x; q < s_base[NS]; q += blockDim.x) {
-    int t = 0;
-    while (t + 1 < NS && s_base[t + 1] <= q) ++t;
-    s_samp[q] = keys[(so.off[t] + ((int64_t)(q - s_base[t]) << sshift)) * kstride];
-  }
-  __syncthreads();
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    int sg = 0;
-    while (sg + 1 < so.nseg && so.off[sg + 1] <= i) ++sg;
-    const uint64_t k = keys[i * kstride];
-    int64_t a[NS], len[NS];
-#pragma unroll
-    for (int t = 0; t < NS; ++t) {  // the window of segment t that holds the boundary
-      a[t] = 0;
-      len[t] = 0;
-      if (t < so.nseg && t != sg) {
-        int lo = s_base[t], hi = s_base[t + 1];
-        while (lo < hi) {  // samples before the boundary: keys <= k (t < sg) or < k (t > sg)
-          const int mid = (lo + hi) >> 1;
-          const uint64_t x = s_samp[mid];
-          if (x < k || (t < sg && x == k)) lo = mid + 1;
-          else hi = mid;
-        }
-        const int64_t c = lo - s_base[t], seglen = so.off[t + 1] - so.off[t];
-        const int64_t w0 = c == 0 ? 0 : ((c - 1) << sshift) + 1, w1 = (c << sshift) < seglen ? (c << sshift) : seglen;
-        a[t] = so.off[t] + w0;
-        len[t] = w1 > w0 ? w1 - w0 : 0;
-      }
-    }
-    for (int st = 0; st < sshift; ++st) {
-      uint64_t km[NS];
-#pragma unroll
-      for (int t = 0; t < NS; ++t) {  // every segment's probe first: independent loads
-        const int64_t m = a[t] + (len[t] >> 1);
-        km[t] = keys[(len[t] > 0 ? m : i) * kstride];
-      }
-#pragma unroll
-      for (int t = 0; t < NS; ++t) {
-        if (len[t] > 0) {
-          const int64_t half = len[t] >> 1;
-          const bool right = km[t] < k || (t < sg && km[t] == k);
-          a[t] = right ? a[t] + half + 1 : a[t];
-          len[t] = right ? len[t] - half - 1 : half;
-        }
-      }
-    }
-    int64_t pos = i - so.off[sg];
-#pragma unroll
-    for (int t = 0; t < NS; ++t)
-      if (t < so.nseg && t != sg) pos += a[t] - so.off[t];
-    keys_out[pos] = k;
-    idx_out[pos] = i;
-  }
-}
-
 // ------------------------------------------------------------------ 5. closed-form signal power
 // sin and cos of 2*pi*turns, reduced in turns (|2*pi*frac| <= pi keeps ocml on its short path;
 // the arguments here reach thousands of radians, where the general reduction is slow)
@@ -2238,6 +2159,7 @@ struct rt_coverage {
   bool profile = false;
   hipEvent_t pev[8] = {};
   unsigned long long* hcnt = nullptr;  // pinned copy of counters[0..2] (the candidate stage's read-back)
+  int64_t* hbounds = nullptr;          // pinned (ray mode): the trace stage's owner bounds [world + 1], then the look-back error count
   hipEvent_t ev_cnt = nullptr;         // recorded after that copy
   bool ev_rec[8] = {};
   unsigned long long* work = nullptr;
@@ -3756,6 +3678,7 @@ int rt_coverage_destroy(rt_coverage* c) {
     if (e) (void)hipEventDestroy(e);
   if (c->ev_cnt) (void)hipEventDestroy(c->ev_cnt);
   if (c->hcnt) (void)hipHostFree(c->hcnt);
+  if (c->hbounds) (void)hipHostFree(c->hbounds);
   delete c;
   return RT_OK;
 }
@@ -3812,7 +3735,8 @@ int rt_coverage_create_rays(int device, const rt_mesh* env, int max_bounces, int
   if (rc) return rc;
   c->n_total = n_rays_total;
   c->ray_mode = true;
-  if (hipMalloc(&c->bounds, sizeof(int64_t) * (world + 1)) != hipSuccess) {
+  if (hipMalloc(&c->bounds, sizeof(int64_t) * (world + 1)) != hipSuccess ||
+      hipHostMalloc((void**)&c->hbounds, sizeof(int64_t) * (world + 2), hipHostMallocDefault) != hipSuccess) {
     rt_coverage_destroy(c);
     return rt::hip_fail(hipErrorOutOfMemory, "rt_coverage_create_rays");
   }
@@ -3928,12 +3852,14 @@ int trace_records_impl(rt_coverage* c, const float* tx_pos, double tx_power, dou
     }
     RT_HIP(hipGetLastError());
     prof_mark(c, 7, s);
-    RT_HIP(hipMemcpyAsync(b.data(), c->bounds, sizeof(int64_t) * (world + 1), hipMemcpyDeviceToHost, s));
-    // look-back waits that gave up (k_send_runs here, k_owner_runs of an earlier owner stage):
-    // their sums would be wrong, so the run fails instead
-    RT_HIP(hipMemcpyAsync(c->hcnt + 3, c->own_aux + 1, 8, hipMemcpyDeviceToHost, s));
+    // both into pinned memory (a pageable copy stages through the host: ~20 us of gap per rank),
+    // the bounds and the count of look-back waits that gave up (k_send_runs here, k_owner_runs of
+    // an earlier owner stage): their sums would be wrong, so the run fails instead
+    RT_HIP(hipMemcpyAsync(c->hbounds, c->bounds, sizeof(int64_t) * (world + 1), hipMemcpyDeviceToHost, s));
+    RT_HIP(hipMemcpyAsync(c->hbounds + world + 1, c->own_aux + 1, 8, hipMemcpyDeviceToHost, s));
     RT_HIP(hipStreamSynchronize(s));
-    if (c->hcnt[3] & 0xFFFFFFFFull) {
+    for (int o = 0; o <= world; ++o) b[o] = c->hbounds[o];
+    if (c->hbounds[world + 1] & 0xFFFFFFFFll) {
       RT_HIP(hipMemset(c->own_aux + 1, 0, 8));
       rt::set_error("rt_coverage_trace_records: a look-back wait timed out (results discarded)");
       return RT_EHIP;
@@ -4088,11 +4014,7 @@ int power_segments_impl(rt_coverage* c, const uint64_t* keys, const uint64_t* su
     for (int t = 0; t < nseg; ++t) longest = std::max<int64_t>(longest, seg_counts[t]);
     const int steps = bits_for((uint64_t)longest);  // a search over len keys takes <= bits(len) halvings
     const dim3 gm((unsigned)std::min<int64_t>((n + 255) / 256, 8192));
-    int sshift = 6;  // samples every 2^sshift keys, as many as a block's LDS holds
-    while (sshift < 20 && (n >> sshift) + nseg > kMergeSampCap) ++sshift;
-    if (RT_MERGE_SAMPLED && nseg <= 8 && sshift < steps)
-      hipLaunchKernelGGL(k_merge_sampled<8>, gm, dim3(256), 0, s, keys, stride, so, sshift, c->okeys_sorted, idx_sorted);
-    else if (RT_MERGE_LOCKSTEP && nseg <= 2)
+    if (RT_MERGE_LOCKSTEP && nseg <= 2)
       hipLaunchKernelGGL(k_merge_lockstep<2>, gm, dim3(256), 0, s, keys, stride, so, steps, c->okeys_sorted, idx_sorted);
     else if (RT_MERGE_LOCKSTEP && nseg <= 4)
       hipLaunchKernelGGL(k_merge_lockstep<4>, gm, dim3(256), 0, s, keys, stride, so, steps, c->okeys_sorted, idx_sorted);
