@@ -1467,9 +1467,16 @@ constexpr int64_t kReplayWindowMax = RT_REPLAY_WINDOW_MAX;
 #ifndef RT_REPLAY_EARLY
 #define RT_REPLAY_EARLY 1
 #endif
+// RT_REPLAY_ORDER_IDX: the window order writes the processing order (4-B item indices) and the
+// replay gathers its items through it, inside the window just read (L2-resident); 0: the order
+// kernel copies the 16-B items themselves (K3 rank: order 19 -> 37 us, replay 266 -> 258 us)
+#ifndef RT_REPLAY_ORDER_IDX
+#define RT_REPLAY_ORDER_IDX 1
+#endif
 template <bool USE_BVH>
 __global__ __launch_bounds__(1024) void k_replay_order(CovParams p, const ReplayItem* items, int64_t nl,
-                                                       const unsigned long long* nl_dev, ReplayItem* sorted) {
+                                                       const unsigned long long* nl_dev, ReplayItem* sorted,
+                                                       int32_t* order) {
   using Sort = rocprim::block_radix_sort<uint16_t, 1024, RT_REPLAY_WIN_ITEMS, int32_t>;
   __shared__ typename Sort::storage_type st;
   if (nl_dev) nl = min(nl, (int64_t)*nl_dev);  // launched before the host knows the list length
@@ -1485,8 +1492,11 @@ __global__ __launch_bounds__(1024) void k_replay_order(CovParams p, const Replay
   }
   Sort().sort(k, v, st);
 #pragma unroll
-  for (int i = 0; i < RT_REPLAY_WIN_ITEMS; ++i)  // the window's items, just read: L2-resident
-    if (base + i < nl) sorted[base + i] = items[v[i]];
+  for (int i = 0; i < RT_REPLAY_WIN_ITEMS; ++i) {  // the window's items, just read: L2-resident
+    if (base + i >= nl) continue;
+    if (order) order[base + i] = v[i];
+    else sorted[base + i] = items[v[i]];
+  }
 }
 
 template <bool USE_BVH, bool RX_FIRST>
@@ -3361,14 +3371,15 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
     uint16_t* k_out = (uint16_t*)((char*)ws + kbs);
     int32_t* v_in = (int32_t*)((char*)ws + 2 * kbs);
     int32_t* v_out = (int32_t*)((char*)ws + 2 * kbs + rbs);
+    int32_t* worder = RT_REPLAY_ORDER_IDX ? v_out : nullptr;
     if (windows) {
       const unsigned grid_w = (unsigned)((nl + kReplayWin - 1) / kReplayWin);
       if (bvh)
         hipLaunchKernelGGL(k_replay_order<true>, dim3(grid_w), dim3(1024), 0, s, p, c->ritems, nl, nl_dev,
-                           c->ritems_sorted);
+                           c->ritems_sorted, worder);
       else
         hipLaunchKernelGGL(k_replay_order<false>, dim3(grid_w), dim3(1024), 0, s, p, c->ritems, nl, nl_dev,
-                           c->ritems_sorted);
+                           c->ritems_sorted, worder);
     } else {
       if (bvh)
         hipLaunchKernelGGL(k_replay_keys<true>, dim3(grid_l), dim3(256), 0, s, p, c->ritems, nl, k_in, v_in);
@@ -3379,8 +3390,8 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
     }
     prof_mark(c, 4, s);
     // the window order wrote the items in processing order; the device-wide sort gives an order
-    const ReplayItem* rit = windows ? c->ritems_sorted : c->ritems;
-    const int32_t* rord = windows ? nullptr : v_out;
+    const ReplayItem* rit = windows && !worder ? c->ritems_sorted : c->ritems;
+    const int32_t* rord = windows ? worder : v_out;
     // BVH scenes: receiver first, the traversal culled at its t (K5 replay 3.47 -> 2.7 ms); the
     // LDS brute force tests every face anyway (a plane-culled variant measured 5% slower on K3,
     // a receiver-first one skipping faces beyond the receiver's t 5% slower too: 2.50 vs 2.63 ms,
