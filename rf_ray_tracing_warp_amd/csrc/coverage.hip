@@ -3263,6 +3263,10 @@ WideKey wide_key(const rt_coverage* c, const KeyBits& k, bool owner_local = true
 
 // Stages 1-4 (trajectories, candidates, exact receiver tests, replay): the first-win records of
 // this plan's rays as (compact record key, amplitude) in c->okeys / c->oamps, in candidate order.
+// RT_COV_ZBAND: the plan's ray order puts the most nearly horizontal rays first (dir_order_banded)
+#ifndef RT_COV_ZBAND
+#define RT_COV_ZBAND 0
+#endif
 int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double light_speed, double sample_rate,
                 int flags, int64_t n_bins, hipStream_t s, int64_t* ncand_out, int64_t* nlist_out) {
   CovParams p{};
@@ -3314,7 +3318,8 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
     // plan, sorts per call).  K5: ~0.1 ms per one-GPU map, a fixed ~30 us per rank of 8.
     if (!c->ray_order) {
       void* ws = nullptr;
-      const int32_t* o = rt::dir_order(c->ray_offset, c->n, s, &ws);
+      const int32_t* o = RT_COV_ZBAND ? rt::dir_order_banded(c->ray_offset, c->n, s, &ws)
+                                      : rt::dir_order(c->ray_offset, c->n, s, &ws);
       if (!o) return RT_EHIP;
       RT_HIP(hipMalloc(&c->ray_order, sizeof(int32_t) * (size_t)c->n));
       RT_HIP(hipMemcpyAsync(c->ray_order, o, sizeof(int32_t) * (size_t)c->n, hipMemcpyDeviceToDevice, s));

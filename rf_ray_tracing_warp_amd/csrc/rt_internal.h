@@ -68,6 +68,7 @@ void keep_pool_memory();
 // Row order for tracing rays [ray_offset, ray_offset+n) of one burst sorted by initial direction
 // (trace.hip).  Stream-ordered workspace returned in *ws (hipFreeAsync it after the consumer).
 const int32_t* dir_order(int64_t ray_offset, int64_t n, hipStream_t stream, void** ws);
+const int32_t* dir_order_banded(int64_t ray_offset, int64_t n, hipStream_t stream, void** ws);
 // Device view of a mesh's BVH for rt::bvh_query
 inline BvhView bvh_view(const rt_mesh* m) {
   return BvhView{(const float4*)m->nodes, (const int2*)m->leaves, (const float4*)m->lcomp, (int)m->nf,

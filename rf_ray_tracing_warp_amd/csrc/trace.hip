@@ -1054,6 +1054,18 @@ __device__ __forceinline__ uint16_t dir_cell(int64_t gid) {
   for (int b = 0; b < 8; ++b) k |= ((cx >> b) & 1u) << (2 * b) | ((cy >> b) & 1u) << (2 * b + 1);
   return (uint16_t)k;
 }
+// Coverage plans (dir_order_banded): the direction cell under a band of |d.z| (8 bands, the most
+// nearly horizontal first).  A terrain's grazing rays walk the longest BVH chains; issued first,
+// their waves run beside the short ones instead of after them (a rank's trajectory pass is two
+// rounds of the GPU's wave slots).  Only the processing order changes.
+__global__ __launch_bounds__(256) void k_dir_keys_banded(int64_t ray_offset, int64_t n, uint32_t* keys, int32_t* rows) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float3 d = rt::ray_dir(ray_offset + i);
+  const uint32_t band = (uint32_t)fminf(fabsf(d.z) * 8.0f, 7.0f);
+  keys[i] = band << 16 | dir_cell(ray_offset + i);
+  rows[i] = (int32_t)i;
+}
 __global__ __launch_bounds__(256) void k_dir_keys(int64_t ray_offset, int64_t n, uint16_t* keys, int32_t* rows) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -1136,6 +1148,38 @@ const int32_t* dir_order(int64_t ray_offset, int64_t n, hipStream_t stream, void
   e = hipcub::DeviceRadixSort::SortPairs(tmp, cub_bytes, k_in, k_out, r_in, r_out, (int)n, 0, 16, stream);
   if (e != hipSuccess) {
     hip_fail(e, "dir_order sort");
+    return nullptr;
+  }
+  return r_out;
+}
+
+// dir_order with the |d.z| bands first (k_dir_keys_banded); nullptr on failure
+const int32_t* dir_order_banded(int64_t ray_offset, int64_t n, hipStream_t stream, void** ws) {
+  size_t cub_bytes = 0;
+  *ws = nullptr;
+  keep_pool_memory();
+  if (hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                         (int32_t*)nullptr, (int32_t*)nullptr, (int)n, 0, 19, stream) != hipSuccess) {
+    set_error("dir_order_banded: hipcub sizing failed");
+    return nullptr;
+  }
+  const size_t kb = ((size_t)n * 4 + 255) / 256 * 256;
+  hipError_t e = hipMallocAsync(ws, 4 * kb + cub_bytes, stream);
+  if (e != hipSuccess) {
+    hip_fail(e, "dir_order_banded workspace");
+    *ws = nullptr;
+    return nullptr;
+  }
+  uint32_t* k_in = (uint32_t*)*ws;
+  uint32_t* k_out = (uint32_t*)((char*)*ws + kb);
+  int32_t* r_in = (int32_t*)((char*)*ws + 2 * kb);
+  int32_t* r_out = (int32_t*)((char*)*ws + 3 * kb);
+  void* tmp = (char*)*ws + 4 * kb;
+  hipLaunchKernelGGL(k_dir_keys_banded, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, ray_offset, n, k_in,
+                     r_in);
+  e = hipcub::DeviceRadixSort::SortPairs(tmp, cub_bytes, k_in, k_out, r_in, r_out, (int)n, 0, 19, stream);
+  if (e != hipSuccess) {
+    hip_fail(e, "dir_order_banded sort");
     return nullptr;
   }
   return r_out;
