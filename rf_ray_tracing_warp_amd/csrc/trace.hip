@@ -118,6 +118,11 @@ __device__ __forceinline__ bool rx_maybe(const TraceArgs& a, float3 o, float3 d,
 #ifndef RT_XCD_WINDOWS
 #define RT_XCD_WINDOWS 0
 #endif
+// RT_TRACE_ZBAND: rt_trace's BVH bursts in the banded direction order (dir_order_banded: the most
+// nearly horizontal rays first), as coverage plans use
+#ifndef RT_TRACE_ZBAND
+#define RT_TRACE_ZBAND 0
+#endif
 #ifndef RT_SPARSE_RX
 #define RT_SPARSE_RX 1
 #endif
@@ -1262,7 +1267,9 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
   const bool windows = sort && RT_XCD_WINDOWS && n >= 64 * (int64_t)kDirWinRows;
   if (sort) trace_mark(0, stream);
   if (sort) {
-    a.order = windows ? dir_order_windows(ray_offset, n, stream, &sort_ws) : dir_order(ray_offset, n, stream, &sort_ws);
+    a.order = windows          ? dir_order_windows(ray_offset, n, stream, &sort_ws)
+              : RT_TRACE_ZBAND ? dir_order_banded(ray_offset, n, stream, &sort_ws)
+                               : dir_order(ray_offset, n, stream, &sort_ws);
     if (!a.order) return -1;
     a.win_chunks = windows ? kDirWinRows / 256 : 0;
     trace_mark(1, stream);
