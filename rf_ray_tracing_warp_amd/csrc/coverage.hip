@@ -1405,6 +1405,9 @@ __global__ __launch_bounds__(256) void k_sel_scatter(const uint8_t* flag, const 
 #ifndef RT_REPLAY_RAY_KEY
 #define RT_REPLAY_RAY_KEY 0
 #endif
+#ifndef RT_REPLAY_LONG_FIRST
+#define RT_REPLAY_LONG_FIRST 0
+#endif
 template <bool USE_BVH>
 __device__ __forceinline__ uint16_t replay_key(const CovParams& p, uint64_t key) {
   {
@@ -1427,7 +1430,9 @@ __device__ __forceinline__ uint16_t replay_key(const CovParams& p, uint64_t key)
 #pragma unroll
     for (int b = 0; b < 5; ++b) mz |= ((cx >> b) & 1u) << (2 * b) | ((cy >> b) & 1u) << (2 * b + 1);
     if (USE_BVH && RT_COV_BVH_DIRKEY) return (uint16_t)((dy * 8 + dx) << 10 | mz);
-    const uint32_t rem = (uint32_t)min(max(p.B - 1 - k0, 0), 3);
+    // bounces left, in 2 bits; RT_REPLAY_LONG_FIRST: the most first (a window's longest replays
+    // start first, so the kernel's last waves are short ones)
+    const uint32_t rem0 = (uint32_t)min(max(p.B - 1 - k0, 0), 3), rem = RT_REPLAY_LONG_FIRST ? 3u - rem0 : rem0;
     if (!USE_BVH && RT_REPLAY_RAY_KEY) {  // brute force: the ray's trajectory slot after the bounces left
       const int sh = max(0, 32 - __clz((int)max(p.n - 1, (int64_t)1)) - 14);
       return (uint16_t)(rem << 14 | ((uint32_t)(r >> sh) & 0x3FFFu));

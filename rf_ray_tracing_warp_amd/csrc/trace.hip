@@ -121,7 +121,7 @@ __device__ __forceinline__ bool rx_maybe(const TraceArgs& a, float3 o, float3 d,
 // RT_TRACE_ZBAND: rt_trace's BVH bursts in the banded direction order (dir_order_banded: the most
 // nearly horizontal rays first), as coverage plans use
 #ifndef RT_TRACE_ZBAND
-#define RT_TRACE_ZBAND 0
+#define RT_TRACE_ZBAND 1  // K4 rt_trace 978 -> 934 us, bit-identical (profiles/r4z5_k4_trace_zband_ab.jsonl)
 #endif
 #ifndef RT_SPARSE_RX
 #define RT_SPARSE_RX 1
