@@ -1059,7 +1059,11 @@ __device__ __forceinline__ uint16_t dir_cell(int64_t gid) {
   for (int b = 0; b < 8; ++b) k |= ((cx >> b) & 1u) << (2 * b) | ((cy >> b) & 1u) << (2 * b + 1);
   return (uint16_t)k;
 }
-// Coverage plans (dir_order_banded): the direction cell under a band of |d.z| (8 bands, the most
+#ifndef RT_ZBANDS
+#define RT_ZBANDS 8  // bands of |d.z| (a power of two <= 256)
+#endif
+constexpr int kZBandBits = RT_ZBANDS <= 1 ? 0 : 32 - __builtin_clz((unsigned)(RT_ZBANDS - 1));
+// Coverage plans (dir_order_banded): the direction cell under a band of |d.z| (RT_ZBANDS bands, the most
 // nearly horizontal first).  A terrain's grazing rays walk the longest BVH chains; issued first,
 // their waves run beside the short ones instead of after them (a rank's trajectory pass is two
 // rounds of the GPU's wave slots).  Only the processing order changes.
@@ -1067,7 +1071,7 @@ __global__ __launch_bounds__(256) void k_dir_keys_banded(int64_t ray_offset, int
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const float3 d = rt::ray_dir(ray_offset + i);
-  const uint32_t band = (uint32_t)fminf(fabsf(d.z) * 8.0f, 7.0f);
+  const uint32_t band = (uint32_t)fminf(fabsf(d.z) * (float)RT_ZBANDS, (float)(RT_ZBANDS - 1));
   keys[i] = band << 16 | dir_cell(ray_offset + i);
   rows[i] = (int32_t)i;
 }
@@ -1164,7 +1168,7 @@ const int32_t* dir_order_banded(int64_t ray_offset, int64_t n, hipStream_t strea
   *ws = nullptr;
   keep_pool_memory();
   if (hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                                         (int32_t*)nullptr, (int32_t*)nullptr, (int)n, 0, 19, stream) != hipSuccess) {
+                                         (int32_t*)nullptr, (int32_t*)nullptr, (int)n, 0, 16 + kZBandBits, stream) != hipSuccess) {
     set_error("dir_order_banded: hipcub sizing failed");
     return nullptr;
   }
@@ -1182,7 +1186,7 @@ const int32_t* dir_order_banded(int64_t ray_offset, int64_t n, hipStream_t strea
   void* tmp = (char*)*ws + 4 * kb;
   hipLaunchKernelGGL(k_dir_keys_banded, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, ray_offset, n, k_in,
                      r_in);
-  e = hipcub::DeviceRadixSort::SortPairs(tmp, cub_bytes, k_in, k_out, r_in, r_out, (int)n, 0, 19, stream);
+  e = hipcub::DeviceRadixSort::SortPairs(tmp, cub_bytes, k_in, k_out, r_in, r_out, (int)n, 0, 16 + kZBandBits, stream);
   if (e != hipSuccess) {
     hip_fail(e, "dir_order_banded sort");
     return nullptr;
