@@ -68,6 +68,10 @@ void keep_pool_memory();
 // Row order for tracing rays [ray_offset, ray_offset+n) of one burst sorted by initial direction
 // (trace.hip).  Stream-ordered workspace returned in *ws (hipFreeAsync it after the consumer).
 const int32_t* dir_order(int64_t ray_offset, int64_t n, hipStream_t stream, void** ws);
+// dir_order_banded: bands of |d.z| (a power of two <= 256), the most nearly horizontal first
+#ifndef RT_ZBANDS
+#define RT_ZBANDS 16  // K4 rt_trace 1037 / 945 / 915 / 928 / 976 us at 4 / 8 / 16 / 32 / 64 (r4z7, r4z8)
+#endif
 const int32_t* dir_order_banded(int64_t ray_offset, int64_t n, hipStream_t stream, void** ws);
 // Device view of a mesh's BVH for rt::bvh_query
 inline BvhView bvh_view(const rt_mesh* m) {

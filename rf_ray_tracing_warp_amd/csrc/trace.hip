@@ -1059,9 +1059,6 @@ __device__ __forceinline__ uint16_t dir_cell(int64_t gid) {
   for (int b = 0; b < 8; ++b) k |= ((cx >> b) & 1u) << (2 * b) | ((cy >> b) & 1u) << (2 * b + 1);
   return (uint16_t)k;
 }
-#ifndef RT_ZBANDS
-#define RT_ZBANDS 16  // bands of |d.z| (a power of two <= 256): K4 rt_trace 1037 / 945 / 915 us at 4 / 8 / 16 (r4z7)
-#endif
 constexpr int kZBandBits = RT_ZBANDS <= 1 ? 0 : 32 - __builtin_clz((unsigned)(RT_ZBANDS - 1));
 // Coverage plans (dir_order_banded): the direction cell under a band of |d.z| (RT_ZBANDS bands, the most
 // nearly horizontal first).  A terrain's grazing rays walk the longest BVH chains; issued first,
