@@ -43,6 +43,7 @@ namespace {
 
 
 struct CovParams {
+  int cols_spans;  // k_cols: cooperative span writes (the plan's last run averaged enough items per ray)
   const float4* env_perm;
   const float4* env_nrm;
   int env_nf;
@@ -801,6 +802,9 @@ __device__ __forceinline__ void owned_strips(const CovParams& p, const Seg& s, i
 #define RT_COLS_SPANS 1
 #endif
 constexpr int kColSpans = 4;
+#ifndef RT_COLS_SPANS_MIN
+#define RT_COLS_SPANS_MIN 0
+#endif
 struct ColSpan {
   int32_t ia0;   // first column
   uint32_t n;    // columns
@@ -811,7 +815,8 @@ __global__ __launch_bounds__(256) void k_cols(CovParams p) {
   __shared__ uint32_t s_tot;
   __shared__ ColSpan s_span[kColSpans][256];
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const bool spans_ok = RT_COLS_SPANS && (int64_t)p.B * p.g.nz <= kColSpans && p.g.nz <= 4096 && p.nshard < 65536;
+  const bool spans_ok = RT_COLS_SPANS && p.cols_spans && (int64_t)p.B * p.g.nz <= kColSpans && p.g.nz <= 4096 &&
+                        p.nshard < 65536;
   for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < p.n; base += stride) {
     const int64_t r = base + threadIdx.x;
     const bool active = r < p.n;
@@ -2164,6 +2169,7 @@ struct rt_coverage {
   int64_t cap = 0;
   int64_t last_candidates = 0;
   int64_t last_list = 0;  // first wins of the last run (sizes the early replay's grid)
+  int64_t last_items = -1;  // column items of the last run (k_cols' write mode), -1: none yet
   int64_t last_received = 0;  // first-win (cell, ray) records of the last run
   void* rord = nullptr;        // replay-order sort workspace (16-bit keys + int32 rows, x2, + hipCUB)
   size_t rord_bytes = 0;
@@ -2998,6 +3004,12 @@ __global__ __launch_bounds__(256) void k_iota(int64_t n, int64_t* out) {
 }
 
 void free_cands(rt_coverage* c) {
+  // Work still in flight may read these buffers: the early window replay is launched before the
+  // host sees the candidate counts, and an overflow regrows the buffers right after (a K3 rank of
+  // 4 with 250k rays overflows the initial 8-per-ray capacity on its first run: the replay then
+  // read freed memory, an illegal address in the N = 4 rehearsal, profiles/r4zb_rehearse_4.log).
+  // Growth is rare (first runs), so wait for the device here.
+  (void)hipDeviceSynchronize();
   for (void* q : {(void*)c->keys, (void*)c->keys_sorted, (void*)c->okeys, (void*)c->okeys_sorted, (void*)c->ukeys,
                   (void*)c->oamps, (void*)c->oamps_sorted, (void*)c->uamps, (void*)c->tcos, (void*)c->tsin, (void*)c->ev,
                   (void*)c->win, (void*)c->trx,
@@ -3109,6 +3121,7 @@ int alloc_cands(rt_coverage* c, int64_t cap) {
 }
 
 int alloc_items(rt_coverage* c, int64_t cap) {
+  (void)hipDeviceSynchronize();  // as free_cands: nothing in flight may still read the old list
   if (c->items) (void)hipFree(c->items);
   c->items = nullptr;
   RT_HIP(hipMalloc(&c->items, cap * 8));
@@ -3365,8 +3378,11 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
   }
   p.bin_bits = kb.bin;
   p.cell_bits = kb.cell;
-  int64_t ncand = 0, nrec = 0, nlist = 0;
+  int64_t ncand = 0, nrec = 0, nlist = 0, nitems_last = -1;
   const unsigned grid_items = 4096;
+  // k_cols writes a block's items cooperatively when rays average more than RT_COLS_SPANS_MIN items
+  // (K3: a room's segments cross many columns), else each lane its own few (K5's terrain)
+  p.cols_spans = c->last_items < 0 || c->last_items > (int64_t)RT_COLS_SPANS_MIN * c->n ? 1 : 0;
   // Replay launched before the list length reaches the host (RT_REPLAY_EARLY): the kernels read it
   // from the device counter, so the host's counter read-back and its wake-up (~36 us per K3 rank
   // of 8, profiles/r3j_k3.timeline.txt) overlap the replay instead of idling the GPU.  Only for
@@ -3463,6 +3479,7 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
     const unsigned long long h[3] = {c->hcnt[0], c->hcnt[1], c->hcnt[2]};
     ncand = (int64_t)h[0];
     const int64_t nitems = (int64_t)h[1];
+    nitems_last = nitems;
     nlist = (int64_t)h[2];
     if (ncand <= c->cap && nitems <= c->item_cap) break;
     if (attempt >= 3) {
@@ -3483,6 +3500,7 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
   }
   c->last_candidates = ncand;
   c->last_list = nlist;
+  c->last_items = nitems_last;
   *ncand_out = ncand;
   if (ncand > 0) {
     if (nlist > 0) {
