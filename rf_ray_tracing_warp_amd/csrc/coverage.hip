@@ -1294,11 +1294,20 @@ __device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab
 #ifndef RT_WIN_WAVES
 #define RT_WIN_WAVES 6  // 80 VGPRs, spill-free with the dot-form ball test: K3 k_win 0.935 -> 0.895 ms, K5 0.79 -> 0.76 (r3ze); before it, 5 waves (96 VGPRs, 60 B scratch) beat 4 and 6: 1.03 -> 0.98 ms (r2zj)
 #endif
+// candidates of this attempt, 0 if they overflowed the buffers (k_win, the first-win list and the
+// early replay then do nothing: a lane's keys that would cross the capacity are not written, and
+// reading the hole took the replay to illegal addresses in the N = 4 one-GPU rehearsal)
+__device__ __forceinline__ int64_t cand_count(const unsigned long long* n_dev, int64_t cap) {
+  const int64_t n = (int64_t)*n_dev;
+  return n > cap ? 0 : n;
+}
 __global__ __launch_bounds__(256, RT_WIN_WAVES) void k_win(CovParams p, const uint64_t* keys, const unsigned long long* nkeys_dev,
                                              int64_t cap, uint8_t* first_flag, float* trx) {
   __shared__ RxLds L;
   stage_rx(L, p.r_rx);
-  const int64_t nkeys = min((int64_t)*nkeys_dev, cap);  // the candidate count, capped as k_cells stored it
+  // the candidate count; past the capacity the keys have holes (k_cells skips a lane's keys that
+  // would cross it) and the host reruns the attempt, so this one tests nothing
+  const int64_t nkeys = cand_count(nkeys_dev, cap);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nkeys; i += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t key = keys[i];
     const int64_t cell = (int64_t)(key >> 28), r = (int64_t)((key >> 4) & 0xFFFFFF);
@@ -1357,7 +1366,7 @@ __device__ __forceinline__ int block_sum(int v, int* s4) {
 __global__ __launch_bounds__(256) void k_sel_count(const uint8_t* flag, const unsigned long long* n_dev, int64_t cap,
                                                    int32_t* counts) {
   __shared__ int s4[4];
-  const int64_t n = min((int64_t)*n_dev, cap), tile = sel_tile(n, gridDim.x);
+  const int64_t n = cand_count(n_dev, cap), tile = sel_tile(n, gridDim.x);
   const int64_t lo = (int64_t)blockIdx.x * tile, hi = min(lo + tile, n);
   int c = 0;
   for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) c += flag[i] != 0;
@@ -1369,7 +1378,7 @@ __global__ __launch_bounds__(256) void k_sel_scatter(const uint8_t* flag, const 
                                                      ReplayItem* items, unsigned long long* nlist) {
   __shared__ int s4[4];
   __shared__ int w4[4];
-  const int64_t n = min((int64_t)*n_dev, cap), tile = sel_tile(n, gridDim.x);
+  const int64_t n = cand_count(n_dev, cap), tile = sel_tile(n, gridDim.x);
   const int64_t lo = (int64_t)blockIdx.x * tile, hi = min(lo + tile, n);
   int before = 0;
   for (int j = threadIdx.x; j < (int)blockIdx.x; j += blockDim.x) before += counts[j];
