@@ -118,6 +118,34 @@ def test_poisoned_buffers_do_not_change_ray_sharded_coverage():
     env.close()
 
 
+def test_poisoned_overflowing_first_run_of_a_rank_plan():
+    """A K3 rank plan of 8 (125k of 1M rays, 256^2 cells) overflows its first candidate capacity (8
+    per ray) on its first run while the early window replay is queued: that attempt must test
+    nothing (the keys past the capacity have holes -- poison here) and the rerun must give the
+    unpoisoned plan's records bit for bit."""
+    room = load_stl(os.path.join(REPO, "models", "room.stl"))
+    grid = CoverageGrid.square(256, 15.0, 5.0)
+    tx, win, W, r = (10.0, 0.0, 5.0), 100e-9, 8, 3
+
+    def records():
+        pl = Coverage(room, 2.998e8, 100e9, win, 3, 1_000_000, grid, 0.1, device=0, shard_index=r, shard_count=W,
+                      shard_mode="rays")
+        k, a, counts = pl.trace_records(tx, 1)
+        out = (k.cpu().numpy().copy(), a.cpu().numpy().copy(), list(counts), pl.last_candidates)
+        pl.close()
+        return out
+
+    _poison(-1)
+    ref = records()
+    assert ref[3] > 8 * (1_000_000 // W)  # the first attempt overflowed
+    for byte in (0xFF, 0xA5):
+        _poison(byte)
+        got = records()
+        assert got[2] == ref[2], f"poison {byte:#x}"
+        assert got[0].tobytes() == ref[0].tobytes() and got[1].tobytes() == ref[1].tobytes(), f"poison {byte:#x}"
+    _poison(-1)
+
+
 def test_poisoned_pool_does_not_change_bvh_trace():
     """rt_trace on a BVH mesh sorts its rows by direction in a stream-ordered pool workspace."""
     terr = synthetic_terrain(256, 50.0)
