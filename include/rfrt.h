@@ -147,7 +147,9 @@ int rt_coverage_trace_records(rt_coverage* cov, const float* tx_pos, double tx_p
                               void* stream);
 /* rt_coverage_trace_records that also writes the records (rt_coverage_records' layout) into the
  * caller's device buffers of max_out records before it synchronizes, when they fit: stats[2] = 1
- * then (else 0, and the caller takes them with rt_coverage_records).  stats: 3 int64. */
+ * then (else 0, and the caller takes them with rt_coverage_records).  stats: 3 int64.
+ * The trace calls return RT_EHIP ("a look-back wait timed out") if a cross-tile wait of this
+ * call's record reduce, or of the plan's previous owner stage, gave up: the sums would be wrong. */
 int rt_coverage_trace_records_to(rt_coverage* cov, const float* tx_pos, double tx_power, double light_speed,
                                  double sample_rate, int flags, int64_t n_bins, uint64_t* keys_out, uint64_t* sums_out,
                                  int64_t max_out, int64_t* counts, int64_t* stats, void* stream);
