@@ -2591,10 +2591,14 @@ constexpr int kOwnItems = RT_OWN_ITEMS, kOwnTile = 256 * kOwnItems;
 #define RT_OWNER_LOOKBACK 1
 #endif
 // RT_LOOKBACK_TICKET 1: tiles taken in order from a ticket counter (one same-address atomic per
-// block); 0: tile = block index -- the dispatcher issues workgroups in index order, so every
-// predecessor a block waits on is already resident and makes progress
+// block), so a block only ever waits on tiles that running blocks hold.  0 (tile = block index) is
+// ~13 us faster per rank of 8 on an idle GPU, but unsafe: each XCD dispatches its share of the
+// workgroups on its own, so a block can wait on a predecessor its XCD cannot place while other
+// work fills it.  With four processes on one GPU (the N = 4 rehearsal) the waits ran out, the
+// prefixes were wrong and the power sweeps read out of bounds (profiles/r4zd_rehearse_4.log; with
+// tickets: r4zf_ticket_*.log).
 #ifndef RT_LOOKBACK_TICKET
-#define RT_LOOKBACK_TICKET 0
+#define RT_LOOKBACK_TICKET 1
 #endif
 constexpr uint64_t kOwnAgg = 1ull << 38, kOwnInc = 2ull << 38, kOwnCount = (1ull << 38) - 1;
 constexpr uint64_t kOwnTagMask = ~(kOwnInc | kOwnAgg | kOwnCount);
