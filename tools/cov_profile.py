@@ -111,6 +111,8 @@ def rays_case(case, m, grid, tx, win, B, env, S, reps):
                       "ms_trace_stage": [round(x * 1e3, 3) for x in t_trace],
                       "ms_owner_stage": [round(x * 1e3, 3) for x in t_own],
                       "records_sent": nsent, "records_received": nrec}), flush=True)
+    for p in plans:
+        p.close()
 
 
 # Cost model of the three collectives of a ray-sharded map (run() / bench.py: dist.exchange_rows =
@@ -135,8 +137,6 @@ def collective_model(nsent, nrec, grid, S):
     return {"xgmi_gbs_assumed": gbs, "latency_us_per_collective": lat, "a2a_bytes_max": int(a2a),
             "allgather_bytes_in": int(ag_in), "ms_all_to_all": round(ms_a2a, 4), "ms_all_gather": round(ms_ag, 4),
             "ms_total": round(ms_a2a + ms_ag, 4)}
-    for p in plans:
-        p.close()
 
 
 if __name__ == "__main__":
