@@ -22,7 +22,7 @@ def test_collective_model_arithmetic(monkeypatch):
     monkeypatch.setenv("XGMI_GBS", "300")
     monkeypatch.setenv("COLL_US", "25")
     m = _model()([200_000, 180_000], [150_000, 210_000], _Grid(), 8)
-    a2a = 210_000 * 32 * 7 / 8  # the largest receiver, its own eighth local
+    a2a = 210_000 * 32 * 7 / 8  # the largest sender or receiver, its own eighth local
     ag = (256 + 7) // 8 * 256 * 8 * 7  # the other owners' columns, f64
     assert m["a2a_bytes_max"] == int(a2a)
     assert m["allgather_bytes_in"] == ag
