@@ -67,6 +67,8 @@ def parse():
     ap.add_argument("--cpu-rays", type=int, default=8_000_000, help="rays per CPU-baseline run (all threads)")
     ap.add_argument("--cpu-cells", type=int, default=8,
                     help="K3 / K5 cells per coverage CPU-baseline run (SURVEY 8(d) D5: median of 5 after a warm-up)")
+    ap.add_argument("--cpu-cells-1thread", type=int, default=1,
+                    help="K3 / K5 cells per run of the one-thread coverage leg (the first of the seeded cells)")
     ap.add_argument("--no-coverage", action="store_true", help="skip K3 (same as leaving it out of --legs)")
     ap.add_argument("--coverage-grid", type=int, default=256, help="K3: n x n receiver cells at z=5 on room.stl")
     ap.add_argument("--coverage-rays", type=int, default=1_000_000)
@@ -167,7 +169,8 @@ def cpu_baseline_k2(args, B, tx, rx, info, build):
 def cpu_baseline_k3(args, info):
     """coverage.py:38-57 literally on the host for a seeded sample of K3 cells (full 1M-ray trace
     with the cell's icosphere, the per-path host CIR of tracer.py:84-117, np.convolve power):
-    cells/s over the sample, median of cpu_runs.  Also the reference's np.convolve step alone."""
+    cells/s over the sample, median of cpu_runs, on all threads and (the first cpu_cells_1thread
+    cells) on one thread.  Also the reference's np.convolve step alone."""
     from oracle import oracle as orc
     from rf_ray_tracing_warp_amd.coverage import CoverageGrid
     from rf_ray_tracing_warp_amd.mesh import load_stl, sphere
@@ -179,22 +182,24 @@ def cpu_baseline_k3(args, info):
     cen = grid.centers().reshape(-1, 3)[cells]
     N, B, tx = args.coverage_rays, args.bounces, (10.0, 0.0, 5.0)
 
-    def run():
-        for c in cen:
-            rxm = sphere(c, 0.1, 1)
-            o = orc.trace(E, orc.Mesh(rxm.vertices, rxm.faces), tx, B, 0, N, want_traced=False,
-                          nthreads=info["threads_used"])
-            ir = orc.cir_from_paths(orc.clean_paths(o["received"], o["mask"]), 1, N, 2.998e8, 100e9, 100e-9)
-            orc.signal_power(ir, 100e-9)
-    med, ts = _median_runs(run, args.cpu_runs)
+    def leg(sel, threads):
+        def run():
+            for c in cen[:sel]:
+                rxm = sphere(c, 0.1, 1)
+                o = orc.trace(E, orc.Mesh(rxm.vertices, rxm.faces), tx, B, 0, N, want_traced=False, nthreads=threads)
+                ir = orc.cir_from_paths(orc.clean_paths(o["received"], o["mask"]), 1, N, 2.998e8, 100e9, 100e-9)
+                orc.signal_power(ir, 100e-9)
+        med, ts = _median_runs(run, args.cpu_runs)
+        return {"value": sel / med, "unit": "cells/s", "cores": threads, "kind": "port",
+                "sample": f"{sel} seeded K3 cells ({', '.join(str(int(c)) for c in cells[:sel])}), each the reference "
+                          f"loop body: {N}-ray trace with its icosphere + host CIR + np.convolve power; median of "
+                          f"{len(ts)} runs after 1 warm-up ({', '.join(f'{t:.2f}' for t in ts)} s)", "host": info}
     ir = np.zeros(10000)
     ir[[3000, 5000, 7000]] = 1e-6
     conv, _ = _median_runs(lambda: orc.signal_power(ir, 100e-9), 5)
-    return {"value": len(cells) / med, "unit": "cells/s", "cores": info["threads_used"], "kind": "port",
-            "sample": f"{len(cells)} seeded K3 cells ({', '.join(str(int(c)) for c in cells)}), each the reference "
-                      f"loop body: {N}-ray trace with its icosphere + host CIR + np.convolve power; median of "
-                      f"{len(ts)} runs after 1 warm-up ({', '.join(f'{t:.2f}' for t in ts)} s)",
-            "np_convolve_power_ms_per_cell": conv * 1e3, "host": info}
+    out = {"all": leg(len(cells), info["threads_used"]), "1thread": leg(args.cpu_cells_1thread, 1)}
+    out["all"]["np_convolve_power_ms_per_cell"] = conv * 1e3
+    return out
 
 
 def cpu_baseline_k1(args, info, build):
@@ -252,7 +257,8 @@ def cpu_baseline_k4(args, terr, info, build):
 
 def cpu_baseline_k5(args, terr, info):
     """coverage.py:38-57 literally on the host for seeded K5 cells of the terrain map: per cell a
-    1M-ray trace with its icosphere (oracle BVH path), host CIR, np.convolve power."""
+    1M-ray trace with its icosphere (oracle BVH path), host CIR, np.convolve power; all threads and
+    (the first cpu_cells_1thread cells) one thread."""
     from oracle import oracle as orc
     from rf_ray_tracing_warp_amd.coverage import CoverageGrid
     from rf_ray_tracing_warp_amd.mesh import sphere
@@ -263,20 +269,20 @@ def cpu_baseline_k5(args, terr, info):
     cen = grid.centers().reshape(-1, 3)[ids]
     N, B, tx = args.k5_rays, 3, (10.0, 0.0, 4.5)
 
-    def run():
-        for c in cen:
-            rxm = sphere(c, 0.1, 1)
-            o = orc.trace(E, orc.Mesh(rxm.vertices, rxm.faces), tx, B, 0, N, want_traced=False,
-                          nthreads=info["threads_used"])
-            ir = orc.cir_from_paths(orc.clean_paths(o["received"], o["mask"]), 1, N, 2.998e8, 100e9, 200e-9)
-            orc.signal_power(ir, 200e-9)
-    med, ts = _median_runs(run, args.cpu_runs)
-    return {"value": len(ids) / med, "unit": "cells/s", "cores": info["threads_used"], "kind": "port",
-            "sample": f"{len(ids)} seeded K5 cells ({', '.join(str(int(c)) for c in ids)}), each the reference loop "
-                      f"body: {N}-ray trace over the terrain stand-in with its icosphere (oracle BVH path) + host "
-                      f"CIR + np.convolve power; median of {len(ts)} runs after 1 warm-up "
-                      f"({', '.join(f'{t:.2f}' for t in ts)} s)",
-            "host": info}
+    def leg(sel, threads):
+        def run():
+            for c in cen[:sel]:
+                rxm = sphere(c, 0.1, 1)
+                o = orc.trace(E, orc.Mesh(rxm.vertices, rxm.faces), tx, B, 0, N, want_traced=False, nthreads=threads)
+                ir = orc.cir_from_paths(orc.clean_paths(o["received"], o["mask"]), 1, N, 2.998e8, 100e9, 200e-9)
+                orc.signal_power(ir, 200e-9)
+        med, ts = _median_runs(run, args.cpu_runs)
+        return {"value": sel / med, "unit": "cells/s", "cores": threads, "kind": "port",
+                "sample": f"{sel} seeded K5 cells ({', '.join(str(int(c)) for c in ids[:sel])}), each the reference "
+                          f"loop body: {N}-ray trace over the terrain stand-in with its icosphere (oracle BVH path) + "
+                          f"host CIR + np.convolve power; median of {len(ts)} runs after 1 warm-up "
+                          f"({', '.join(f'{t:.2f}' for t in ts)} s)", "host": info}
+    return {"all": leg(len(ids), info["threads_used"]), "1thread": leg(args.cpu_cells_1thread, 1)}
 
 
 # ------------------------------------------------------------------ coverage legs
@@ -532,7 +538,8 @@ def terrain_legs(args, local, rank, world, dist):
             cb = cpu_baseline_k4(args, terr, info, build)
             k4["cpu_baseline"], k4["cpu_baseline_1thread"] = cb["all"], cb["1thread"]
         if k5 is not None:
-            k5["cpu_baseline"] = cpu_baseline_k5(args, terr, info)
+            cb = cpu_baseline_k5(args, terr, info)
+            k5["cpu_baseline"], k5["cpu_baseline_1thread"] = cb["all"], cb["1thread"]
     return k4, k5
 
 
@@ -547,20 +554,23 @@ def summary(out):
 
     s = {"k2": {"value": r(out["value"]), "ms_per_step": r(out["ms_per_step"]),
                 "roofline_frac": r(out["roofline"]["frac"], 3), "kernel_ms": r(out["roofline"]["kernel_ms"]),
-                "cpu": r((out.get("cpu_baseline") or {}).get("value"))}}
+                "cpu": r((out.get("cpu_baseline") or {}).get("value")),
+                "cpu_1t": r((out.get("cpu_baseline_1thread") or {}).get("value"))}}
     for key, name in (("k1_plumbing", "k1"), ("k4_terrain", "k4")):
         leg = out.get(key)
         if leg:
             f, k = roof(leg)
             s[name] = {"value": r(leg["value"]), "ms_per_step": r(leg["ms_per_step"]), "roofline_frac": f,
-                       "kernel_ms": k, "cpu": r((leg.get("cpu_baseline") or {}).get("value"))}
+                       "kernel_ms": k, "cpu": r((leg.get("cpu_baseline") or {}).get("value")),
+                       "cpu_1t": r((leg.get("cpu_baseline_1thread") or {}).get("value"))}
     for key, name in (("coverage", "k3"), ("k5_terrain_coverage", "k5")):
         leg = out.get(key)
         if leg:
             f, k = roof(leg)
             s[name] = {"value": r(leg["value"]), "ms_per_map": r(leg["ms_per_map"]), "roofline_frac": f,
                        "traj_ms": k, "replay_ms": r((leg.get("stage_ms") or {}).get("replay_ms")),
-                       "cpu": r((leg.get("cpu_baseline") or {}).get("value"))}
+                       "cpu": r((leg.get("cpu_baseline") or {}).get("value")),
+                       "cpu_1t": r((leg.get("cpu_baseline_1thread") or {}).get("value"))}
     return s
 
 
@@ -758,7 +768,8 @@ def main():
             # Warp's CPU launch is serial: the same restatement on one thread
             out["cpu_baseline_1thread"] = cb["1thread"]
             if cov_out is not None:
-                out["coverage"]["cpu_baseline"] = cpu_baseline_k3(args, info)
+                cb3 = cpu_baseline_k3(args, info)
+                out["coverage"]["cpu_baseline"], out["coverage"]["cpu_baseline_1thread"] = cb3["all"], cb3["1thread"]
             if k1_out is not None:
                 cb1 = cpu_baseline_k1(args, info, build)
                 k1_out["cpu_baseline"], k1_out["cpu_baseline_1thread"] = cb1["all"], cb1["1thread"]
