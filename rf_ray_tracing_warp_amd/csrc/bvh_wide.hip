@@ -1,5 +1,5 @@
 // bvh_wide.hip -- collapse the binary BVH (either builder, after pack_leaf_refs) into 4-wide
-// nodes for rt::Walk4, or compressed 8-wide nodes for rt::Walk8 (rt_bvh.h, RT_BVH_WIDTH).  Host pass over the device tree: every wide node takes the
+// nodes for rt::Walk4 (rt_bvh.h).  Host pass over the device tree: every wide node takes the
 // children of one binary node and keeps opening its largest inner child (surface area) until it
 // has four, or until opening more would let the walk's stack bound exceed RT_BVH_STACK; nodes are
 // numbered breadth first, so the top levels are contiguous from node 0.
@@ -36,72 +36,14 @@ double half_area(const float* b) {
 
 namespace rt {
 
-namespace {
-// One 8-wide node in the compressed form of rt::Walk8 (rt_bvh.h), from its k <= 8 children.
-// Every child box is quantised to 8 bits per bound on a per-axis grid origin + q * 2^e with
-// origin = the node's box low corner: the low bound rounded down and the high bound up, checked
-// in the very f32 arithmetic the device decodes with (fmaf(q, 2^e, origin): q * 2^e is exact, so
-// both sides round the same exact sum once).  The decoded box therefore always contains the
-// binary tree's (already outward-rounded and padded) box, and culling stays conservative.
-void emit_node8(const Child* ch, int k, const int* ref, float* node) {
-  for (int i = 0; i < 32; ++i) node[i] = 0.0f;
-  float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-  auto used = [&](int c) { return c < k && ref[c] != -1 && ch[c].box[0] <= ch[c].box[3] &&
-                                   ch[c].box[1] <= ch[c].box[4] && ch[c].box[2] <= ch[c].box[5]; };
-  for (int c = 0; c < k; ++c)
-    if (used(c))
-      for (int a = 0; a < 3; ++a) {
-      lo[a] = std::min(lo[a], ch[c].box[a]);
-      hi[a] = std::max(hi[a], ch[c].box[3 + a]);
-    }
-  uint8_t q[6][8];  // lo.x hi.x lo.y hi.y lo.z hi.z
-  uint32_t ebits = 0;
-  for (int a = 0; a < 3; ++a) {
-    const float o = lo[a] <= hi[a] ? lo[a] : 0.0f;
-    const double ext = lo[a] <= hi[a] ? (double)hi[a] - (double)lo[a] : 0.0;
-    int e = -126;
-    while (e < 127 && std::ldexp(255.0, e) < ext) ++e;
-    for (;; ++e) {  // grow the step until every high bound fits in 255 steps
-      const float sc = std::ldexp(1.0f, e);
-      bool ok = true;
-      for (int c = 0; c < 8 && ok; ++c) {
-        if (!used(c)) {
-          q[2 * a][c] = 255;  // empty slot (its reference says so; the box is never used)
-          q[2 * a + 1][c] = 0;
-          continue;
-        }
-        const float l = ch[c].box[a], h = ch[c].box[3 + a];
-        long ql = (long)std::floor(((double)l - (double)o) / (double)sc);
-        ql = std::max(0L, std::min(255L, ql));
-        while (ql > 0 && (float)(o + (float)ql * sc) > l) --ql;
-        long qh = (long)std::ceil(((double)h - (double)o) / (double)sc);
-        qh = std::max(0L, qh);
-        while (qh <= 255 && (float)(o + (float)qh * sc) < h) ++qh;
-        if (qh > 255 || (float)(o + (float)ql * sc) > l) {
-          ok = false;
-          break;
-        }
-        q[2 * a][c] = (uint8_t)ql;
-        q[2 * a + 1][c] = (uint8_t)qh;
-      }
-      if (ok || e >= 127) break;
-    }
-    node[a] = o;
-    ebits |= (uint32_t)(e + 127) << (8 * a);
-  }
-  std::memcpy(&node[3], &ebits, 4);
-  std::memcpy(&node[4], &q[0][0], 48);  // dwords 4..15: lo.x[8] hi.x[8] lo.y[8] hi.y[8] lo.z[8] hi.z[8]
-  std::memcpy(&node[16], ref, 32);      // dwords 16..23: child refs
-}
-}  // namespace
-
-// The tree as RT_BVH_WIDTH-wide nodes (4: the uncompressed 128-B nodes of Walk4; 8: the
-// compressed 128-B nodes of Walk8).  Both collapse the binary tree the same way: every wide node
-// takes the children of one binary node and keeps opening its largest inner child (surface area)
-// until it has W, within the traversal stack's budget.
+// The tree as 4-wide nodes (the 128-B nodes of Walk4): every wide node takes the children of one
+// binary node and keeps opening its largest inner child (surface area) until it has four, within
+// the traversal stack's budget.  (A compressed 8-wide form -- 8-bit child bounds on a per-node
+// power-of-two grid -- was bit-identical and slower, K4 973 -> 1175 us; removed in round 5, last
+// in commit 43de9a4)
 int build_wide(rt_mesh* m) {
   if (!m->nodes || m->nnodes <= 0) return RT_OK;
-  constexpr int W = RT_BVH_WIDTH == 8 ? 8 : 4;
+  constexpr int W = 4;
   std::vector<float> bin((size_t)m->nnodes * 16);
   RT_HIP(hipMemcpy(bin.data(), m->nodes, bin.size() * sizeof(float), hipMemcpyDeviceToHost));
   auto children = [&](int n, Child* out) {
@@ -165,7 +107,7 @@ int build_wide(rt_mesh* m) {
     return true;
   };
   for (size_t w = 0; w < order.size(); ++w) {
-    Child ch[8];
+    Child ch[W];
     children(order[w], ch);
     int k = 2;
     while (k < W) {
@@ -190,24 +132,6 @@ int build_wide(rt_mesh* m) {
     float node[32];
     int inner = 0;
     for (int c = 0; c < k; ++c) inner += ch[c].inner;
-    if (W == 8) {
-      int ref[8];
-      for (int c = 0; c < 8; ++c) {
-        ref[c] = -1;  // empty slot
-        if (c >= k) continue;
-        if (ch[c].inner) {
-          ref[c] = (int)order.size();
-          order.push_back(ch[c].id);
-          occ.push_back(occ[w] + inner - 1);
-          max_occ = std::max(max_occ, occ.back());
-        } else {
-          ref[c] = ~ch[c].id;  // count 0 (an empty leaf) gives -1, the empty slot
-        }
-      }
-      emit_node8(ch, k, ref, node);
-      wide.insert(wide.end(), node, node + 32);
-      continue;
-    }
     for (int c = 0; c < 4; ++c) {
       int ref = -1;  // empty slot
       if (c < k) {

@@ -43,7 +43,6 @@ namespace {
 
 
 struct CovParams {
-  int cols_spans;  // k_cols: cooperative span writes (the plan's last run averaged enough items per ray)
   const float4* env_perm;
   const float4* env_nrm;
   int env_nf;
@@ -106,28 +105,17 @@ __device__ __forceinline__ void cell_center(const rt_grid& g, int64_t cell, doub
 
 // environment closest hit from the LDS table (same code path as the trace kernel)
 __device__ __forceinline__ rt::Hit env_query_lds(const float4* tab, int nf, const rt::Shear& s) {
-#if RT_LAZY_HIT
   rt::LazyHit h;  // faces in ascending order: the division waits for the winner (rt_device.h)
   rt::lazy_init(h);
-#else
-  rt::Hit h;
-  rt::hit_init(h);
-#endif
   const int off = s.kcase * 3;
   for (int f = 0; f < nf; ++f) {
     const float4 q0 = tab[f * 18 + off + 0];
     const float4 q1 = tab[f * 18 + off + 1];
     const float c2 = tab[f * 18 + off + 2].x;
     float T, det;
-#if RT_LAZY_HIT
     if (rt::tri_test(s, q0, q1, c2, T, det)) rt::lazy_consider(h, T, det, f);
   }
   return rt::lazy_finish(h);
-#else
-    if (rt::tri_test(s, q0, q1, c2, T, det)) rt::hit_consider(h, T, det, f);
-  }
-  return h;
-#endif
 }
 
 template <bool USE_BVH>
@@ -148,91 +136,12 @@ __device__ __forceinline__ void stage_env(const CovParams& p, float4* lds_tab) {
 }
 
 // The cell's receiver: vertex i = (float)(unit_i * r + centre) in double, exactly mesh.sphere() +
-// astype(float32) (tracer.py:27-28), generated directly in the ray's permuted axis order
-// (x=[kx], y=[ky], z=[kz]) so the 80 unrolled faces index registers with compile-time indices.
-struct RxPerm {
-  float v[RT_ICO1_NV][3];
-};
-__device__ __forceinline__ void make_rx_perm(const rt_grid& g, int64_t cell, double r, int kx, int ky, int kz,
-                                             RxPerm& rx) {
-  double c[3];
-  cell_center(g, cell, c);
-#pragma unroll
-  for (int i = 0; i < RT_ICO1_NV; ++i) {
-    float w[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const double m = rt_ico1_v[i][k] * r;
-      w[k] = (float)(m + c[k]);
-    }
-    rx.v[i][0] = kx == 0 ? w[0] : (kx == 1 ? w[1] : w[2]);
-    rx.v[i][1] = ky == 0 ? w[0] : (ky == 1 ? w[1] : w[2]);
-    rx.v[i][2] = kz == 0 ? w[0] : (kz == 1 ? w[1] : w[2]);
-  }
-}
-
-// receiver closest hit for ray (o, d) against cell's icosphere (80 faces, unrolled)
-__device__ __forceinline__ rt::Hit rx_query(const rt_grid& g, int64_t cell, double r, float3 o, float3 d) {
-  const rt::Shear s = rt::make_shear(o, d);
-  const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
-  const int kz = (ax > ay && ax > az) ? 0 : ((ay > az) ? 1 : 2);
-  int kx = kz + 1;
-  if (kx == 3) kx = 0;
-  int ky = kx + 1;
-  if (ky == 3) ky = 0;
-  if (rt::comp(d, kz) < 0.0f) {
-    const int t = kx;
-    kx = ky;
-    ky = t;
-  }
-  RxPerm rx;
-  make_rx_perm(g, cell, r, kx, ky, kz, rx);
-  rt::Hit h;
-  rt::hit_init(h);
-#pragma unroll
-  for (int f = 0; f < RT_ICO1_NF; ++f) {
-    const float* a = rx.v[rt_ico1_f[f][0]];
-    const float* b = rx.v[rt_ico1_f[f][1]];
-    const float* c = rx.v[rt_ico1_f[f][2]];
-    float T, det;
-    if (rt::tri_test(s, make_float4(a[0], a[1], a[2], b[0]), make_float4(b[1], b[2], c[0], c[1]), c[2], T, det))
-      rt::hit_consider(h, T, det, f);
-  }
-  return h;
-}
-
-// rx_query with the vertices computed per face instead of held in registers: the same double
-// arithmetic (unit * r + centre, rounded once to float) on the same values, so every bit agrees
-// with rx_query; about twice its VALU but ~130 fewer VGPRs, for the latency-bound replay kernel
-// whose occupancy the 126 live vertex floats would otherwise set at one wave per SIMD.
-__device__ __forceinline__ double pickd(double x, double y, double z, int k) { return k == 0 ? x : (k == 1 ? y : z); }
-__device__ __forceinline__ rt::Hit rx_query_lean(const rt_grid& g, int64_t cell, double r, float3 o, float3 d) {
-  const rt::Shear s = rt::make_shear(o, d);
-  double c[3];
-  cell_center(g, cell, c);
-  const double cx = pickd(c[0], c[1], c[2], s.kx), cy = pickd(c[0], c[1], c[2], s.ky),
-               cz = pickd(c[0], c[1], c[2], s.kz);
-  rt::Hit h;
-  rt::hit_init(h);
-#pragma unroll 1
-  for (int f = 0; f < RT_ICO1_NF; ++f) {
-    float q[9];
-#pragma unroll
-    for (int v = 0; v < 3; ++v) {
-      const int vi = rt_ico1_f[f][v];
-      const double ux = rt_ico1_v[vi][0], uy = rt_ico1_v[vi][1], uz = rt_ico1_v[vi][2];
-      const double mx = pickd(ux, uy, uz, s.kx) * r, my = pickd(ux, uy, uz, s.ky) * r, mz = pickd(ux, uy, uz, s.kz) * r;
-      q[3 * v + 0] = (float)(mx + cx);
-      q[3 * v + 1] = (float)(my + cy);
-      q[3 * v + 2] = (float)(mz + cz);
-    }
-    float T, det;
-    if (rt::tri_test(s, make_float4(q[0], q[1], q[2], q[3]), make_float4(q[4], q[5], q[6], q[7]), q[8], T, det))
-      rt::hit_consider(h, T, det, f);
-  }
-  return h;
-}
-
+// astype(float32) (tracer.py:27-28), permuted to the ray's shear axes where a face is tested.
+// Three earlier forms of the query gave the same bits -- all 42 vertices in registers (126 live
+// floats), three vertices per face recomputed (twice the vertex VALU), and the 12 icosahedron
+// corners in registers with each group's midpoints generated (72 vertex evaluations); the culled
+// group form below replaced them (K3 map 8.84 / 10.41 / 7.18 -> 5.96 ms); removed in
+// round 5, last in commit 43de9a4.
 // Faces 4g..4g+3 of icosphere(1) subdivide icosahedron face g (trimesh's subdivide order): with
 // the corners c0 c1 c2 (vertex ids < 12) and edge midpoints m01 m12 m20 of face g they are
 // (c0 m01 m20), (m01 c1 m12), (m20 m12 c2), (m01 m12 m20).  kIcoGroup[g] = {c0, c1, c2, m01, m12, m20}.
@@ -264,50 +173,6 @@ constexpr bool ico_groups_ok() {
   return true;
 }
 static_assert(ico_groups_ok(), "rt_icosphere1.h is not in trimesh's subdivide order");
-
-// receiver vertex vi of the sphere centred at c: (float)(unit * r + centre) per axis in double, as
-// make_rx_perm, permuted to the ray's shear axes
-__device__ __forceinline__ float3 rx_vert(const double c[3], double r, int vi, const rt::Shear& s) {
-  const float w0 = (float)(rt_ico1_v[vi][0] * r + c[0]);
-  const float w1 = (float)(rt_ico1_v[vi][1] * r + c[1]);
-  const float w2 = (float)(rt_ico1_v[vi][2] * r + c[2]);
-  return make_float3(rt::pick(w0, w1, w2, s.kx), rt::pick(w0, w1, w2, s.ky), rt::pick(w0, w1, w2, s.kz));
-}
-
-// rx_query with the 12 icosahedron corners held in registers and each group's 3 edge midpoints
-// generated where the group is tested (a midpoint belongs to two groups and is computed twice,
-// 72 vertex evaluations instead of 42): the same double arithmetic on the same values as
-// make_rx_perm, so every bit agrees with rx_query, with ~45 live vertex floats instead of 126.
-__device__ __forceinline__ rt::Hit rx_query_grouped(const rt_grid& g, int64_t cell, double r, float3 o, float3 d) {
-  const rt::Shear s = rt::make_shear(o, d);
-  double c[3];
-  cell_center(g, cell, c);
-  float3 cn[12];
-#pragma unroll
-  for (int i = 0; i < 12; ++i) cn[i] = rx_vert(c, r, i, s);
-  rt::Hit h;
-  rt::hit_init(h);
-#pragma unroll
-  for (int gi = 0; gi < RT_ICO1_NF / 4; ++gi) {
-    // a fresh copy of r per group: the midpoints shared with another group are recomputed there
-    // instead of being kept live (CSE would hold all 30 midpoints in registers)
-    double rg = r;
-    asm volatile("" : "+v"(rg));
-    float3 v[6];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) v[j] = cn[kIcoGroup.v[gi][j]];
-#pragma unroll
-    for (int j = 3; j < 6; ++j) v[j] = rx_vert(c, rg, kIcoGroup.v[gi][j], s);
-#pragma unroll
-    for (int f = 0; f < 4; ++f) {
-      const float3 a = v[kGroupFace[f][0]], b = v[kGroupFace[f][1]], q = v[kGroupFace[f][2]];
-      float T, det;
-      if (rt::tri_test(s, make_float4(a.x, a.y, a.z, b.x), make_float4(b.y, b.z, q.x, q.y), q.z, T, det))
-        rt::hit_consider(h, T, det, 4 * gi + f);
-    }
-  }
-  return h;
-}
 
 // ---- culled receiver query.  The 80 faces come in 20 groups of 4 (one subdivided icosahedron face
 // each, kIcoGroup), every group inside a ball (rt_ico1_gball, unit coordinates).  A face the
@@ -359,9 +224,6 @@ __device__ __forceinline__ void rx_group(const RxLds& L, const double c[3], cons
   }
 }
 
-#ifndef RT_RXQ_DOT_BALL
-#define RT_RXQ_DOT_BALL 1
-#endif
 // ROLLED: the 20-group ball test as a loop over the table (constants by scalar loads) instead of
 // unrolled -- fewer VGPRs (K3 k_replay 167 -> 125, so 4 waves per SIMD without spills), slower where
 // the occupancy does not change (k_win 0.95 -> 1.01 ms, K5 replay 1.23 -> 1.30 ms; r3zc)
@@ -377,17 +239,15 @@ __device__ __forceinline__ rt::Hit rx_query_culled(const RxLds& L, const rt_grid
   const double t0 = (qx * d.x + qy * d.y + qz * d.z) / dd;
   const float ux = (float)(t0 * d.x - qx), uy = (float)(t0 * d.y - qy), uz = (float)(t0 * d.z - qz);
   const float ddf = (float)dd, inv_dd = (float)(1.0 / dd), inv_len = (float)(1.0 / sqrt(dd)), t0f = (float)t0;
-  const float rf = (float)r;
   // pad: f32 vertices (half an ulp of the coordinates) and the watertight test's rounding
   const double amax = fmax(fmax(fabs(c[0]), fabs(c[1])), fmax(fabs(c[2]), fmax(fmax(fabs(o.x), fabs(o.y)), fabs(o.z))));
   const float pad = (float)(1e-3 * r + 2e-5 * (1.0 + amax) + 4e-6 * fabs(t0) * sqrt(dd));
   uint32_t near = 0, far = 0;
   float far_tmin = INFINITY;
-#if RT_RXQ_DOT_BALL
   // Per group, with the unit direction e = d / |d| and u perpendicular to it: the squared distance
   // from the ball centre m to the line is |m - u|^2 - (m.e)^2 = |m|^2 + |u|^2 - 2 m.u - (m.e)^2, and
   // the centre's line parameter is t0 + (m.e) / |d|.  ~20 VALU per group against ~45 for the cross
-  // product form below; its f32 rounding (~1e-7 r^2 in the squared distance) is far inside the
+  // product form (removed in round 5); its f32 rounding (~1e-7 r^2 in the squared distance) is far inside the
   // pad (1e-3 r), so the test stays conservative and every hit is the same.
   (void)ddf;
   (void)inv_dd;
@@ -399,10 +259,7 @@ __device__ __forceinline__ rt::Hit rx_query_culled(const RxLds& L, const rt_grid
   asm volatile("" : "+v"(z));
   const float4* gb = L.gb + z;
   const float* gmm = L.gmm + z;
-#ifndef RT_RXQ_DOT_UNROLL
-#define RT_RXQ_DOT_UNROLL 4
-#endif
-#pragma unroll(ROLLED ? 1 : RT_RXQ_DOT_UNROLL)
+#pragma unroll(ROLLED ? 1 : 4)
   for (int gi = 0; gi < RT_ICO1_NF / 4; ++gi) {
     const float4 m = gb[gi];
     const float me = fmaf(m.x, ex, fmaf(m.y, ey, m.z * ez));
@@ -416,23 +273,6 @@ __device__ __forceinline__ rt::Hit rx_query_culled(const RxLds& L, const rt_grid
       far_tmin = fminf(far_tmin, fmaf(me - R, inv_len, t0f));
     }
   }
-#else
-#pragma unroll(ROLLED ? 1 : RT_ICO1_NF / 4)
-  for (int gi = 0; gi < RT_ICO1_NF / 4; ++gi) {
-    const float mx = rt_ico1_gball[gi][0] * rf, my = rt_ico1_gball[gi][1] * rf, mz = rt_ico1_gball[gi][2] * rf;
-    const float wx = mx - ux, wy = my - uy, wz = mz - uz;  // ball centre relative to the closest point
-    const float cx = wy * d.z - wz * d.y, cy = wz * d.x - wx * d.z, cz = wx * d.y - wy * d.x;
-    const float R = rt_ico1_gball[gi][3] * rf + pad;
-    const float tb = t0f + (mx * d.x + my * d.y + mz * d.z) * inv_dd;  // the ball centre's line parameter
-    const float half = R * inv_len;
-    const bool ok = (cx * cx + cy * cy + cz * cz <= R * R * ddf) && (tb + half >= 0.0f);
-    if (ok && tb <= t0f) near |= 1u << gi;
-    if (ok && tb > t0f) {
-      far |= 1u << gi;
-      far_tmin = fminf(far_tmin, tb - half);
-    }
-  }
-#endif
   rt::Hit h;
   rt::hit_init(h);
   while (near) {
@@ -449,48 +289,16 @@ __device__ __forceinline__ rt::Hit rx_query_culled(const RxLds& L, const rt_grid
   return h;
 }
 
-// receiver query used by the candidate test and the replay (A/B: RT_COV_RXQ 0 registers,
-// 1 per face, 2 grouped, 3 culled groups)
-#ifndef RT_COV_RXQ
-#define RT_COV_RXQ 3
-#endif
-#ifndef RT_COV_RXQ_BVH
-#define RT_COV_RXQ_BVH 3
-#endif
-#ifndef RT_COV_RXQ_WIN
-#define RT_COV_RXQ_WIN 3
-#endif
-template <int V, bool ROLLED = false>
-__device__ __forceinline__ rt::Hit rx_query_v(const RxLds& L, const rt_grid& g, int64_t cell, double r, float3 o,
-                                              float3 d) {
-  if constexpr (V == 0) return rx_query(g, cell, r, o, d);
-  else if constexpr (V == 1) return rx_query_lean(g, cell, r, o, d);
-  else if constexpr (V == 2) return rx_query_grouped(g, cell, r, o, d);
-  else return rx_query_culled<ROLLED>(L, g, cell, r, o, d);
-}
-
-// Minimum waves per SIMD the coverage kernels are built for (launch bounds; 1 = register-unbounded).
-// Unbounded, k_traj<true> took 98 VGPRs (4 waves) and k_replay 201 (2 waves); 5 and 3 (96 and 168
-// VGPRs, ~100 B more spills in the replay) measured K5 6.06 -> 5.59 ms and K3 6.01 -> 5.60 ms per
-// map (k_replay<true> 2.50 -> 2.08 ms, k_replay<false> 3.03 -> 2.53 ms); 4 for the replay
-// (128 VGPRs, 200 B more spills) was no better; re-measured at the round-2 end (r2zk, K3 / K5 replay
-// ms): 3 waves 2.33 / 1.96, 4 waves 2.39 / 2.20, 2 waves (no spills in the LDS replay) 2.86 / 2.30.
-#ifndef RT_COV_TRAJ_WAVES
-#define RT_COV_TRAJ_WAVES 5
-#endif
-// LDS scenes (K3): 4 waves with the rolled receiver ball test (125 VGPRs, no spills): K3 replay
-// 2.067 -> 1.917 ms (r3zc, profiles/r3zc_cov_replay_waves_ab.jsonl); BVH scenes keep 3 (the walk
-// stack's 32 KB of LDS and 155 VGPRs)
-#ifndef RT_COV_REPLAY_WAVES
-#define RT_COV_REPLAY_WAVES 4
-#endif
-#ifndef RT_COV_REPLAY_WAVES_BVH
-#define RT_COV_REPLAY_WAVES_BVH 3
-#endif
+// Minimum waves per SIMD the coverage kernels are built for (launch bounds).  Unbounded, k_traj<true>
+// took 98 VGPRs (4 waves) and k_replay 201 (2 waves); 5 and 3 (96 and 168 VGPRs) measured K5 6.06 ->
+// 5.59 ms and K3 6.01 -> 5.60 ms per map; re-measured at the round-2 end (r2zk).  LDS scenes (K3)
+// replay at 4 waves with the rolled receiver ball test (125 VGPRs, no spills): K3 replay 2.067 ->
+// 1.917 ms (r3zc); BVH scenes keep 3 (the walk stack's 32 KB of LDS and 155 VGPRs).
+constexpr int kTrajWaves = 5, kReplayWaves = 4, kReplayWavesBvh = 3;
 
 // ------------------------------------------------------------------ 1. environment trajectories
 template <bool USE_BVH>
-__global__ __launch_bounds__(256, RT_COV_TRAJ_WAVES) void k_traj(CovParams p) {
+__global__ __launch_bounds__(256, kTrajWaves) void k_traj(CovParams p) {
   extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
   if (p.zero_ctr && blockIdx.x == 0 && threadIdx.x < 4) p.zero_ctr[threadIdx.x] = 0ull;
   stage_env<USE_BVH>(p, lds_tab);
@@ -529,18 +337,10 @@ __global__ __launch_bounds__(256, RT_COV_TRAJ_WAVES) void k_traj(CovParams p) {
 // walking its quarter of the tree below the root's grandchildren (rt::split_init); the group's
 // closest hit is the ray's.  Same trajectories bit for bit; the slowest ray's chain of dependent
 // node fetches is split over four lanes.
-#ifndef RT_TRAJ_SPLIT_G
-#define RT_TRAJ_SPLIT_G 4
-#endif
-// (Splitting the ray's t range over the G lanes instead of the root's subtrees -- each lane opens
-// only boxes overlapping its piece of the ray, so a grazing ray's long run of leaves is divided G
-// ways -- was bit-identical and no faster: K5 rank of 8 1.134 ms vs 1.154 / 1.142 / 1.208 ms for
-// G = 4 / 8 / 16, profiles/r3za_k5_traj_tsplit_ab.jsonl.)
-#ifndef RT_TRAJ_SPLIT_WAVES
-#define RT_TRAJ_SPLIT_WAVES 4  // 120 VGPRs, no spills (5: 96 + 23 spilled); K5 rank of 8 1.204 -> 1.154 ms (r3z)
-#endif
+constexpr int kTrajSplitG = 4;
+// 4 waves per SIMD: 120 VGPRs, no spills (5: 96 + 23 spilled); K5 rank of 8 1.204 -> 1.154 ms (r3z)
 template <int G>
-__global__ __launch_bounds__(256, RT_TRAJ_SPLIT_WAVES) void k_traj_split(CovParams p) {
+__global__ __launch_bounds__(256, 4) void k_traj_split(CovParams p) {
   constexpr int LG = G == 16 ? 4 : 2;
   if (p.zero_ctr && blockIdx.x == 0 && threadIdx.x < 4) p.zero_ctr[threadIdx.x] = 0ull;
   const int j = threadIdx.x & (G - 1);
@@ -557,19 +357,11 @@ __global__ __launch_bounds__(256, RT_TRAJ_SPLIT_WAVES) void k_traj_split(CovPara
     bool alive = valid;
     for (int k = 0; k < p.B; ++k) {
       const rt::Shear s = rt::make_shear(pos, dir);
-#if RT_BVH_WIDTH == 8
-      rt::Walk8 w;
-#else
       rt::Walk4 w;
-#endif
       rt::WalkStack st = rt::make_stack();
       bool active = false;
       if (alive) {
-#if RT_BVH_WIDTH == 8
-        rt::split_init8<G>(w, st, p.env_bvh, s, pos, dir, j);
-#else
         rt::split_init<G>(w, st, p.env_bvh, s, pos, dir, j);
-#endif
         active = true;
       } else {
         rt::hit_init(w.h);
@@ -605,15 +397,13 @@ __global__ __launch_bounds__(256, RT_TRAJ_SPLIT_WAVES) void k_traj_split(CovPara
   }
 }
 
-// k_traj for brute-force scenes with few rays (a ray-sharded rank's share, RT_TRAJ_LDS_SPLIT): G
+// k_traj for brute-force scenes with few rays (a ray-sharded rank's share, kTrajLdsSplit): G
 // lanes per ray, lane j testing the faces f = j, j + G, ... of the LDS table (ascending, so the
 // deferred division's order rule holds within the lane); the lexicographic (t, face) minimum of the
 // G lanes (group_hit) is the ray's closest hit, bit for bit the one-lane loop's.  A K3 rank of 8
 // has 125k rays: one lane per ray is ~490 waves for 1024 SIMDs, and the kernel took as long as one
 // wave's 3 x 44 face tests (41 us against 20 for an eighth of the one-GPU pass).
-#ifndef RT_TRAJ_LDS_SPLIT
-#define RT_TRAJ_LDS_SPLIT 4
-#endif
+constexpr int kTrajLdsSplit = 4;
 template <int G>
 __global__ __launch_bounds__(256) void k_traj_lds_split(CovParams p) {
   extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
@@ -633,13 +423,8 @@ __global__ __launch_bounds__(256) void k_traj_lds_split(CovParams p) {
     bool alive = valid;
     for (int k = 0; k < p.B; ++k) {
       const rt::Shear s = rt::make_shear(pos, dir);
-#if RT_LAZY_HIT
       rt::LazyHit lh;
       rt::lazy_init(lh);
-#else
-      rt::Hit lh;
-      rt::hit_init(lh);
-#endif
       if (alive) {
         const int off = s.kcase * 3;
         for (int f = j; f < p.env_nf; f += G) {
@@ -647,18 +432,10 @@ __global__ __launch_bounds__(256) void k_traj_lds_split(CovParams p) {
           const float4 q1 = lds_tab[f * 18 + off + 1];
           const float c2 = lds_tab[f * 18 + off + 2].x;
           float T, det;
-#if RT_LAZY_HIT
           if (rt::tri_test(s, q0, q1, c2, T, det)) rt::lazy_consider(lh, T, det, f);
-#else
-          if (rt::tri_test(s, q0, q1, c2, T, det)) rt::hit_consider(lh, T, det, f);
-#endif
         }
       }
-#if RT_LAZY_HIT
       const rt::Hit he = rt::group_hit<G>(rt::lazy_finish(lh));
-#else
-      const rt::Hit he = rt::group_hit<G>(lh);
-#endif
       if (!alive) continue;
       if (j == 0) {
         float4* tp = p.traj + 2 * (ir * p.B + k);  // slot ir, as k_traj
@@ -798,13 +575,7 @@ __device__ __forceinline__ void owned_strips(const CovParams& p, const Seg& s, i
 // (Each lane writing its own items serially made a wave last as long as its longest ray: up to ~770
 // stores for a segment across the whole room; K3 rank of 8 49 us for 125k rays.)  Plans with more
 // than kColSpans spans per ray (B x nz) keep the serial writes.
-#ifndef RT_COLS_SPANS
-#define RT_COLS_SPANS 1
-#endif
 constexpr int kColSpans = 4;
-#ifndef RT_COLS_SPANS_MIN
-#define RT_COLS_SPANS_MIN 0
-#endif
 struct ColSpan {
   int32_t ia0;   // first column
   uint32_t n;    // columns
@@ -815,8 +586,7 @@ __global__ __launch_bounds__(256) void k_cols(CovParams p) {
   __shared__ uint32_t s_tot;
   __shared__ ColSpan s_span[kColSpans][256];
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const bool spans_ok = RT_COLS_SPANS && p.cols_spans && (int64_t)p.B * p.g.nz <= kColSpans && p.g.nz <= 4096 &&
-                        p.nshard < 65536;
+  const bool spans_ok = (int64_t)p.B * p.g.nz <= kColSpans && p.g.nz <= 4096 && p.nshard < 65536;
   for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < p.n; base += stride) {
     const int64_t r = base + threadIdx.x;
     const bool active = r < p.n;
@@ -927,10 +697,7 @@ __device__ __forceinline__ unsigned column_cells(const CovParams& p, uint64_t it
 
 // One pass: an item's keys are kept in the thread's LDS slots while the block reserves its
 // output range; only items with more than kCellBuf candidates run the geometry a second time.
-#ifndef RT_CELL_BUF
-#define RT_CELL_BUF 8  // 16 KB of LDS per block instead of 32 (r2zj: candidates stage 0.640 -> 0.636 ms on K3, 0.49 -> 0.48 on K5)
-#endif
-constexpr int kCellBuf = RT_CELL_BUF;
+constexpr int kCellBuf = 8;  // 16 KB of LDS per block instead of 32 (r2zj: candidates stage 0.640 -> 0.636 ms on K3, 0.49 -> 0.48 on K5)
 
 __global__ __launch_bounds__(256) void k_cells(CovParams p) {
   __shared__ uint64_t sbuf[kCellBuf][256];
@@ -962,21 +729,14 @@ __device__ __forceinline__ float npdot(const float* a, const float* b) {
   const float p0 = a[0] * b[0], p1 = a[1] * b[1], p2 = a[2] * b[2];
   return (float)(((double)p0 + (double)p1) + (double)p2);
 }
-// RT_AMP_SQRT: cos(asin(x)) evaluated as sqrt(1 - x^2) (|x| <= 1/5, so the root is >= 0.979 and the
-// identity costs ~1 ulp) and theta's sine and cosine from one sincos -- the replay's per-vertex
-// f64 work without the arcsine and one cosine.  Amplitudes move by ~1e-16 relative, far inside
-// the 1e-9 the coverage tests hold the device to.
-#ifndef RT_AMP_SQRT
-#define RT_AMP_SQRT 1
-#endif
-// sin and cos of x in [0, pi/2 + 1e-6] (bounce_amp's theta): one Cody-Waite step against pi/2 above
-// pi/4 (x - pio2_1 is exact there), then the classic fdlibm kernels on [-pi/4, pi/4] (< 1 ulp).
-// ocml's general sincos carries the large-argument (Payne-Hanek) reduction, whose registers
-// k_replay cannot afford beside its other f64 work (18 VGPRs spilled, 76 B scratch per lane).
-// RT_AMP_SINCOS_Q1=0 restores ocml's sincos.
-#ifndef RT_AMP_SINCOS_Q1
-#define RT_AMP_SINCOS_Q1 1
-#endif
+// cos(asin(x)) is evaluated as sqrt(1 - x^2) (|x| <= 1/5, so the root is >= 0.979 and the
+// identity costs ~1 ulp) and theta's sine and cosine come from one sincos -- the replay's per-vertex
+// f64 work without the arcsine and one cosine (K3 replay 2.50 -> 2.35 ms, r2zh).  Amplitudes move by
+// ~1e-16 relative, far inside the 1e-9 the coverage tests hold the device to.
+// sincos_q1: sin and cos of x in [0, pi/2 + 1e-6] (bounce_amp's theta): one Cody-Waite step against
+// pi/2 above pi/4 (x - pio2_1 is exact there), then the classic fdlibm kernels on [-pi/4, pi/4]
+// (< 1 ulp).  ocml's general sincos carries the large-argument (Payne-Hanek) reduction, whose
+// registers k_replay cannot afford beside its other f64 work (18 VGPRs spilled, 76 B scratch per lane).
 __device__ __forceinline__ void sincos_q1(double x, double& s, double& c) {
   const double pio2_1 = 1.57079632673412561417e+00, pio2_1t = 6.07710050650619224932e-11;
   const bool hi = x > 0.78539816339744828;
@@ -1002,20 +762,11 @@ __device__ __forceinline__ void sincos_q1(double x, double& s, double& c) {
 __device__ __forceinline__ double bounce_amp(float angle) {
   if (isnan(angle)) return 0.0;
   const double theta = (double)(1.57079637050628662109375f - angle / 2.0f);
-#if RT_AMP_SQRT
   double st, ct;
-#if RT_AMP_SINCOS_Q1
   sincos_q1(theta, st, ct);
-#else
-  sincos(theta, &st, &ct);
-#endif
   const double x = st / 5.0;
   const double cti = sqrt(1.0 - x * x);
   const double q = (cti - 5.0 * ct) / (cti + 5.0 * ct);
-#else
-  const double ti = asin(sin(theta) / 5.0);
-  const double q = (cos(ti) - 5.0 * cos(theta)) / (cos(ti) + 5.0 * cos(theta));
-#endif
   double amp = -(q * q);
   if (amp < -1.0) amp = -1.0;
   if (isnan(amp)) return 0.0;
@@ -1024,87 +775,12 @@ __device__ __forceinline__ double bounce_amp(float angle) {
 
 // Incremental form of tracer.py:104-113 for a path that grows one point at a time: distance is
 // the ordered float32 sum of segment norms, amplitude the ordered product of _bounce_amplitude over
-// interior vertices -- identical operations to the loop over (p1, p2, p3) triples.
-struct PathAcc {
-  float prev[3], seg[3];
-  int npts;
-  float dist;
-  double amp;
-  __device__ __forceinline__ void start(float x, float y, float z, double amp0) {
-    prev[0] = x;
-    prev[1] = y;
-    prev[2] = z;
-    npts = 1;
-    dist = 0.0f;
-    amp = amp0;
-  }
-  __device__ __forceinline__ void add(float x, float y, float z) {
-    const float s2[3] = {x - prev[0], y - prev[1], z - prev[2]};
-    if (npts >= 2) {  // vertex prev is interior: angle between seg (p1->p2) and s2 (p2->p3)
-      const float l1 = sqrtf(npdot(seg, seg));
-      const float cosv = npdot(seg, s2) / (l1 * sqrtf(npdot(s2, s2)));
-      amp *= bounce_amp((float)acos((double)cosv));
-    }
-    dist += sqrtf(npdot(s2, s2));
-    seg[0] = s2[0];
-    seg[1] = s2[1];
-    seg[2] = s2[2];
-    prev[0] = x;
-    prev[1] = y;
-    prev[2] = z;
-    ++npts;
-  }
-};
-
-// PathAcc with the previous point and segment (6 floats, read and written once per path vertex)
-// in the thread's LDS column instead of registers (RT_REPLAY_ACC_LDS): the replay's bounce loop
-// keeps its queries' state in registers and spilled ~17 VGPRs to scratch (r3a_kernel_resources).
-// Same operations on the same values, so the same bits.
-#ifndef RT_REPLAY_ACC_LDS
-#define RT_REPLAY_ACC_LDS 0
-#endif
-struct PathAccL {
-  float* col;  // [6][256]: prev xyz, seg xyz at col[256 * i]
-  int npts;
-  float dist;
-  double amp;
-  __device__ __forceinline__ void start(float x, float y, float z, double amp0) {
-    col[0] = x;
-    col[256] = y;
-    col[512] = z;
-    npts = 1;
-    dist = 0.0f;
-    amp = amp0;
-  }
-  __device__ __forceinline__ void add(float x, float y, float z) {
-    const float prev[3] = {col[0], col[256], col[512]};
-    const float s2[3] = {x - prev[0], y - prev[1], z - prev[2]};
-    if (npts >= 2) {
-      const float seg[3] = {col[768], col[1024], col[1280]};
-      const float l1 = sqrtf(npdot(seg, seg));
-      const float cosv = npdot(seg, s2) / (l1 * sqrtf(npdot(s2, s2)));
-      amp *= bounce_amp((float)acos((double)cosv));
-    }
-    dist += sqrtf(npdot(s2, s2));
-    col[768] = s2[0];
-    col[1024] = s2[1];
-    col[1280] = s2[2];
-    col[0] = x;
-    col[256] = y;
-    col[512] = z;
-    ++npts;
-  }
-};
-
-// PathAcc with the amplitude deferred (RT_REPLAY_DEFER_AMP, default): during the bounce loop each
-// interior vertex's cosine (the f32 value acos is taken of) goes to the thread's LDS column, and
-// the f64 product of _bounce_amplitude factors is formed after the loop, in the same vertex order
-// -- the same multiplications of the same values, so the same bits.  The f64 acos and sincos then
-// no longer add their registers to the queries' live state: k_replay<false> spilled 21 VGPRs
-// (88 B of scratch per lane) with them inside the loop, 1 with them stubbed out.
-#ifndef RT_REPLAY_DEFER_AMP
-#define RT_REPLAY_DEFER_AMP 1
-#endif
+// interior vertices -- identical operations to the loop over (p1, p2, p3) triples.  The amplitude
+// is deferred: during the bounce loop each interior vertex's cosine (the f32 value acos is taken of)
+// goes to the thread's LDS column, and the f64 product of _bounce_amplitude factors is formed after
+// the loop, in the same vertex order -- the same multiplications of the same values, so the same
+// bits.  The f64 acos and sincos then no longer add their registers to the queries' live state:
+// k_replay<false> spilled 21 VGPRs (88 B of scratch per lane) with them inside the loop.
 // A path has at most B + 1 points (the TX, then one per bounce), so at most B - 1 interior vertices.
 struct PathAccD {
   float prev[3], seg[3];
@@ -1136,7 +812,7 @@ struct PathAccD {
     ++npts;
   }
 };
-// amp0 times the factors of the first n interior vertices, in path order (PathAcc::amp's product)
+// amp0 times the factors of the first n interior vertices, in path order (tracer.py:104-113)
 __device__ __forceinline__ double amp_product(const float* cosv, int n, double amp0) {
   double amp = amp0;
 #pragma unroll 1
@@ -1167,8 +843,7 @@ __device__ __forceinline__ uint64_t record_key(const CovParams& p, int64_t cell,
 __device__ __forceinline__ bool rx_wins(const CovParams& p, const RxLds& L, int64_t cell, int64_t r, int k,
                                         float& tr) {
   const float4 tp = traj_p(p, r, k), td = traj_d(p, r, k);
-  const rt::Hit hr = rx_query_v<RT_COV_RXQ_WIN>(L, p.g, cell, p.r_rx, make_float3(tp.x, tp.y, tp.z),
-                                                make_float3(td.x, td.y, td.z));
+  const rt::Hit hr = rx_query_culled(L, p.g, cell, p.r_rx, make_float3(tp.x, tp.y, tp.z), make_float3(td.x, td.y, td.z));
   tr = hr.t;
   return hr.face >= 0 && (isinf(tp.w) || tp.w > hr.t);
 }
@@ -1184,24 +859,12 @@ __device__ __forceinline__ bool rx_wins(const CovParams& p, const RxLds& L, int6
 template <bool USE_BVH, bool RX_FIRST>
 __device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab, const RxLds& L, int64_t cell,
                                        int64_t r, int k0, float tr, uint64_t& okey, double& oamp) {
-#if RT_REPLAY_DEFER_AMP
   // the B - 1 columns after the environment table in dynamic LDS (k_replay's launch sizes it)
   PathAccD acc;
   acc.cosv = reinterpret_cast<float*>(const_cast<float4*>(lds_tab) + (USE_BVH ? 0 : (size_t)p.env_nf * 18)) + threadIdx.x;
   acc.ncap = p.B - 1;
-#elif RT_REPLAY_ACC_LDS
-  __shared__ float acc_lds[6 * 256];
-  PathAccL acc;
-  acc.col = acc_lds + threadIdx.x;
-#else
-  PathAcc acc;
-#endif
   const float4 t0 = traj_p(p, r, 0);
-#if RT_REPLAY_DEFER_AMP
   acc.start(t0.x, t0.y, t0.z);  // p_0 = tx
-#else
-  acc.start(t0.x, t0.y, t0.z, p.amp0);  // p_0 = tx
-#endif
   for (int q = 1; q <= k0; ++q) {       // environment prefix p_1 .. p_k0
     const float4 tq = traj_p(p, r, q);
     acc.add(tq.x, tq.y, tq.z);
@@ -1215,11 +878,7 @@ __device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab
   pos.z = fmaf(dir.z, tr, pos.z);
   acc.add(pos.x, pos.y, pos.z);
   float rec_dist = acc.dist;
-#if RT_REPLAY_DEFER_AMP
   int rec_nint = acc.nint;
-#else
-  double rec_amp = acc.amp;
-#endif
   float3 d = dir;
   for (int b = k0 + 1; b < p.B; ++b) {  // kernel.py:57-98 with this cell's receiver
     const rt::Shear s = rt::make_shear(pos, d);
@@ -1227,8 +886,8 @@ __device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab
     // receiver first: at the last bounce only a receiver hit can still change the record, so a
     // miss there ends the path without the environment query (K3: most first wins at bounce 0
     // leave their receiver at bounce 1 and miss it at bounce 2)
-    hr = USE_BVH ? rx_query_v<RT_COV_RXQ_BVH>(L, p.g, cell, p.r_rx, pos, d)
-                 : rx_query_v<RT_COV_RXQ, RT_COV_REPLAY_WAVES >= 4>(L, p.g, cell, p.r_rx, pos, d);
+    hr = USE_BVH ? rx_query_culled(L, p.g, cell, p.r_rx, pos, d)
+                 : rx_query_culled<true>(L, p.g, cell, p.r_rx, pos, d);
     if (hr.face < 0 && b + 1 >= p.B) break;
     if constexpr (RX_FIRST) {
       // the environment culled at the receiver's t: every environment hit with t <= hr.t is
@@ -1245,11 +904,7 @@ __device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab
       pos.z = fmaf(d.z, hr.t, pos.z);
       acc.add(pos.x, pos.y, pos.z);
       rec_dist = acc.dist;  // received_paths = traced prefix through this point (kernel.py:89-90)
-#if RT_REPLAY_DEFER_AMP
       rec_nint = acc.nint;
-#else
-      rec_amp = acc.amp;
-#endif
     } else if (env_hit) {
       // after the last bounce only a receiver hit could still change the record: an environment
       // hit there ends the path, its vertex (and its angle's f64 amplitude) unused
@@ -1268,9 +923,7 @@ __device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab
       break;
     }
   }
-#if RT_REPLAY_DEFER_AMP
   const double rec_amp = amp_product(acc.cosv, rec_nint, p.amp0);
-#endif
   double dl;
   if (p.flags & RT_CIR_C_F64) {
     dl = ((double)rec_dist / p.c64) * p.fs64;
@@ -1291,9 +944,8 @@ __device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab
 // replayed in a coherent order by k_replay.  (Replaying inside this kernel on brute-force scenes
 // measured 37% slower on K3, 10.1 vs 7.4 ms per map: the replay's divergent tail and registers
 // held every candidate's wave.)
-#ifndef RT_WIN_WAVES
-#define RT_WIN_WAVES 6  // 80 VGPRs, spill-free with the dot-form ball test: K3 k_win 0.935 -> 0.895 ms, K5 0.79 -> 0.76 (r3ze); before it, 5 waves (96 VGPRs, 60 B scratch) beat 4 and 6: 1.03 -> 0.98 ms (r2zj)
-#endif
+// 6 waves per SIMD: 80 VGPRs, spill-free with the dot-form ball test: K3 k_win 0.935 -> 0.895 ms, K5
+// 0.79 -> 0.76 (r3ze); before it, 5 waves (96 VGPRs, 60 B scratch) beat 4 and 6: 1.03 -> 0.98 ms (r2zj)
 // candidates of this attempt, 0 if they overflowed the buffers (k_win, the first-win list and the
 // early replay then do nothing: a lane's keys that would cross the capacity are not written, and
 // reading the hole took the replay to illegal addresses in the N = 4 one-GPU rehearsal)
@@ -1301,7 +953,7 @@ __device__ __forceinline__ int64_t cand_count(const unsigned long long* n_dev, i
   const int64_t n = (int64_t)*n_dev;
   return n > cap ? 0 : n;
 }
-__global__ __launch_bounds__(256, RT_WIN_WAVES) void k_win(CovParams p, const uint64_t* keys, const unsigned long long* nkeys_dev,
+__global__ __launch_bounds__(256, 6) void k_win(CovParams p, const uint64_t* keys, const unsigned long long* nkeys_dev,
                                              int64_t cap, uint8_t* first_flag, float* trx) {
   __shared__ RxLds L;
   stage_rx(L, p.r_rx);
@@ -1406,22 +1058,9 @@ __global__ __launch_bounds__(256) void k_sel_scatter(const uint8_t* flag, const 
 // Replay order key of list entry li.  A wave runs as long as its lane with the most bounces left
 // after the first win, so the remaining bounce count (2 bits) leads; then the ray's direction at
 // its first win (8x8 octahedral cell) and the cell's coarse position (16x16 Morton), so the lanes
-// of a wave walk nearby BVH paths.  (RT_COV_BVH_DIRKEY=1 restores direction over a 32x32 Morton
-// cell for BVH scenes: k_replay<true> 3564 vs 3468 us on K5.)  Only the processing order changes:
-// records are written at li.
-#ifndef RT_COV_BVH_DIRKEY
-#define RT_COV_BVH_DIRKEY 0
-#endif
-// RT_REPLAY_RAY_KEY (brute-force scenes): after the bounces left, the ray's trajectory slot
-// instead of direction and cell.  The LDS brute force tests every face whatever the direction, so
-// direction coherence buys little there, while slot order makes a wave's trajectory, key and trx
-// reads fall on shared lines (K3 k_replay<false> fetched 1.24 GB per launch at L2 hit 0.19).
-#ifndef RT_REPLAY_RAY_KEY
-#define RT_REPLAY_RAY_KEY 0
-#endif
-#ifndef RT_REPLAY_LONG_FIRST
-#define RT_REPLAY_LONG_FIRST 0
-#endif
+// of a wave walk nearby BVH paths.  Only the processing order changes: records are written at li.
+// (Direction over a 32x32 Morton cell, the ray slot instead of direction and cell on brute-force
+// scenes, and the longest replays first were measured no better and removed in round 5.)
 template <bool USE_BVH>
 __device__ __forceinline__ uint16_t replay_key(const CovParams& p, uint64_t key) {
   {
@@ -1443,14 +1082,7 @@ __device__ __forceinline__ uint16_t replay_key(const CovParams& p, uint64_t key)
     uint32_t mz = 0;
 #pragma unroll
     for (int b = 0; b < 5; ++b) mz |= ((cx >> b) & 1u) << (2 * b) | ((cy >> b) & 1u) << (2 * b + 1);
-    if (USE_BVH && RT_COV_BVH_DIRKEY) return (uint16_t)((dy * 8 + dx) << 10 | mz);
-    // bounces left, in 2 bits; RT_REPLAY_LONG_FIRST: the most first (a window's longest replays
-    // start first, so the kernel's last waves are short ones)
-    const uint32_t rem0 = (uint32_t)min(max(p.B - 1 - k0, 0), 3), rem = RT_REPLAY_LONG_FIRST ? 3u - rem0 : rem0;
-    if (!USE_BVH && RT_REPLAY_RAY_KEY) {  // brute force: the ray's trajectory slot after the bounces left
-      const int sh = max(0, 32 - __clz((int)max(p.n - 1, (int64_t)1)) - 14);
-      return (uint16_t)(rem << 14 | ((uint32_t)(r >> sh) & 0x3FFFu));
-    }
+    const uint32_t rem = (uint32_t)min(max(p.B - 1 - k0, 0), 3);  // bounces left, in 2 bits
     return (uint16_t)(rem << 14 | (dy * 8 + dx) << 8 | mz >> 2);
   }
 }
@@ -1463,63 +1095,44 @@ __global__ __launch_bounds__(256) void k_replay_keys(CovParams p, const ReplayIt
   }
 }
 
-// The replay order by windows (RT_REPLAY_WINDOW): list entries [w W, (w + 1) W), W = 1024 *
-// RT_REPLAY_WIN_ITEMS, sorted by replay_key inside the window by one 1024-thread block in LDS --
-// one launch instead of k_replay_keys and a device-wide radix sort (hipCUB: ~8 launches and fills,
-// ~100 us per K3 rank of 8, profiles/r3b_k3.timeline.txt).  A wave still gets lanes with the same
-// bounces left and nearby directions and cells, from its window instead of from the whole list.
-#ifndef RT_REPLAY_WINDOW
-#define RT_REPLAY_WINDOW 1
-#endif
-#ifndef RT_REPLAY_WIN_ITEMS
-#define RT_REPLAY_WIN_ITEMS 4  // 4096-entry windows: twice the blocks for a rank's list; K5 rank of 8 1.088 -> 1.003 ms, K3 0.99 -> 0.92 (r4c)
-#endif
-constexpr int kReplayWin = 1024 * RT_REPLAY_WIN_ITEMS;
-// Larger lists (one GPU's whole map: K3 7.9M, K5 6.4M first wins) keep the device-wide sort: there
-// the windows cost more replay coherence than the sort's launches (K5 map 4.73 -> 5.21 ms with
-// windows, K3 4.94 -> 5.13 ms; a K3 rank of 8: order 105 -> 36 us, replay 310 -> 319 us;
-// profiles/r3d_*).
-#ifndef RT_REPLAY_WINDOW_MAX
-#define RT_REPLAY_WINDOW_MAX (1 << 21)
-#endif
-constexpr int64_t kReplayWindowMax = RT_REPLAY_WINDOW_MAX;
-#ifndef RT_REPLAY_EARLY
-#define RT_REPLAY_EARLY 1
-#endif
-// RT_REPLAY_ORDER_IDX: the window order writes the processing order (4-B item indices) and the
-// replay gathers its items through it, inside the window just read (L2-resident); 0: the order
-// kernel copies the 16-B items themselves (K3 rank: order 19 -> 37 us, replay 266 -> 258 us)
-#ifndef RT_REPLAY_ORDER_IDX
-#define RT_REPLAY_ORDER_IDX 1
-#endif
+// The replay order by windows: list entries [w W, (w + 1) W), W = 1024 * kReplayWinItems, sorted by
+// replay_key inside the window by one 1024-thread block in LDS -- one launch instead of
+// k_replay_keys and a device-wide radix sort (hipCUB: ~8 launches and fills, ~100 us per K3 rank of
+// 8, profiles/r3b_k3.timeline.txt).  A wave still gets lanes with the same bounces left and nearby
+// directions and cells, from its window instead of from the whole list.  The order kernel writes
+// the processing order (4-B item indices) and the replay gathers its items through it, inside the
+// window just read (L2-resident; copying the 16-B items instead: K3 rank order 19 -> 37 us).
+// 4096-entry windows: twice the blocks for a rank's list (K5 rank of 8 1.088 -> 1.003 ms, K3 0.99 ->
+// 0.92, r4c).  Larger lists (one GPU's whole map: K3 7.9M, K5 6.4M first wins) keep the
+// device-wide sort: there the windows cost more replay coherence than the sort's launches (K5 map
+// 4.73 -> 5.21 ms with windows, K3 4.94 -> 5.13 ms; profiles/r3d_*).
+constexpr int kReplayWinItems = 4;
+constexpr int kReplayWin = 1024 * kReplayWinItems;
+constexpr int64_t kReplayWindowMax = 1 << 21;
 template <bool USE_BVH>
 __global__ __launch_bounds__(1024) void k_replay_order(CovParams p, const ReplayItem* items, int64_t nl,
-                                                       const unsigned long long* nl_dev, ReplayItem* sorted,
-                                                       int32_t* order) {
-  using Sort = rocprim::block_radix_sort<uint16_t, 1024, RT_REPLAY_WIN_ITEMS, int32_t>;
+                                                       const unsigned long long* nl_dev, int32_t* order) {
+  using Sort = rocprim::block_radix_sort<uint16_t, 1024, kReplayWinItems, int32_t>;
   __shared__ typename Sort::storage_type st;
   if (nl_dev) nl = min(nl, (int64_t)*nl_dev);  // launched before the host knows the list length
   if ((int64_t)blockIdx.x * kReplayWin >= nl) return;
-  const int64_t base = (int64_t)blockIdx.x * kReplayWin + (int64_t)threadIdx.x * RT_REPLAY_WIN_ITEMS;
-  uint16_t k[RT_REPLAY_WIN_ITEMS];
-  int32_t v[RT_REPLAY_WIN_ITEMS];
+  const int64_t base = (int64_t)blockIdx.x * kReplayWin + (int64_t)threadIdx.x * kReplayWinItems;
+  uint16_t k[kReplayWinItems];
+  int32_t v[kReplayWinItems];
 #pragma unroll
-  for (int i = 0; i < RT_REPLAY_WIN_ITEMS; ++i) {
+  for (int i = 0; i < kReplayWinItems; ++i) {
     const int64_t li = base + i;
     k[i] = li < nl ? replay_key<USE_BVH>(p, items[li].key) : (uint16_t)0xFFFF;
     v[i] = (int32_t)li;
   }
   Sort().sort(k, v, st);
 #pragma unroll
-  for (int i = 0; i < RT_REPLAY_WIN_ITEMS; ++i) {  // the window's items, just read: L2-resident
-    if (base + i >= nl) continue;
-    if (order) order[base + i] = v[i];
-    else sorted[base + i] = items[v[i]];
-  }
+  for (int i = 0; i < kReplayWinItems; ++i)
+    if (base + i < nl) order[base + i] = v[i];
 }
 
 template <bool USE_BVH, bool RX_FIRST>
-__global__ __launch_bounds__(256, USE_BVH ? RT_COV_REPLAY_WAVES_BVH : RT_COV_REPLAY_WAVES) void k_replay(CovParams p, const ReplayItem* items,
+__global__ __launch_bounds__(256, USE_BVH ? kReplayWavesBvh : kReplayWaves) void k_replay(CovParams p, const ReplayItem* items,
                                                 int64_t nl, const unsigned long long* nl_dev,
                                                 const int32_t* order, uint64_t* out_key, double* out_amp) {
   extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
@@ -1607,9 +1220,6 @@ __global__ __launch_bounds__(256) void k_merge_segments(const uint64_t* keys, in
 // so a thread waits `steps` memory latencies instead of (nseg - 1) x steps -- the searches over
 // L2-resident keys are a chain of dependent loads, and k_merge_segments' time was that chain
 // (52 us for a K5 owner's 465k records, profiles/r3zg_k5_rank_timeline.txt).
-#ifndef RT_MERGE_LOCKSTEP
-#define RT_MERGE_LOCKSTEP 1
-#endif
 template <int NS>
 __global__ __launch_bounds__(256) void k_merge_lockstep(const uint64_t* keys, int64_t kstride, SegOffsets so,
                                                         int steps, uint64_t* keys_out, int64_t* idx_out) {
@@ -1841,37 +1451,9 @@ __global__ __launch_bounds__(256) void k_cell_ranges(const uint64_t* ukeys, cons
 }
 
 constexpr int kPowLds = 192;  // terms per wave staged in LDS (3 per lane); larger cells read global memory
-#ifndef RT_POW_SMALL
-#define RT_POW_SMALL 16
-#endif
-constexpr int kPowSmall = RT_POW_SMALL;  // cells with at most this many terms: one thread each (k_power_small)
-// RT_POW_SMALL_LDS: k_power_small first copies each thread's terms into its LDS column (independent
-// loads, one memory latency), then sweeps them there -- instead of a chain of dependent global
-// loads per interval (~37 us for a K3 rank's 8k cells, profiles/r3e_k3.timeline.txt)
-#ifndef RT_POW_SMALL_LDS
-#define RT_POW_SMALL_LDS 0  // measured: K3 rank 37 -> 33 us, but K5 rank 42 -> 65 us (53 KB of LDS: 3 waves per CU), r3f
-#endif
-struct LdsTerms {  // a thread's terms k = lo .. lo + K - 1 at column `lane` of the block's arrays
-  const int32_t (*sm)[64];
-  const double (*sc)[64];
-  const double (*ss)[64];
-  const double (*sev)[4][64];
-  int64_t lo;
-  int lane;
-  __device__ __forceinline__ int64_t m(int64_t k) const { return sm[k - lo][lane]; }
-  __device__ __forceinline__ void cs(int64_t k, double& c, double& s) const {
-    c = sc[k - lo][lane];
-    s = ss[k - lo][lane];
-  }
-  __device__ __forceinline__ void start(int64_t k, double& s, double& c) const {
-    s = sev[k - lo][0][lane];
-    c = sev[k - lo][1][lane];
-  }
-  __device__ __forceinline__ void stop(int64_t k, double& s, double& c) const {
-    s = sev[k - lo][2][lane];
-    c = sev[k - lo][3][lane];
-  }
-};
+constexpr int kPowSmall = 16;  // cells with at most this many terms: one thread each (k_power_small)
+// (Copying each thread's terms into its LDS column first measured K3 rank 37 -> 33 us but K5 rank
+// 42 -> 65 us -- 53 KB of LDS, 3 waves per CU; r3f.  Removed in round 5.)
 
 // cells of ours with 0..kPowSmall terms: one thread per cell, serial sweep (most cells of a large
 // map receive a handful of bins; a wave per such cell costs more than its whole sweep)
@@ -1903,20 +1485,7 @@ __global__ __launch_bounds__(64) void k_power_small(TermArrays G, const int32_t*
       const bool has = cepoch[c] == epoch;
       const int64_t lo = has ? cstart[c] : 0, hi = has ? cend[c] : 0;
       if (hi - lo <= kPowSmall) {
-#if RT_POW_SMALL_LDS
-        __shared__ int32_t sm[kPowSmall][64];
-        __shared__ double sc[kPowSmall][64], ss[kPowSmall][64], sev[kPowSmall][4][64];
-        const int K = (int)(hi - lo);
-        for (int k = 0; k < K; ++k) {
-          sm[k][lane] = (int32_t)G.m(lo + k);
-          sc[k][lane] = G.tcos[lo + k];
-          ss[k][lane] = G.tsin[lo + k];
-          for (int r = 0; r < 4; ++r) sev[k][r][lane] = G.ev[4 * (lo + k) + r];
-        }
-        power[c] = power_sparse(lo, hi, P, LdsTerms{sm, sc, ss, sev, lo, lane});  // NaN when empty
-#else
         power[c] = power_sparse(lo, hi, P, G);  // NaN when empty
-#endif
       } else {
         is_big = true;
       }
@@ -2168,7 +1737,7 @@ struct rt_coverage {
   uint8_t* first_flag = nullptr;
   float* trx = nullptr;
   int64_t* list = nullptr;
-  ReplayItem *ritems = nullptr, *ritems_sorted = nullptr;  // first wins (candidate order / processing order)
+  ReplayItem* ritems = nullptr;  // first wins, in candidate order
   uint64_t* items = nullptr;
   int64_t item_cap = 0;
   unsigned long long* counters = nullptr;  // [0] candidates, [1] column items, [2] replay list (int64)
@@ -2178,7 +1747,6 @@ struct rt_coverage {
   int64_t cap = 0;
   int64_t last_candidates = 0;
   int64_t last_list = 0;  // first wins of the last run (sizes the early replay's grid)
-  int64_t last_items = -1;  // column items of the last run (k_cols' write mode), -1: none yet
   int64_t last_received = 0;  // first-win (cell, ray) records of the last run
   void* rord = nullptr;        // replay-order sort workspace (16-bit keys + int32 rows, x2, + hipCUB)
   size_t rord_bytes = 0;
@@ -2286,19 +1854,8 @@ __host__ __device__ __forceinline__ double fx_to_double(const Fx192& x) {
 }
 
 // The exact sums of the runs of equal keys in sorted records, in place of a generic reduce-by-key
-// (rocPRIM's took 357 us per 7.9M records with the 24-B fixed-point value, 127 us with f64):
-//   k_run_flags   head flag of every record (its key differs from the previous one)
-//   inclusive scan of the flags (rocPRIM, int32): the run index of every record, and the run count
-//   k_run_starts  the first record of every run
-//   k_run_sums    one thread per run of <= 64 records: serial sum; longer runs get a long-run id
-//                 (the transmitter cells' bins collect ~1M records each)
-//   k_long_spans  one wave per span of 512 records, 64-record tiles: a tile meets at most two long
-//                 runs (its first and last record's); runs inside the span are summed whole, the
-//                 pieces of the runs crossing the span's edges go to per-span head/tail slots
-//   k_long_final  assembles the runs crossing spans from their pieces
-// Integer sums throughout, so neither the tiling nor the atomics' order changes a bit.
-constexpr int kShortRun = 64;  // > 64: a 64-record tile meets at most two such runs
-
+// (rocPRIM's took 357 us per 7.9M records with the 24-B fixed-point value, 127 us with f64).
+// Integer sums throughout, so the tiling cannot change a bit.
 struct AmpVal {  // sorted replay records: f64 amplitudes
   const double* a;
   __device__ __forceinline__ Fx192 operator()(int64_t i) const { return fx_from_double(a[i]); }
@@ -2313,131 +1870,7 @@ struct SumVal {  // received records: fixed-point sums, in sorted-index order
   }
 };
 
-__global__ __launch_bounds__(256) void k_run_flags(const uint64_t* keys, int64_t n, int32_t* flags) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    flags[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1 : 0;
-}
-__global__ __launch_bounds__(256) void k_run_starts(const int32_t* flags, const int32_t* scan, int64_t n,
-                                                    int32_t* starts, int64_t* nuniq) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    if (flags[i]) starts[scan[i] - 1] = (int32_t)i;
-    if (i == n - 1) *nuniq = scan[i];
-  }
-}
-// longid (overwrites the flags, one per run): the run's long-run id, or -1; longu[lid] = run
-template <typename Val>
-__global__ __launch_bounds__(256) void k_run_sums(const uint64_t* keys, Val val, int64_t n, const int32_t* starts,
-                                                  const int64_t* nuniq, WideKey wk, uint64_t* ukeys, Fx192* usums,
-                                                  int32_t* longid, int32_t* longu, unsigned* nlong) {
-  const int64_t nu = *nuniq;
-  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < nu; u += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t b = starts[u], e = u + 1 < nu ? starts[u + 1] : n;
-    ukeys[u] = wk(keys[b]);
-    if (e - b > kShortRun) {
-      const unsigned lid = atomicAdd(nlong, 1u);
-      longid[u] = (int32_t)lid;
-      longu[lid] = (int32_t)u;
-      continue;
-    }
-    longid[u] = -1;
-    Fx192 acc = val(b);
-    for (int64_t i = b + 1; i < e; ++i) acc = FxPlus()(acc, val(i));
-    usums[u] = acc;
-  }
-}
-// wave sum of a Fx192 (xor butterfly; every lane ends with the total)
-__device__ __forceinline__ Fx192 wave_fx_sum(Fx192 x) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    Fx192 y;
-    y.w0 = __shfl_xor(x.w0, o, 64);
-    y.w1 = __shfl_xor(x.w1, o, 64);
-    y.w2 = __shfl_xor(x.w2, o, 64);
-    x = FxPlus()(x, y);
-  }
-  return x;
-}
-constexpr int kSpanTiles = 8;  // a wave's span: 8 tiles of 64 records
-constexpr int64_t kSpan = 64 * kSpanTiles;
-
-// One wave per span of kSpan sorted records: the pieces of the long runs in the span, tile by tile
-// (a 64-record tile meets at most two long runs, its first and its last record's).  A long run
-// inside the span is written whole; the piece of a run that began in an earlier span goes to
-// head[span], that of a run beginning here and running on to tail[span].
-template <typename Val>
-__global__ __launch_bounds__(256) void k_long_spans(Val val, int64_t n, const int32_t* scan, const int32_t* starts,
-                                                    const int64_t* nuniq, const int32_t* longid,
-                                                    const unsigned* nlong, Fx192* head, Fx192* tail, Fx192* usums) {
-  if (*nlong == 0) return;
-  const int lane = threadIdx.x & 63;
-  const int64_t nspan = (n + kSpan - 1) / kSpan;
-  const int64_t nu = *nuniq;
-  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t sp = wave; sp < nspan; sp += nwave) {
-    const int64_t s0 = sp * kSpan, s1 = s0 + kSpan < n ? s0 + kSpan : n;
-    int32_t cur = -1;  // run whose piece is being summed (uniform)
-    Fx192 acc{0, 0, 0};
-    auto flush = [&]() {
-      if (cur < 0 || lane != 0) return;
-      const int64_t b = starts[cur], e = cur + 1 < nu ? starts[cur + 1] : n;
-      if (b < s0) head[sp] = acc;       // began in an earlier span (may also run past this one)
-      else if (e > s1) tail[sp] = acc;  // runs on into the next span
-      else usums[cur] = acc;            // the whole run lies inside the span
-    };
-    for (int64_t t0 = s0; t0 < s1; t0 += 64) {
-      const int64_t t1 = t0 + 64 < s1 ? t0 + 64 : s1;
-      const int64_t i = t0 + lane;
-      const int32_t u = i < t1 ? scan[i] - 1 : -1;
-      const int32_t ua = __shfl(u, 0, 64), ub = __shfl(u, (int)(t1 - t0 - 1), 64);
-      const bool la = longid[ua] >= 0, lb = ub != ua && longid[ub] >= 0;
-      if (!la && !lb) continue;
-      const Fx192 z{0, 0, 0};
-      const Fx192 v = i < t1 ? val(i) : z;
-      const Fx192 A = wave_fx_sum(la && u == ua ? v : z);
-      const Fx192 Bv = wave_fx_sum(lb && u == ub ? v : z);
-      if (la) {
-        if (cur == ua) {
-          acc = FxPlus()(acc, A);
-        } else {
-          flush();
-          cur = ua;
-          acc = A;
-        }
-      }
-      if (lb) {
-        flush();
-        cur = ub;
-        acc = Bv;
-      }
-    }
-    flush();
-  }
-}
-// every long run crossing spans: tail[its first span] + head[every later span it reaches] (a run
-// inside one span was written whole by k_long_spans)
-__global__ __launch_bounds__(256) void k_long_final(const int32_t* starts, const int64_t* nuniq, int64_t n,
-                                                    const int32_t* longu, const unsigned* nlong, const Fx192* head,
-                                                    const Fx192* tail, Fx192* usums) {
-  // one wave per long run: the transmitter cells' bins cross hundreds of spans
-  const unsigned nl = *nlong;
-  const int64_t nu = *nuniq;
-  const int lane = threadIdx.x & 63;
-  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t j = wave; j < nl; j += nwave) {
-    const int32_t u = longu[j];
-    const int64_t b = starts[u], e = u + 1 < nu ? starts[u + 1] : n;
-    const int64_t sa = b / kSpan, sb = (e - 1) / kSpan;
-    if (sa == sb) continue;  // uniform
-    Fx192 acc{0, 0, 0};
-    for (int64_t q = sa + 1 + lane; q <= sb; q += 64) acc = FxPlus()(acc, head[q]);
-    acc = wave_fx_sum(acc);
-    if (lane == 0) usums[u] = FxPlus()(acc, tail[sa]);
-  }
-}
-
-// ---- Run sums in three launches (RT_RUN_SUMS_V2, default).  The sorted records are cut into
+// ---- Run sums in three launches.  The sorted records are cut into
 // ntiles <= kMaxTiles tiles of T records (T a multiple of 64); a record is a run head when its key
 // differs from the previous record's.
 //   k_tile_heads  per tile: its number of heads
@@ -2450,10 +1883,7 @@ __global__ __launch_bounds__(256) void k_long_final(const int32_t* starts, const
 //                 headparts of the following tiles up to the first one with a head
 // Integer sums throughout (Fx192), so the tiling cannot change a bit.  The round-2 form took 7
 // launches and three passes over the records (flags, scan, starts, ...; ~90 us on a K3 rank of 8,
-// profiles/r3b_k3_rank_timeline.txt).
-#ifndef RT_RUN_SUMS_V2
-#define RT_RUN_SUMS_V2 1
-#endif
+// profiles/r3b_k3_rank_timeline.txt; removed in round 5).
 constexpr int64_t kMaxTiles = 4096;  // each wave of k_tile_sums sums the earlier tiles' heads: <= 64 per lane
 constexpr int64_t kMinTile = 256;    // 4 chunks per wave: enough waves to fill the GPU on a rank's ~1M records
 struct TileMeta {
@@ -2462,6 +1892,18 @@ struct TileMeta {
   Fx192* headpart;  // [ntiles] sum of the records before the tile's first head (whole tile if none)
   Fx192* tailpart;  // [ntiles] sum of the open run's records in the tile
 };
+// wave sum of a Fx192 (xor butterfly; every lane ends with the total)
+__device__ __forceinline__ Fx192 wave_fx_sum(Fx192 x) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    Fx192 y;
+    y.w0 = __shfl_xor(x.w0, o, 64);
+    y.w1 = __shfl_xor(x.w1, o, 64);
+    y.w2 = __shfl_xor(x.w2, o, 64);
+    x = FxPlus()(x, y);
+  }
+  return x;
+}
 __device__ __forceinline__ Fx192 shfl_fx(const Fx192& x, int src) {
   return Fx192{__shfl(x.w0, src, 64), __shfl(x.w1, src, 64), __shfl(x.w2, src, 64)};
 }
@@ -2568,7 +2010,7 @@ __global__ __launch_bounds__(256) void k_cross_tiles(int64_t ntiles, TileMeta tm
   }
 }
 
-// ---- Owner stage, runs + terms + cell ranges in one launch (RT_OWNER_FUSED).  After the segment
+// ---- Owner stage, runs + terms + cell ranges in one launch.  After the segment
 // merge, a run of equal keys holds at most one record per source rank (each rank's segment has
 // unique keys), so it is at most nseg long: the record that heads a run sums it on its own, reading
 // on past its tile's end when the run crosses it (a run that began in an earlier tile is its head's).
@@ -2578,28 +2020,14 @@ __global__ __launch_bounds__(256) void k_cross_tiles(int64_t ntiles, TileMeta tm
 // writes its key and f64 sum, its power-sweep terms (k_terms) and, at cell boundaries, the cell's
 // range (k_cell_ranges).  Replaces k_tile_heads, k_tile_sums, k_cross_tiles, k_terms and
 // k_cell_ranges (five launches) on merged segments.
-#ifndef RT_OWNER_FUSED
-#define RT_OWNER_FUSED 1
-#endif
-#ifndef RT_OWN_ITEMS
-#define RT_OWN_ITEMS 4
-#endif
-constexpr int kOwnItems = RT_OWN_ITEMS, kOwnTile = 256 * kOwnItems;
-// RT_OWNER_LOOKBACK 0: the tiles' head counts come from k_tile_heads and every block sums the
-// counts before it (no ticket, no waiting on other blocks)
-#ifndef RT_OWNER_LOOKBACK
-#define RT_OWNER_LOOKBACK 1
-#endif
-// RT_LOOKBACK_TICKET 1: tiles taken in order from a ticket counter (one same-address atomic per
-// block), so a block only ever waits on tiles that running blocks hold.  0 (tile = block index) is
-// ~13 us faster per rank of 8 on an idle GPU, but unsafe: each XCD dispatches its share of the
-// workgroups on its own, so a block can wait on a predecessor its XCD cannot place while other
-// work fills it.  With four processes on one GPU (the N = 4 rehearsal) the waits ran out, the
-// prefixes were wrong and the power sweeps read out of bounds (profiles/r4zd_rehearse_4.log; with
-// tickets: r4zf_ticket_*.log).
-#ifndef RT_LOOKBACK_TICKET
-#define RT_LOOKBACK_TICKET 1
-#endif
+constexpr int kOwnItems = 4, kOwnTile = 256 * kOwnItems;
+// Tiles are taken in order from a ticket counter (one same-address atomic per block), so a block
+// only ever waits on tiles that running blocks hold.  Taking the tile from the block index was ~13 us
+// faster per rank of 8 on an idle GPU, but unsafe: each XCD dispatches its share of the workgroups
+// on its own, so a block can wait on a predecessor its XCD cannot place while other work fills it.
+// With four processes on one GPU (the N = 4 rehearsal) the waits ran out, the prefixes were wrong
+// and the power sweeps read out of bounds (profiles/r4zd_rehearse_4.log; with tickets:
+// r4zf_ticket_*.log).  Removed in round 5 (last in commit 43de9a4).
 constexpr uint64_t kOwnAgg = 1ull << 38, kOwnInc = 2ull << 38, kOwnCount = (1ull << 38) - 1;
 constexpr uint64_t kOwnTagMask = ~(kOwnInc | kOwnAgg | kOwnCount);
 struct OwnerRuns {
@@ -2618,14 +2046,13 @@ struct OwnerRuns {
   int32_t epoch;
   unsigned* nbig;
   PowerParams P;
-  const int32_t* heads;  // RT_OWNER_LOOKBACK 0: head count of every tile
 };
 __global__ __launch_bounds__(256) void k_owner_runs(OwnerRuns a) {
   __shared__ uint32_t s_tile;
   __shared__ int s_w[4];
   __shared__ int64_t s_prefix;
   if (threadIdx.x == 0)
-    s_tile = RT_OWNER_LOOKBACK && RT_LOOKBACK_TICKET ? (uint32_t)(atomicAdd(a.ticket, 1ull) - a.ticket_base) : blockIdx.x;
+    s_tile = (uint32_t)(atomicAdd(a.ticket, 1ull) - a.ticket_base);
   if (blockIdx.x == 0 && threadIdx.x == 0) *a.nbig = 0u;  // k_power_small lists the big cells afresh
   __syncthreads();
   const int64_t tile = s_tile;
@@ -2655,25 +2082,7 @@ __global__ __launch_bounds__(256) void k_owner_runs(OwnerRuns a) {
   int before = 0;
   for (int q = 0; q < w; ++q) before += s_w[q];
   const int total = s_w[0] + s_w[1] + s_w[2] + s_w[3];
-#if !RT_OWNER_LOOKBACK
-  {  // the heads of the tiles before this one, summed by the block
-    int64_t hb = 0;
-    for (int64_t j = threadIdx.x; j < tile; j += blockDim.x) hb += a.heads[j];
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) hb += __shfl_xor(hb, o, 64);
-    __shared__ int64_t s_hb[4];
-    __syncthreads();
-    if (lane == 0) s_hb[w] = hb;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      s_prefix = s_hb[0] + s_hb[1] + s_hb[2] + s_hb[3];
-      if (i0 + kOwnTile >= a.n) *a.nuniq = s_prefix + total;
-    }
-  }
-  if (false) {
-#else
   if (w == 0) {  // the look-back, by wave 0: lane L reads the state of tile jbase - L
-#endif
     uint64_t* st = a.states + tile;
     if (lane == 0)
       __hip_atomic_store(st, a.tag | (tile == 0 ? kOwnInc : kOwnAgg) | (uint64_t)total, __ATOMIC_RELAXED,
@@ -2750,7 +2159,7 @@ __global__ __launch_bounds__(256) void k_owner_runs(OwnerRuns a) {
   }
 }
 
-// ---- Trace-stage reduce in one launch (RT_SEND_FUSED): the sorted replay records of a ray-sharded
+// ---- Trace-stage reduce in one launch: the sorted replay records of a ray-sharded
 // rank -> its unique (owner, cell, bin) keys with their exact sums, the send rows and the owner
 // bounds.  Tiles of kSendTile records in ticket order; each thread holds 4 consecutive records.  A
 // run of equal keys may be any length (a K3 rank's transmitter cell: ~125k records in one bin), so
@@ -2764,9 +2173,6 @@ __global__ __launch_bounds__(256) void k_owner_runs(OwnerRuns a) {
 // record: key, exact sum, f64, its row (packed 32 B or key + sum) and, at owner changes, the bounds.
 // Replaces k_tile_heads, k_tile_sums, k_cross_tiles and k_bounds_strip (four launches, ~50 us per
 // rank of 8, profiles/r4h_k5.timeline.txt).  Integer sums: the same bits in any grouping.
-#ifndef RT_SEND_FUSED
-#define RT_SEND_FUSED 1
-#endif
 constexpr int kSendItems = 4, kSendTile = 256 * kSendItems;
 static_assert(kSendTile == kOwnTile, "k_send_runs shares k_owner_runs' tile states");
 constexpr uint64_t kSendHead = 1ull << 37, kSendCount = (1ull << 37) - 1;
@@ -2815,7 +2221,7 @@ __global__ __launch_bounds__(256) void k_send_runs(SendRuns a) {
   __shared__ SegFx s_ws[4];
   __shared__ int64_t s_prefix;
   __shared__ Fx192 s_carry;
-  if (threadIdx.x == 0) s_tile = RT_LOOKBACK_TICKET ? (uint32_t)(atomicAdd(a.ticket, 1ull) - a.ticket_base) : blockIdx.x;
+  if (threadIdx.x == 0) s_tile = (uint32_t)(atomicAdd(a.ticket, 1ull) - a.ticket_base);
   __syncthreads();
   const int64_t tile = s_tile;
   const int64_t i0 = tile * kSendTile + (int64_t)threadIdx.x * kSendItems;
@@ -2998,22 +2404,9 @@ __global__ __launch_bounds__(256) void k_send_runs(SendRuns a) {
   }
 }
 
-hipError_t scan_flags(void* tmp, size_t& bytes, const int32_t* flags, int32_t* scan, int64_t n, hipStream_t s) {
-  return rocprim::inclusive_scan(tmp, bytes, flags, scan, (size_t)n, rocprim::plus<int32_t>(), s);
-}
-
-__global__ __launch_bounds__(256) void k_fx_to_amps(const Fx192* usums, const int64_t* nuniq, double* uamps) {
-  const int64_t nu = *nuniq;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nu; i += (int64_t)gridDim.x * blockDim.x)
-    uamps[i] = fx_to_double(usums[i]);
-}
 __global__ __launch_bounds__(256) void k_amps_to_fx(const double* amps, int64_t n, Fx192* sums) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     sums[i] = fx_from_double(amps[i]);
-}
-__global__ __launch_bounds__(256) void k_iota(int64_t n, int64_t* out) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    out[i] = i;
 }
 
 void free_cands(rt_coverage* c) {
@@ -3026,8 +2419,7 @@ void free_cands(rt_coverage* c) {
   for (void* q : {(void*)c->keys, (void*)c->keys_sorted, (void*)c->okeys, (void*)c->okeys_sorted, (void*)c->ukeys,
                   (void*)c->oamps, (void*)c->oamps_sorted, (void*)c->uamps, (void*)c->tcos, (void*)c->tsin, (void*)c->ev,
                   (void*)c->win, (void*)c->trx,
-                  (void*)c->list, (void*)c->first_flag, c->tmp, c->rord, (void*)c->runs, (void*)c->ritems,
-                  (void*)c->ritems_sorted})
+                  (void*)c->list, (void*)c->first_flag, c->tmp, c->rord, (void*)c->runs, (void*)c->ritems})
     if (q) (void)hipFree(q);
   c->keys = c->keys_sorted = c->okeys = c->okeys_sorted = c->ukeys = nullptr;
   c->oamps = c->oamps_sorted = c->uamps = c->tcos = c->tsin = c->ev = nullptr;
@@ -3035,7 +2427,7 @@ void free_cands(rt_coverage* c) {
   c->first_flag = nullptr;
   c->trx = nullptr;
   c->list = nullptr;
-  c->ritems = c->ritems_sorted = nullptr;
+  c->ritems = nullptr;
   c->runs = nullptr;
   if (c->own_states) (void)hipFree(c->own_states);
   c->own_states = nullptr;
@@ -3058,22 +2450,11 @@ size_t rord_row_bytes(int64_t n) { return ((size_t)n * 4 + 255) / 256 * 256; }
 // stage's ~0.7M records on 51 bits take 238 us merged vs ~205 us by Onesweep; the owner stage's
 // ~0.2M (31 bits) are faster merged (owner stage 0.23 vs 0.29 ms) and K5's ~0.47M (36 bits) by
 // Onesweep (0.46 vs 0.50 ms).  So: Onesweep from 300k items, rocprim's default below.
-#ifndef RT_SORT_RADIX_BITS
-#define RT_SORT_RADIX_BITS 10  // 0: rocprim's gfx950 default, 8 bits per pass (tools/gpu_sortvar.sh: 10 bits, 1024-thread blocks, K5 rank of 8 1.58 -> 1.53 ms)
-#endif
-#if RT_SORT_RADIX_BITS
-#ifndef RT_SORT_HIST_BLOCK
-#define RT_SORT_HIST_BLOCK 1024
-#endif
-#ifndef RT_SORT_BLOCK
-#define RT_SORT_BLOCK 1024
-#endif
+// 10-bit digits and 1024-thread blocks (rocprim's gfx950 default is 8 bits per pass;
+// tools/gpu_sortvar.sh: K5 rank of 8 1.58 -> 1.53 ms)
 using OnesweepCfg =
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<RT_SORT_HIST_BLOCK, 8>, rocprim::kernel_config<RT_SORT_BLOCK, 8>,
-                                        RT_SORT_RADIX_BITS, rocprim::block_radix_rank_algorithm::match>;
-#else
-using OnesweepCfg = rocprim::default_config;
-#endif
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 8>, rocprim::kernel_config<1024, 8>, 10,
+                                        rocprim::block_radix_rank_algorithm::match>;
 using OnesweepOnly = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, OnesweepCfg, 0>;
 constexpr int64_t kOnesweepMinItems = 300000;
 template <typename V>
@@ -3102,8 +2483,7 @@ int alloc_cands(rt_coverage* c, int64_t cap) {
   RT_HIP(hipMalloc(&c->trx, cap * 4));
   RT_HIP(hipMalloc(&c->list, cap * 8));
   RT_HIP(hipMalloc(&c->ritems, cap * sizeof(ReplayItem)));
-  RT_HIP(hipMalloc(&c->ritems_sorted, cap * sizeof(ReplayItem)));
-  RT_HIP(hipMalloc(&c->runs, (cap * 3 + 64) * 4));  // run flags, their scan, run starts, long-run list
+  RT_HIP(hipMalloc(&c->runs, (cap * 3 + 64) * 4));  // tile heads / open-run indices (run_sums), counters
   // k_owner_runs' states: zero = no tag (tags start at 1 << 40)
   RT_HIP(hipMalloc(&c->own_states, ((size_t)cap / kOwnTile + 2) * 8));
   RT_HIP(hipMemset(c->own_states, 0, ((size_t)cap / kOwnTile + 2) * 8));
@@ -3119,8 +2499,7 @@ int alloc_cands(rt_coverage* c, int64_t cap) {
   size_t b2i = 0;  // the owner stage sorts (key, record index) pairs
   RT_HIP(sort_records(nullptr, b2i, c->okeys, c->okeys_sorted, (const int64_t*)c->oamps, (int64_t*)c->oamps_sorted, cap,
                       64, 0));
-  RT_HIP(scan_flags(nullptr, b3, c->runs, c->runs, cap, 0));
-  b3 = std::max(b3, b2i);
+  b3 = b2i;
   c->tmp_bytes = std::max(std::max(b1, b2), b3);
   RT_HIP(hipMalloc(&c->tmp, c->tmp_bytes));
   // replay-order sort workspace for up to cap records (one allocation per growth, not per run)
@@ -3156,7 +2535,7 @@ int poison_plan(rt_coverage* c, hipStream_t s) {
               {c->oamps_sorted, (size_t)c->cap * 8}, {c->uamps, (size_t)c->cap * 8}, {c->tcos, (size_t)c->cap * 8},
               {c->tsin, (size_t)c->cap * 8}, {c->ev, (size_t)c->cap * 32}, {c->first_flag, (size_t)c->cap},
               {c->trx, (size_t)c->cap * 4}, {c->list, (size_t)c->cap * 8},
-              {c->ritems, (size_t)c->cap * sizeof(ReplayItem)}, {c->ritems_sorted, (size_t)c->cap * sizeof(ReplayItem)}, {c->items, (size_t)c->item_cap * 8},
+              {c->ritems, (size_t)c->cap * sizeof(ReplayItem)}, {c->items, (size_t)c->item_cap * 8},
               {c->tmp, c->tmp_bytes}, {c->rord, c->rord_bytes}, {c->counters, 32}, {c->nuniq, 8},
               {c->cstart, sizeof(int32_t) * (size_t)nc}, {c->cend, sizeof(int32_t) * (size_t)nc},
               {c->bigcells, sizeof(int32_t) * (size_t)nc}, {c->cepoch, sizeof(int32_t) * (size_t)nc},
@@ -3294,10 +2673,6 @@ WideKey wide_key(const rt_coverage* c, const KeyBits& k, bool owner_local = true
 
 // Stages 1-4 (trajectories, candidates, exact receiver tests, replay): the first-win records of
 // this plan's rays as (compact record key, amplitude) in c->okeys / c->oamps, in candidate order.
-// RT_COV_ZBAND: the plan's ray order puts the most nearly horizontal rays first (dir_order_banded)
-#ifndef RT_COV_ZBAND
-#define RT_COV_ZBAND 1  // K5 rank of 8 1.031 -> 0.982 ms, K5 map 3.77 -> 3.68 ms (same box, r4z3 vs r4z3_zband)
-#endif
 int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double light_speed, double sample_rate,
                 int flags, int64_t n_bins, hipStream_t s, int64_t* ncand_out, int64_t* nlist_out) {
   CovParams p{};
@@ -3338,7 +2713,7 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
   p.n_bins = n_bins;
   const size_t lds = bvh ? 0 : (size_t)p.env_nf * 18 * sizeof(float4);
   // k_replay: the deferred amplitude's B - 1 cosine columns follow the environment table
-  const size_t lds_replay = lds + (RT_REPLAY_DEFER_AMP ? (size_t)std::max(p.B - 1, 1) * 256 * sizeof(float) : 0);
+  const size_t lds_replay = lds + (size_t)std::max(p.B - 1, 1) * 256 * sizeof(float);
   const unsigned grid_rays = (unsigned)std::min<int64_t>((c->n + 255) / 256, 4096);
   p.order = nullptr;
   p.zero_ctr = c->counters;  // zeroed by the trajectory kernel (first attempt; retries use a fill)
@@ -3347,20 +2722,21 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
     // The order depends only on the plan's ray ids (their initial directions, kernel.py:51-52), so
     // the plan sorts once, on its first run, and keeps the permutation (rt_trace, which has no
     // plan, sorts per call).  K5: ~0.1 ms per one-GPU map, a fixed ~30 us per rank of 8.
+    // The plan's ray order puts the most nearly horizontal rays first (dir_order_banded: K5 rank of 8
+    // 1.031 -> 0.982 ms, K5 map 3.77 -> 3.68 ms, r4z3); it depends only on the plan's ray ids, so the
+    // library computes it once (dir_order_cached) and the plan keeps its own copy (the library's
+    // entries may be evicted).
     if (!c->ray_order) {
-      void* ws = nullptr;
-      const int32_t* o = RT_COV_ZBAND ? rt::dir_order_banded(c->ray_offset, c->n, s, &ws)
-                                      : rt::dir_order(c->ray_offset, c->n, s, &ws);
+      const int32_t* o = rt::dir_order_cached(c->ray_offset, c->n, s);
       if (!o) return RT_EHIP;
       RT_HIP(hipMalloc(&c->ray_order, sizeof(int32_t) * (size_t)c->n));
       RT_HIP(hipMemcpyAsync(c->ray_order, o, sizeof(int32_t) * (size_t)c->n, hipMemcpyDeviceToDevice, s));
-      RT_HIP(hipFreeAsync(ws, s));
     }
     p.order = c->ray_order;
     prof_mark(c, 0, s);
     if (c->n <= traj_split_max_rays())  // too few rays to fill the GPU: four lanes per ray
-      hipLaunchKernelGGL(k_traj_split<RT_TRAJ_SPLIT_G>,
-                         dim3((unsigned)std::min<int64_t>((RT_TRAJ_SPLIT_G * c->n + 255) / 256, 8192)), dim3(256), 0,
+      hipLaunchKernelGGL(k_traj_split<kTrajSplitG>,
+                         dim3((unsigned)std::min<int64_t>((kTrajSplitG * c->n + 255) / 256, 8192)), dim3(256), 0,
                          s, p);
     else
       hipLaunchKernelGGL(k_traj<true>, dim3(grid_rays), dim3(256), lds, s, p);
@@ -3368,9 +2744,9 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
     p.order = nullptr;
   } else {
     prof_mark(c, 0, s);
-    if (RT_TRAJ_LDS_SPLIT > 1 && c->n <= traj_split_max_rays())  // few rays: G lanes per ray
-      hipLaunchKernelGGL(k_traj_lds_split<RT_TRAJ_LDS_SPLIT>,
-                         dim3((unsigned)std::min<int64_t>((RT_TRAJ_LDS_SPLIT * c->n + 255) / 256, 8192)), dim3(256),
+    if (c->n <= traj_split_max_rays())  // few rays: G lanes per ray
+      hipLaunchKernelGGL(k_traj_lds_split<kTrajLdsSplit>,
+                         dim3((unsigned)std::min<int64_t>((kTrajLdsSplit * c->n + 255) / 256, 8192)), dim3(256),
                          lds, s, p);
     else
       hipLaunchKernelGGL(k_traj<false>, dim3(grid_rays), dim3(256), lds, s, p);
@@ -3391,12 +2767,9 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
   }
   p.bin_bits = kb.bin;
   p.cell_bits = kb.cell;
-  int64_t ncand = 0, nrec = 0, nlist = 0, nitems_last = -1;
+  int64_t ncand = 0, nrec = 0, nlist = 0;
   const unsigned grid_items = 4096;
-  // k_cols writes a block's items cooperatively when rays average more than RT_COLS_SPANS_MIN items
-  // (K3: a room's segments cross many columns), else each lane its own few (K5's terrain)
-  p.cols_spans = c->last_items < 0 || c->last_items > (int64_t)RT_COLS_SPANS_MIN * c->n ? 1 : 0;
-  // Replay launched before the list length reaches the host (RT_REPLAY_EARLY): the kernels read it
+  // Replay launched before the list length reaches the host (early replay): the kernels read it
   // from the device counter, so the host's counter read-back and its wake-up (~36 us per K3 rank
   // of 8, profiles/r3j_k3.timeline.txt) overlap the replay instead of idling the GPU.  Only for
   // lists the window order takes (a rank's share); the whole-map lists keep the device-wide sort,
@@ -3410,15 +2783,12 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
     uint16_t* k_out = (uint16_t*)((char*)ws + kbs);
     int32_t* v_in = (int32_t*)((char*)ws + 2 * kbs);
     int32_t* v_out = (int32_t*)((char*)ws + 2 * kbs + rbs);
-    int32_t* worder = RT_REPLAY_ORDER_IDX ? v_out : nullptr;
     if (windows) {
       const unsigned grid_w = (unsigned)((nl + kReplayWin - 1) / kReplayWin);
       if (bvh)
-        hipLaunchKernelGGL(k_replay_order<true>, dim3(grid_w), dim3(1024), 0, s, p, c->ritems, nl, nl_dev,
-                           c->ritems_sorted, worder);
+        hipLaunchKernelGGL(k_replay_order<true>, dim3(grid_w), dim3(1024), 0, s, p, c->ritems, nl, nl_dev, v_out);
       else
-        hipLaunchKernelGGL(k_replay_order<false>, dim3(grid_w), dim3(1024), 0, s, p, c->ritems, nl, nl_dev,
-                           c->ritems_sorted, worder);
+        hipLaunchKernelGGL(k_replay_order<false>, dim3(grid_w), dim3(1024), 0, s, p, c->ritems, nl, nl_dev, v_out);
     } else {
       if (bvh)
         hipLaunchKernelGGL(k_replay_keys<true>, dim3(grid_l), dim3(256), 0, s, p, c->ritems, nl, k_in, v_in);
@@ -3428,9 +2798,9 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
                                                 (int)nl, 0, 16, s));
     }
     prof_mark(c, 4, s);
-    // the window order wrote the items in processing order; the device-wide sort gives an order
-    const ReplayItem* rit = windows && !worder ? c->ritems_sorted : c->ritems;
-    const int32_t* rord = windows ? worder : v_out;
+    // the processing order (window order or the device-wide sort) of the items
+    const ReplayItem* rit = c->ritems;
+    const int32_t* rord = v_out;
     // BVH scenes: receiver first, the traversal culled at its t (K5 replay 3.47 -> 2.7 ms); the
     // LDS brute force tests every face anyway (a plane-culled variant measured 5% slower on K3,
     // a receiver-first one skipping faces beyond the receiver's t 5% slower too: 2.50 vs 2.63 ms,
@@ -3481,7 +2851,7 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
     // which needs the length on the host.  The previous run's length (or the cap) sizes the grid and
     // vetoes the window order once a rank's list outgrows kReplayWindowMax; the kernels stride over
     // the device count either way, so a stale length costs time, never correctness.
-    replayed = RT_REPLAY_EARLY && RT_REPLAY_WINDOW && c->ray_mode && c->nshard > 1 &&
+    replayed = c->ray_mode && c->nshard > 1 &&
                (c->last_list > 0 ? c->last_list : c->cap) <= kReplayWindowMax;
     if (replayed) {
       int rc = launch_replay(c->cap, (const unsigned long long*)c->counters + 2, true,
@@ -3492,7 +2862,6 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
     const unsigned long long h[3] = {c->hcnt[0], c->hcnt[1], c->hcnt[2]};
     ncand = (int64_t)h[0];
     const int64_t nitems = (int64_t)h[1];
-    nitems_last = nitems;
     nlist = (int64_t)h[2];
     if (ncand <= c->cap && nitems <= c->item_cap) break;
     if (attempt >= 3) {
@@ -3513,12 +2882,11 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
   }
   c->last_candidates = ncand;
   c->last_list = nlist;
-  c->last_items = nitems_last;
   *ncand_out = ncand;
   if (ncand > 0) {
     if (nlist > 0) {
       if (!replayed) {
-        int rc = launch_replay(nlist, nullptr, RT_REPLAY_WINDOW && nlist <= kReplayWindowMax, nlist);
+        int rc = launch_replay(nlist, nullptr, nlist <= kReplayWindowMax, nlist);
         if (rc) return rc;
       }
       if (c->profile)
@@ -3542,44 +2910,18 @@ int grow_for(rt_coverage* c, int64_t n) {
 // c->nuniq, then their f64 values into c->uamps
 template <typename Val>
 int run_sums(rt_coverage* c, Val val, int64_t n, WideKey wk, hipStream_t s) {
-  if (RT_RUN_SUMS_V2) {
-    const int64_t T = std::max<int64_t>(kMinTile, (n + 64 * kMaxTiles - 1) / (64 * kMaxTiles) * 64);
-    const int64_t ntiles = (n + T - 1) / T;
-    TileMeta tm;
-    tm.heads = c->runs;
-    tm.tail_u = reinterpret_cast<int64_t*>(c->runs + 2 * kMaxTiles);
-    tm.headpart = reinterpret_cast<Fx192*>(c->tcos);  // free until k_terms
-    tm.tailpart = tm.headpart + kMaxTiles;
-    hipLaunchKernelGGL(k_tile_heads, dim3((unsigned)ntiles), dim3(256), 0, s, c->okeys_sorted, n, T, tm.heads);
-    hipLaunchKernelGGL(k_tile_sums<Val>, dim3((unsigned)ntiles), dim3(64), 0, s, c->okeys_sorted, val, n, T, ntiles, tm,
-                       wk, c->ukeys, plan_sums(c), c->uamps, c->nuniq);
-    hipLaunchKernelGGL(k_cross_tiles, dim3((unsigned)((ntiles + 3) / 4)), dim3(256), 0, s, ntiles, tm, plan_sums(c),
-                       c->uamps);
-    RT_HIP(hipGetLastError());
-    return RT_OK;
-  }
-  int32_t* flags = c->runs;  // then the long-run id of every run
-  int32_t* scan = c->runs + c->cap;
-  int32_t* starts = c->runs + 2 * c->cap;
-  unsigned* nlong = reinterpret_cast<unsigned*>(c->runs + 3 * c->cap);
-  int32_t* longu = reinterpret_cast<int32_t*>(c->list);  // free once the replay has run
-  // per span of kSpan records: head and tail pieces (tcos + tsin, 16 B per record, are free until k_terms)
-  Fx192* head = reinterpret_cast<Fx192*>(c->tcos);
-  Fx192* tail = head + (n + kSpan - 1) / kSpan;
-  const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 8192);
-  const unsigned g_span = (unsigned)std::min<int64_t>(((n + kSpan - 1) / kSpan + 3) / 4, 8192);
-  hipLaunchKernelGGL(k_run_flags, dim3(g), dim3(256), 0, s, c->okeys_sorted, n, flags);
-  size_t tb = c->tmp_bytes;
-  RT_HIP(scan_flags(c->tmp, tb, flags, scan, n, s));
-  hipLaunchKernelGGL(k_run_starts, dim3(g), dim3(256), 0, s, flags, scan, n, starts, c->nuniq);
-  RT_HIP(hipMemsetAsync(nlong, 0, 4, s));
-  hipLaunchKernelGGL(k_run_sums<Val>, dim3(g), dim3(256), 0, s, c->okeys_sorted, val, n, starts, c->nuniq, wk, c->ukeys,
-                     plan_sums(c), flags, longu, nlong);
-  hipLaunchKernelGGL(k_long_spans<Val>, dim3(g_span), dim3(256), 0, s, val, n, scan, starts, c->nuniq, flags, nlong,
-                     head, tail, plan_sums(c));
-  hipLaunchKernelGGL(k_long_final, dim3(g_span), dim3(256), 0, s, starts, c->nuniq, n, longu, nlong, head, tail,
-                     plan_sums(c));
-  hipLaunchKernelGGL(k_fx_to_amps, dim3(g), dim3(256), 0, s, plan_sums(c), c->nuniq, c->uamps);
+  const int64_t T = std::max<int64_t>(kMinTile, (n + 64 * kMaxTiles - 1) / (64 * kMaxTiles) * 64);
+  const int64_t ntiles = (n + T - 1) / T;
+  TileMeta tm;
+  tm.heads = c->runs;
+  tm.tail_u = reinterpret_cast<int64_t*>(c->runs + 2 * kMaxTiles);
+  tm.headpart = reinterpret_cast<Fx192*>(c->tcos);  // free until k_terms
+  tm.tailpart = tm.headpart + kMaxTiles;
+  hipLaunchKernelGGL(k_tile_heads, dim3((unsigned)ntiles), dim3(256), 0, s, c->okeys_sorted, n, T, tm.heads);
+  hipLaunchKernelGGL(k_tile_sums<Val>, dim3((unsigned)ntiles), dim3(64), 0, s, c->okeys_sorted, val, n, T, ntiles, tm,
+                     wk, c->ukeys, plan_sums(c), c->uamps, c->nuniq);
+  hipLaunchKernelGGL(k_cross_tiles, dim3((unsigned)((ntiles + 3) / 4)), dim3(256), 0, s, ntiles, tm, plan_sums(c),
+                     c->uamps);
   RT_HIP(hipGetLastError());
   return RT_OK;
 }
@@ -3864,7 +3206,7 @@ int trace_records_impl(rt_coverage* c, const float* tx_pos, double tx_power, dou
   if (nlist > 0) {
     const KeyBits kb = key_bits(c, n_bins);
     // the send buffers are filled before the host synchronizes (no launch after it)
-    if (RT_SEND_FUSED) {
+    {
       if ((rc = grow_for(c, nlist))) return rc;
       size_t tb = c->tmp_bytes;
       const int sb = record_sort_bits(c, kb, n_bins);
@@ -3895,12 +3237,6 @@ int trace_records_impl(rt_coverage* c, const float* tx_pos, double tx_power, dou
       a.packed = packed ? 1 : 0;
       a.cap = keys_out ? max_out : 0;
       hipLaunchKernelGGL(k_send_runs, dim3((unsigned)ntiles), dim3(256), 0, s, a);
-    } else {
-      rc = cov_reduce(c, c->okeys, c->oamps, nlist, record_sort_bits(c, kb, n_bins), wide_key(c, kb), s);
-      if (rc) return rc;
-      hipLaunchKernelGGL(k_bounds_strip, dim3((unsigned)std::min<int64_t>((nlist + 256) / 256, 4096)), dim3(256), 0,
-                         s, c->ukeys, plan_sums(c), c->nuniq, world, keys_out ? max_out : 0, own_shift(c), c->bounds,
-                         keys_out, (Fx192*)sums_out, packed ? 1 : 0);
     }
     RT_HIP(hipGetLastError());
     prof_mark(c, 7, s);
@@ -4066,16 +3402,16 @@ int power_segments_impl(rt_coverage* c, const uint64_t* keys, const uint64_t* su
     for (int t = 0; t < nseg; ++t) longest = std::max<int64_t>(longest, seg_counts[t]);
     const int steps = bits_for((uint64_t)longest);  // a search over len keys takes <= bits(len) halvings
     const dim3 gm((unsigned)std::min<int64_t>((n + 255) / 256, 8192));
-    if (RT_MERGE_LOCKSTEP && nseg <= 2)
+    if (nseg <= 2)
       hipLaunchKernelGGL(k_merge_lockstep<2>, gm, dim3(256), 0, s, keys, stride, so, steps, c->okeys_sorted, idx_sorted);
-    else if (RT_MERGE_LOCKSTEP && nseg <= 4)
+    else if (nseg <= 4)
       hipLaunchKernelGGL(k_merge_lockstep<4>, gm, dim3(256), 0, s, keys, stride, so, steps, c->okeys_sorted, idx_sorted);
-    else if (RT_MERGE_LOCKSTEP && nseg <= 8)
+    else if (nseg <= 8)
       hipLaunchKernelGGL(k_merge_lockstep<8>, gm, dim3(256), 0, s, keys, stride, so, steps, c->okeys_sorted, idx_sorted);
     else
       hipLaunchKernelGGL(k_merge_segments, gm, dim3(256), 0, s, keys, stride, so, c->okeys_sorted, idx_sorted);
     RT_HIP(hipGetLastError());
-    if (RT_OWNER_FUSED && nseg <= 8) {
+    if (nseg <= 8) {
       OwnerRuns a{};
       a.keys = c->okeys_sorted;
       a.val = SumVal{sums, idx_sorted, stride == 1 ? 3 : stride};
@@ -4100,10 +3436,6 @@ int power_segments_impl(rt_coverage* c, const uint64_t* keys, const uint64_t* su
       a.epoch = ++c->range_epoch;
       a.nbig = reinterpret_cast<unsigned*>(c->runs + 3 * c->cap + 1);
       a.P = power_params(n_bins, alpha);
-      a.heads = c->runs;
-      if (!RT_OWNER_LOOKBACK)
-        hipLaunchKernelGGL(k_tile_heads, dim3((unsigned)ntiles), dim3(256), 0, s, c->okeys_sorted, n, (int64_t)kOwnTile,
-                           c->runs);
       hipLaunchKernelGGL(k_owner_runs, dim3((unsigned)ntiles), dim3(256), 0, s, a);
       RT_HIP(hipGetLastError());
       fused = true;

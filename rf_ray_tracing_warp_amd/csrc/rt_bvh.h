@@ -31,10 +31,6 @@ struct BvhView {
 };
 
 #define RT_BVH_STACK 64
-// 0: binary nodes (Walk2), 1: 4-wide nodes (Walk4, default: K4 trace 1438 -> 1277 us)
-#ifndef RT_BVH_WIDE
-#define RT_BVH_WIDE 1
-#endif
 
 struct RayBox {
   float ox, oy, oz, ix, iy, iz;  // origin and per-axis reciprocal direction (never 0/NaN)
@@ -69,39 +65,7 @@ __device__ __forceinline__ float slab(const RayBox& r, float lx, float ly, float
 // leaf faces [first, first + count), count <= 4: the four 48-B records are fetched together
 // (indices clamped into the table, the results of q >= count ignored), so a leaf costs one
 // memory latency instead of one per face
-// RT_LEAF_PAIRS: a leaf's faces fetched two at a time instead of all four (24 instead of 48 VGPRs
-// in flight; a second latency only for leaves of more than two faces)
-#ifndef RT_LEAF_PAIRS
-#define RT_LEAF_PAIRS 0
-#endif
-__device__ __forceinline__ void leaf_face(const Shear& s, float4 a, float4 m, float4 c, Hit& h) {
-  const float4 q0 = make_float4(pick(a.x, a.y, a.z, s.kx), pick(a.x, a.y, a.z, s.ky), pick(a.x, a.y, a.z, s.kz),
-                                pick(a.w, m.x, m.y, s.kx));
-  const float4 q1 = make_float4(pick(a.w, m.x, m.y, s.ky), pick(a.w, m.x, m.y, s.kz), pick(m.z, m.w, c.x, s.kx),
-                                pick(m.z, m.w, c.x, s.ky));
-  const float c2 = pick(m.z, m.w, c.x, s.kz);
-  float T, det;
-  if (tri_test(s, q0, q1, c2, T, det)) hit_consider(h, T, det, __float_as_int(c.y));
-}
 __device__ __forceinline__ void leaf4(const BvhView& b, const Shear& s, int first, int count, Hit& h) {
-#if RT_LEAF_PAIRS
-#pragma unroll
-  for (int q0 = 0; q0 < 4; q0 += 2) {
-    if (q0 >= count) break;
-    float4 A[2], M[2], C[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const float4* p = b.lcomp + (int64_t)min(first + q0 + q, b.nf - 1) * 3;
-      A[q] = p[0];
-      M[q] = p[1];
-      C[q] = p[2];
-    }
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-      if (q0 + q < count) leaf_face(s, A[q], M[q], C[q], h);
-  }
-  return;
-#endif
   float4 A[4], M[4], C[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -140,23 +104,17 @@ __device__ __forceinline__ float cull_limit(const Hit& h, float tc) { return fmi
 //
 // tcull < RT_MAX_T also culls boxes beyond tcull: every hit with t <= tcull is still found
 // exactly, hits beyond it may be missed (callers that only compare against tcull use it).
-//
-// The (node, entry t) stack is a private array: scratch memory.  Kept in LDS instead (12 entries
-// per lane, deeper ones private) it measured no faster on K4 (1431 vs 1454 us) or K5.
 
 // The (node, entry t) stack, kept apart from the walk's scalar state: inside one aggregate with
 // the dynamically indexed arrays, the scalars went to scratch too (k_traj<true> 92 -> 102 VGPRs
 // and +40 B scratch: cur, sp, the best hit and the ray box reloaded every step).
 //
-// RT_BVH_LDS_STACK = K > 0 keeps the K entries nearest the bottom of every lane's stack in LDS
-// (a [K][256] column per thread of the 256-thread block: lanes of a wave always hit distinct banks,
-// whatever their stack pointers) and only deeper entries in the private array, so a walk that stays
-// within K pending entries never touches scratch memory.
-#ifndef RT_BVH_LDS_STACK
-#define RT_BVH_LDS_STACK 16  // K4 rt_trace 1825 -> 1328 us, K5 map 5.53 -> 4.74 ms (profiles/r3b_*)
-#endif
-#if RT_BVH_LDS_STACK
-constexpr int kLdsStack = RT_BVH_LDS_STACK;
+// The kLdsStack entries nearest the bottom of every lane's stack live in LDS (a [K][256] column per
+// thread of the 256-thread block: lanes of a wave always hit distinct banks, whatever their stack
+// pointers) and only deeper entries in the private array, so a walk that stays within K pending
+// entries never touches scratch memory (K4 rt_trace 1825 -> 1328 us, K5 map 5.53 -> 4.74 ms against
+// the all-private stack, profiles/r3b_*; 8 entries measured the same).
+constexpr int kLdsStack = 16;
 struct WalkStack {
   int* ln;    // this thread's LDS column: entry i at ln[256 * i]
   float* lt;
@@ -183,82 +141,11 @@ __device__ __forceinline__ WalkStack make_stack() {
   st.lt = s_t + threadIdx.x;
   return st;
 }
-#else
-struct WalkStack {
-  int node[RT_BVH_STACK];
-  float t[RT_BVH_STACK];
-  __device__ __forceinline__ void set(int i, int c, float tt) {
-    node[i] = c;
-    t[i] = tt;
-  }
-  __device__ __forceinline__ int get_node(int i) const { return node[i]; }
-  __device__ __forceinline__ float get_t(int i) const { return t[i]; }
-};
-__device__ __forceinline__ WalkStack make_stack() { return WalkStack(); }
-#endif
-
-// binary nodes: near child first, far child pushed
-struct Walk2 {
-  Hit h;
-  RayBox r;
-  float tc;
-  int cur, sp;
-
-  __device__ __forceinline__ void init(float3 o, float3 d, float tcull = RT_MAX_T) {
-    hit_init(h);
-    tc = fminf(RT_MAX_T, tcull);
-    r = make_raybox(o, d);
-    cur = 0;
-    sp = 0;
-  }
-  __device__ __forceinline__ bool step(const BvhView& b, const Shear& s, WalkStack& st) {
-    bool visit = true;
-    if (cur < 0) {  // pop
-      if (sp == 0) return false;
-      --sp;
-      if (st.get_t(sp) <= cull_limit(h, tc)) cur = st.get_node(sp);
-      else visit = false;
-    }
-    if (visit) {
-    const float4 q0 = b.nodes[4 * cur + 0], q1 = b.nodes[4 * cur + 1];
-    const float4 q2 = b.nodes[4 * cur + 2], q3 = b.nodes[4 * cur + 3];
-    const int c0 = __float_as_int(q3.x), c1 = __float_as_int(q3.y);
-    float t0 = slab(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y);
-    float t1 = slab(r, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w);
-#pragma unroll
-    for (int side = 0; side < 2; ++side) {
-      const int c = side ? c1 : c0;
-      float& tt = side ? t1 : t0;
-      if (c < 0) {  // leaf child: test its faces now
-        if (tt <= cull_limit(h, tc)) {
-          const int pk = __float_as_int(side ? q3.w : q3.z);
-          leaf4(b, s, pk >> 3, pk & 7, h);
-        }
-        tt = INFINITY;
-      }
-    }
-    const float lim = cull_limit(h, tc);
-    const bool h0 = t0 <= lim, h1 = t1 <= lim;
-    if (h0 && h1) {
-      const bool first0 = t0 <= t1;
-      if (sp < RT_BVH_STACK) {  // cannot overflow: tree depth <= RT_BVH_STACK - 4 (bvh.hip)
-        st.set(sp, first0 ? c1 : c0, first0 ? t1 : t0);
-        ++sp;
-      }
-      cur = first0 ? c0 : c1;
-    } else {
-      cur = h0 ? c0 : (h1 ? c1 : -1);
-    }
-    }
-    return true;
-  }
-};
-
 // 4-wide nodes (bvh_wide.hip collapses the binary tree, breadth first): 8 float4 = 128 B,
 //   w[0] lo.x[4]  w[1] hi.x[4]  w[2] lo.y[4]  w[3] hi.y[4]  w[4] lo.z[4]  w[5] hi.z[4]
 //   w[6] child refs (int bits): >= 0 wide node, -1 empty slot, <= -2 leaf ~(first << 3 | count)
 // The child boxes are the binary tree's own (rounded outward and padded), so culling stays
-// exactly as conservative as Walk2's and the (t, face) minimum cannot depend on the tree.
+// exactly as conservative as the binary tree's and the (t, face) minimum cannot depend on the tree.
 // Per visit: four slab tests; the hit leaves tested on the spot, nearest first; the hit inner
 // children sorted by entry t, the nearest visited next and the others pushed far to near.
 // About half the dependent node fetches of the binary walk per query.  (The top 85 or 192 wide
@@ -274,9 +161,6 @@ __device__ __forceinline__ void cas(float& ta, int& ra, float& tb, int& rb) {
   rb = r1;
 }
 
-#ifndef RT_BVH_PREFETCH
-#define RT_BVH_PREFETCH 0
-#endif
 struct Walk4 {
   Hit h;
   RayBox r;
@@ -326,26 +210,6 @@ struct Walk4 {
     cas(l0, p0, l2, p2);
     cas(l1, p1, l3, p3);
     cas(l1, p1, l2, p2);
-#if RT_BVH_PREFETCH
-    // the node the next step will most likely visit (the nearest hit inner child, else the stack
-    // top), touched before the leaf tests so that its fetch overlaps theirs
-    float pf = 0.0f;
-    if (l0 <= cull_limit(h, tc)) {
-      const float lim0 = cull_limit(h, tc);
-      const float tn = fminf(fminf(c0 >= 0 ? t0 : INFINITY, c1 >= 0 ? t1 : INFINITY),
-                             fminf(c2 >= 0 ? t2 : INFINITY, c3 >= 0 ? t3 : INFINITY));
-      int nx = -1;
-      if (tn <= lim0) {
-        nx = (c0 >= 0 && t0 == tn) ? c0 : (c1 >= 0 && t1 == tn) ? c1 : (c2 >= 0 && t2 == tn) ? c2 : c3;
-      } else if (sp > 0) {
-        nx = st.get_node(sp - 1);
-      }
-      if (nx >= 0) {
-        const float* nw = reinterpret_cast<const float*>(b.wide + 8 * (int64_t)nx);
-        pf = nw[0] + nw[16];
-      }
-    }
-#endif
 #pragma unroll 1
     for (int q = 0; q < 4; ++q) {  // one leaf4 body in the code; the sorted list shifts down
       if (!(l0 <= cull_limit(h, tc))) break;
@@ -372,9 +236,6 @@ struct Walk4 {
     } else {
       cur = -1;
     }
-#if RT_BVH_PREFETCH
-    asm volatile("" ::"v"(pf));  // keeps the touch; its wait lands here, after the leaf tests
-#endif
     }
     return true;
   }
@@ -449,169 +310,9 @@ __device__ __forceinline__ Hit group_hit(Hit h) {
   return h;
 }
 
-// ---- Compressed 8-wide nodes (RT_BVH_WIDTH 8, bvh_wide.hip build_wide / emit_node8), 128 B each:
-//   dwords 0..2  grid origin (x, y, z) = the node box's low corner
-//   dword  3     per-axis step exponents: byte a = e_a + 127, step 2^e_a
-//   dwords 4..15 quantised child bounds, one byte per child: lo.x[8] hi.x[8] lo.y[8] hi.y[8] lo.z[8] hi.z[8]
-//   dwords 16..23 child refs (int): >= 0 wide node, -1 empty slot, <= -2 leaf ~(first << 3 | count)
-// A child's bound is origin + q * 2^e, rounded outward on the host in the same f32 arithmetic, so
-// the decoded box contains the binary tree's padded box and culling stays conservative.  Per child
-// 16 B instead of Walk4's 32 B, and three binary levels per node instead of two: fewer dependent
-// node fetches per query.  The slab test works relative to the ray origin: (origin - o) once per
-// node and axis, then fmaf(q, 2^e, origin - o) per bound -- within an ulp or two of the absolute
-// form, far inside the boxes' 1e-5 padding.
-#ifndef RT_BVH_WIDTH
-#define RT_BVH_WIDTH 4
-#endif
-__device__ __forceinline__ float byte_f(uint32_t w, int b) { return (float)((w >> (8 * b)) & 0xFFu); }
-__device__ __forceinline__ float exp_step(uint32_t e, int a) {
-  return __uint_as_float(((e >> (8 * a)) & 0xFFu) << 23);
-}
-
-// the 8 child boxes of a compressed node against the ray: entry t (INF on a miss) and refs
-struct Node8 {
-  float t[8];
-  int ref[8];
-};
-__device__ __forceinline__ void visit8(const BvhView& b, int node, const RayBox& r, Node8& out) {
-  const float4* w = b.wide + 8 * (int64_t)node;
-  const float4 h = w[0], qa = w[1], qb = w[2], qc = w[3], ra = w[4], rb = w[5];
-  const uint32_t eb = __float_as_uint(h.w);
-  const float sx = exp_step(eb, 0), sy = exp_step(eb, 1), sz = exp_step(eb, 2);
-  const float dx = h.x - r.ox, dy = h.y - r.oy, dz = h.z - r.oz;
-  const uint32_t lxw[2] = {__float_as_uint(qa.x), __float_as_uint(qa.y)};
-  const uint32_t hxw[2] = {__float_as_uint(qa.z), __float_as_uint(qa.w)};
-  const uint32_t lyw[2] = {__float_as_uint(qb.x), __float_as_uint(qb.y)};
-  const uint32_t hyw[2] = {__float_as_uint(qb.z), __float_as_uint(qb.w)};
-  const uint32_t lzw[2] = {__float_as_uint(qc.x), __float_as_uint(qc.y)};
-  const uint32_t hzw[2] = {__float_as_uint(qc.z), __float_as_uint(qc.w)};
-  const int refs[8] = {__float_as_int(ra.x), __float_as_int(ra.y), __float_as_int(ra.z), __float_as_int(ra.w),
-                       __float_as_int(rb.x), __float_as_int(rb.y), __float_as_int(rb.z), __float_as_int(rb.w)};
-#pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    const int wd = c >> 2, by = c & 3;
-    const float tx0 = fmaf(byte_f(lxw[wd], by), sx, dx) * r.ix, tx1 = fmaf(byte_f(hxw[wd], by), sx, dx) * r.ix;
-    const float ty0 = fmaf(byte_f(lyw[wd], by), sy, dy) * r.iy, ty1 = fmaf(byte_f(hyw[wd], by), sy, dy) * r.iy;
-    const float tz0 = fmaf(byte_f(lzw[wd], by), sz, dz) * r.iz, tz1 = fmaf(byte_f(hzw[wd], by), sz, dz) * r.iz;
-    const float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
-    const float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
-    out.ref[c] = refs[c];
-    out.t[c] = (refs[c] != -1 && tn <= tf * 1.00001f + 1e-6f) ? tn : INFINITY;
-  }
-}
-
-struct Walk8 {
-  Hit h;
-  RayBox r;
-  float tc;
-  int cur, sp;
-
-  __device__ __forceinline__ void init(float3 o, float3 d, float tcull = RT_MAX_T) {
-    hit_init(h);
-    tc = fminf(RT_MAX_T, tcull);
-    r = make_raybox(o, d);
-    cur = 0;
-    sp = 0;
-  }
-  __device__ __forceinline__ void push(WalkStack& st, int c, float t) {
-    if (sp < RT_BVH_STACK) {  // cannot overflow: bound checked on the host (build_wide)
-      st.set(sp, c, t);
-      ++sp;
-    }
-  }
-  // one visited node's children: hit leaves tested nearest first, then the nearest hit inner child
-  // is visited next and the others pushed far to near
-  __device__ __forceinline__ void expand(const BvhView& b, const Shear& s, WalkStack& st, const Node8& nd) {
-    uint32_t leaves = 0, inner = 0;
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      leaves |= (nd.ref[c] < -1 && nd.t[c] < INFINITY) ? 1u << c : 0u;
-      inner |= (nd.ref[c] >= 0 && nd.t[c] < INFINITY) ? 1u << c : 0u;
-    }
-#pragma unroll 1
-    while (leaves) {
-      float bt = INFINITY;
-      int bref = 0, bc = 0;
-#pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        const bool take = ((leaves >> c) & 1u) && nd.t[c] < bt;
-        bt = take ? nd.t[c] : bt;
-        bref = take ? nd.ref[c] : bref;
-        bc = take ? c : bc;
-      }
-      if (!(bt <= cull_limit(h, tc))) break;
-      const int pk = ~bref;
-      leaf4(b, s, pk >> 3, pk & 7, h);
-      leaves &= ~(1u << bc);
-    }
-    const float lim = cull_limit(h, tc);
-#pragma unroll
-    for (int c = 0; c < 8; ++c) inner &= nd.t[c] <= lim ? ~0u : ~(1u << c);
-    cur = -1;
-#pragma unroll 1
-    while (inner) {
-      // the farthest remaining child is pushed; the last one left (the nearest) is visited next
-      float bt = -1.0f;
-      int bref = 0, bc = 0;
-#pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        const bool take = ((inner >> c) & 1u) && nd.t[c] > bt;
-        bt = take ? nd.t[c] : bt;
-        bref = take ? nd.ref[c] : bref;
-        bc = take ? c : bc;
-      }
-      inner &= ~(1u << bc);
-      if (inner) push(st, bref, bt);
-      else cur = bref;
-    }
-  }
-  __device__ __forceinline__ bool step(const BvhView& b, const Shear& s, WalkStack& st) {
-    if (cur < 0) {  // pop
-      if (sp == 0) return false;
-      --sp;
-      if (!(st.get_t(sp) <= cull_limit(h, tc))) return true;
-      cur = st.get_node(sp);
-    }
-    Node8 nd;
-    visit8(b, cur, r, nd);
-    expand(b, s, st, nd);
-    return true;
-  }
-};
-
-// Walk8 over G lanes (G = 4 or 8) tracing ONE ray together: lane j takes the root's children
-// c = j, j + G, ... (a leaf child tested on the spot, an inner child pushed when hit); the group's
-// (t, face) minimum is the ray's closest hit (group_hit), each lane culling with the group's best t
-// (group_min_t), as split_init for Walk4.
-template <int G>
-__device__ __forceinline__ void split_init8(Walk8& w, WalkStack& st, const BvhView& b, const Shear& s, float3 o,
-                                            float3 d, int j, float tcull = RT_MAX_T) {
-  static_assert(G == 4 || G == 8, "split over 4 or 8 lanes");
-  w.init(o, d, tcull);
-  w.cur = -1;
-  Node8 nd;
-  visit8(b, 0, w.r, nd);
-#pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    if ((c & (G - 1)) != j) {
-      nd.t[c] = INFINITY;
-      nd.ref[c] = -1;
-    }
-  }
-  w.expand(b, s, st, nd);
-  if (w.cur >= 0) {  // the lane's nearest inner child goes on the stack too: step() starts by popping
-    w.push(st, w.cur, 0.0f);
-    w.cur = -1;
-  }
-}
-
-#if RT_BVH_WIDTH == 8
-using Walk = Walk8;
-#elif RT_BVH_WIDE
+// (Binary nodes (Walk2), compressed 8-wide nodes (Walk8), leaf faces fetched in pairs and a
+// next-node prefetch were measured and removed in round 5; last in commit 43de9a4)
 using Walk = Walk4;
-#else
-using Walk = Walk2;
-#endif
 
 // RT_COUNT_STEPS (diagnostic builds only, tools/walk_stats.py): per query, the lane's walk steps and
 // its share of the wave's loop iterations (1 / active lanes per iteration, so the shares of a wave

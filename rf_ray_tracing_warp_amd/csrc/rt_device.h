@@ -14,9 +14,6 @@
 #include <stdint.h>
 
 #define RT_MAX_T 1.0e6f  // kernel.py:71,82 max_t
-#ifndef RT_LAZY_HIT
-#define RT_LAZY_HIT 1  // brute-force face loops defer the IEEE division (LazyHit); 0 = per-face screen
-#endif
 
 namespace rt {
 

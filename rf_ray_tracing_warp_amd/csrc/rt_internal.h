@@ -65,14 +65,14 @@ extern int g_poison;
 int poison_pool(size_t bytes, hipStream_t s);
 // keep freed blocks of the device's default memory pool across synchronizes (trace.hip)
 void keep_pool_memory();
-// Row order for tracing rays [ray_offset, ray_offset+n) of one burst sorted by initial direction
-// (trace.hip).  Stream-ordered workspace returned in *ws (hipFreeAsync it after the consumer).
-const int32_t* dir_order(int64_t ray_offset, int64_t n, hipStream_t stream, void** ws);
-// dir_order_banded: bands of |d.z| (a power of two <= 256), the most nearly horizontal first
-#ifndef RT_ZBANDS
-#define RT_ZBANDS 16  // K4 rt_trace 1037 / 945 / 915 / 928 / 976 us at 4 / 8 / 16 / 32 / 64 (r4z7, r4z8)
-#endif
+// Row order for tracing rays [ray_offset, ray_offset+n) of one burst (trace.hip): bands of |d.z|
+// (kZBands, a power of two <= 256, the most nearly horizontal first), then the initial direction's
+// cell.  Stream-ordered workspace returned in *ws (hipFreeAsync it after the consumer).
+constexpr int kZBands = 16;  // K4 rt_trace 1037 / 945 / 915 / 928 / 976 us at 4 / 8 / 16 / 32 / 64 (r4z7, r4z8)
 const int32_t* dir_order_banded(int64_t ray_offset, int64_t n, hipStream_t stream, void** ws);
+// The same order, computed once per (device, ray_offset, n) and kept by the library (the rays of a
+// burst depend on their ids only); ready on `stream` when it returns.  nullptr on failure.
+const int32_t* dir_order_cached(int64_t ray_offset, int64_t n, hipStream_t stream);
 // Device view of a mesh's BVH for rt::bvh_query
 inline BvhView bvh_view(const rt_mesh* m) {
   return BvhView{(const float4*)m->nodes, (const int2*)m->leaves, (const float4*)m->lcomp, (int)m->nf,

@@ -45,8 +45,6 @@ struct TraceArgs {
   int32_t* hit_kind;  // (n, B) or null
   int32_t* hit_face;  // (n, B) or null
   const int32_t* order;  // processing order of the rows (null = identity), see launch_trace
-  int win_chunks;        // > 0: order is sorted within windows of win_chunks 256-row chunks, and every
-                         // window's chunks run on one XCD (xcd_chunk)
   bool fused;             // brute-force kernels under rt_trace_cir: list received rows, per-path CIR
   rt::TraceCirFused fz;
 };
@@ -55,32 +53,19 @@ struct TraceArgs {
 // (LDS for the environment, global for the receiver).
 template <typename Ptr>
 __device__ __forceinline__ rt::Hit query_faces(Ptr tab, int nf, const rt::Shear& s) {
-#if RT_LAZY_HIT
   rt::LazyHit h;  // faces in ascending order: the division waits for the winner (rt_device.h)
   rt::lazy_init(h);
-#else
-  rt::Hit h;
-  rt::hit_init(h);
-#endif
   const int off = s.kcase * 3;
-#ifndef RT_FACE_UNROLL
-#define RT_FACE_UNROLL 4  // fewer loop branches / SALU per face (K2 170 -> 164 us at 2 with RT_BF_WAVES; 4: 115.1 -> 114.0 us, r2zc)
-#endif
-#pragma unroll RT_FACE_UNROLL
+  // unrolled by four: fewer loop branches / SALU per face (K2 115.1 -> 114.0 us against two, r2zc)
+#pragma unroll 4
   for (int f = 0; f < nf; ++f) {
     const float4 q0 = tab[f * 18 + off + 0];
     const float4 q1 = tab[f * 18 + off + 1];
     const float c2 = tab[f * 18 + off + 2].x;
     float T, det;
-#if RT_LAZY_HIT
     if (rt::tri_test(s, q0, q1, c2, T, det)) rt::lazy_consider(h, T, det, f);
   }
   return rt::lazy_finish(h);
-#else
-    if (rt::tri_test(s, q0, q1, c2, T, det)) rt::hit_consider(h, T, det, f);
-  }
-  return h;
-#endif
 }
 
 // Can a receiver hit possibly be nearer than t_limit?  Conservative: the receiver's faces all
@@ -98,38 +83,15 @@ __device__ __forceinline__ bool rx_maybe(const TraceArgs& a, float3 o, float3 d,
   return t_enter <= t_limit * 1.0001f + 1e-4f;
 }
 
-// Row stores of the register-resident kernels.  RT_NT_ROWS: non-temporal (streaming) stores --
-// the rows are written once and not read back by this step, so they need not sit dirty in L2
-// until the end-of-kernel writeback.  Brute-force kernels only: there a wave's rows are
+// Row stores of the register-resident kernels.  Brute-force kernels use non-temporal (streaming)
+// stores -- the rows are written once and not read back by this step, and a wave's rows are
 // consecutive, so its stores fill whole lines.  The BVH kernels write direction-sorted rows at
 // scattered row indices, every 72-B row a few partial lines; streaming stores sent each piece to
 // memory on its own (1.0 GB written per K4 launch for 0.31 GB of rows), while ordinary stores let
 // L2 merge a row's pieces first: 0.47 GB, and the K4 kernel 1230 -> 880 us (profiles/r3s_*).
-#ifndef RT_NT_ROWS
-#define RT_NT_ROWS 1
-#endif
-#ifndef RT_ROW_X2
-#define RT_ROW_X2 0  // 8-byte stores for rows of P = 2, 6 points (A/B builds)
-#endif
-// RT_XCD_WINDOWS: BVH bursts of at least 64 windows are traced window by window, each window on one
-// XCD (xcd_chunk); 0 keeps the device-wide direction sort.  Measured: no less write traffic (1.02
-// GB per K4 launch either way), 5x the node fetches, K4 1347 -> 1441 us (profiles/r3c_*).  Off, and
-// compiled out of the trace loop (its index arithmetic cost the K2 kernel 10 more spilled VGPRs).
-#ifndef RT_XCD_WINDOWS
-#define RT_XCD_WINDOWS 0
-#endif
-// RT_TRACE_ZBAND: rt_trace's BVH bursts in the banded direction order (dir_order_banded: the most
-// nearly horizontal rays first), as coverage plans use
-#ifndef RT_TRACE_ZBAND
-#define RT_TRACE_ZBAND 1  // K4 rt_trace 978 -> 934 us, bit-identical (profiles/r4z5_k4_trace_zband_ab.jsonl)
-#endif
-#ifndef RT_SPARSE_RX
-#define RT_SPARSE_RX 1
-#endif
-#ifndef RT_PATH_LDS
-#define RT_PATH_LDS 0
-#endif
-// received rows = NaN, row_mask = 0, in row order with 16-B streaming stores (RT_SPARSE_RX)
+// (8-byte row stores, rows transposed across the wave with ds_bpermute, XCD-affine row windows and
+// the path points in LDS were measured no better and removed in round 5; last in commit 43de9a4.)
+// received rows = NaN, row_mask = 0, in row order with 16-B streaming stores (BVH bursts, see trace_body)
 __global__ __launch_bounds__(256) void k_fill_received(float* received, int64_t nwords, uint32_t* mask, int64_t n) {
   typedef uint32_t u4v __attribute__((ext_vector_type(4)));
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, str = (int64_t)gridDim.x * blockDim.x;
@@ -155,7 +117,7 @@ __global__ __launch_bounds__(256) void k_fill_received(float* received, int64_t 
   }
 }
 
-template <int P, bool NT = (RT_NT_ROWS != 0)>
+template <int P, bool NT>
 __device__ __forceinline__ void store_row_fixed(float* dst, const float (*pts)[3]) {
   if constexpr ((P * 3) % 4 == 0) {  // 16-B aligned rows (P = 4, 8): 16-byte stores
     typedef float f4v __attribute__((ext_vector_type(4)));
@@ -168,67 +130,12 @@ __device__ __forceinline__ void store_row_fixed(float* dst, const float (*pts)[3
       if constexpr (NT) __builtin_nontemporal_store(v, d4 + j);
       else d4[j] = v;
     }
-  } else if constexpr (RT_ROW_X2 && (P * 3) % 2 == 0) {  // 8-B aligned rows (P = 2, 6): 8-byte stores
-    typedef float f2v __attribute__((ext_vector_type(2)));
-    f2v* d2 = reinterpret_cast<f2v*>(dst);
-#pragma unroll
-    for (int j = 0; j < P * 3 / 2; ++j) {
-      const int i = 2 * j;
-      const f2v v = {pts[i / 3][i % 3], pts[(i + 1) / 3][(i + 1) % 3]};
-      if constexpr (NT) __builtin_nontemporal_store(v, d2 + j);
-      else d2[j] = v;
-    }
   } else {
 #pragma unroll
     for (int i = 0; i < P * 3; ++i) {
       if constexpr (NT) __builtin_nontemporal_store(pts[i / 3][i % 3], dst + i);
       else dst[i] = pts[i / 3][i % 3];
     }
-  }
-}
-
-// RT_ROW_PERMUTE (K2's 48-B rows, P = 4): the wave's 64 rows are one contiguous 3,072-B block, but
-// each lane storing its own row writes 16-B pieces at a 48-B stride, so every store instruction
-// touches all 24 lines of the block (WRITE_SIZE 111.7 MB per 100 MB of rows, r2zm).  Here the rows
-// are transposed across the wave with ds_bpermute (no LDS allocation) so that store j writes bytes
-// [1024 j, 1024 (j + 1)) of the block: lane L stores 16-B piece q = 64 j + L, which is part q % 3
-// of row q / 3.  Only for full waves of consecutive rows (every lane valid, no row order).
-#ifndef RT_ROW_PERMUTE
-#define RT_ROW_PERMUTE 0
-#endif
-__device__ __forceinline__ float bperm_f(float v, int src_lane) {
-  return __int_as_float(__builtin_amdgcn_ds_bpermute(src_lane << 2, __float_as_int(v)));
-}
-__device__ __forceinline__ void store_rows_wave4(float* wave_dst, const float (*pts)[3]) {
-  typedef float f4v __attribute__((ext_vector_type(4)));
-  const int lane = threadIdx.x & 63;
-  float f[12];
-#pragma unroll
-  for (int i = 0; i < 12; ++i) f[i] = pts[i / 3][i % 3];
-  f4v* d4 = reinterpret_cast<f4v*>(wave_dst);
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const int q = 64 * j + lane, r = q / 3, part = q - 3 * r;
-    f4v v;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float a0 = bperm_f(f[e], r), a1 = bperm_f(f[4 + e], r), a2 = bperm_f(f[8 + e], r);
-      v[e] = part == 0 ? a0 : (part == 1 ? a1 : a2);
-    }
-#if RT_NT_ROWS
-    __builtin_nontemporal_store(v, d4 + q);
-#else
-    d4[q] = v;
-#endif
-  }
-}
-
-__device__ __forceinline__ void store_row(float* dst, const float (*pts)[3], int P) {
-  // rows are 12*P bytes; use 16-byte stores whenever the row start allows it
-  for (int i = 0; i < P; ++i) {
-    dst[3 * i + 0] = pts[i][0];
-    dst[3 * i + 1] = pts[i][1];
-    dst[3 * i + 2] = pts[i][2];
   }
 }
 
@@ -256,9 +163,6 @@ __device__ __forceinline__ rt::Hit env_hit_query(const TraceArgs& a, const float
 // candidates only, in ascending face order (room.stl: 1.8 candidates per ray, 4.1 per wave, of
 // 44 faces), so every output bit is unchanged.
 constexpr int kConeMaxFaces = 64;  // candidate set = one 64-bit mask per lane
-#ifndef RT_CONE
-#define RT_CONE 1  // 0: bounce 0 tests every face (A/B builds)
-#endif
 
 __device__ __forceinline__ void stage_cones(const TraceArgs& a, float4* cone) {
   for (int f = threadIdx.x; f < a.env_nf; f += blockDim.x) {
@@ -426,42 +330,20 @@ __global__ __launch_bounds__(512) void k_trace_cir_tail(rt::TraceCirFused fz, in
   if (wave == 0 && fz.ir) rt::ir_accumulate_wave(fz.cbin, fz.camp, total, fz.k.n_bins, fz.ir, false);
 }
 
-// XCD-affine chunk order for window-sorted bursts.  Blocks are dispatched round-robin over the 8
-// XCDs (block b on XCD b % 8), and every XCD has its own L2.  Window w (win_chunks consecutive
-// 256-row chunks, its rows sorted by direction inside the window, dir_order_windows) is traced by
-// the blocks of XCD w % 8 only, so the partial 128-B lines its scattered rows leave in that XCD's
-// L2 are completed there before they are written back (a globally sorted burst scatters each row
-// over the whole output: 3x write traffic, profiles/r3b_k4_write_split.json).  Iteration `it` of
-// block b = (xcd, q) takes item q + it * nq of its XCD's (window, chunk) items; -1 when done.
-__device__ __forceinline__ int64_t xcd_chunk(int win_chunks, int64_t nchunks, int64_t it) {
-  const int64_t x = blockIdx.x & 7, q = blockIdx.x >> 3, nq = (int64_t)gridDim.x >> 3;
-  const int64_t t = q + it * nq;
-  const int64_t w = x + 8 * (t / win_chunks);
-  const int64_t chunk = w * win_chunks + t % win_chunks;
-  return w * win_chunks < nchunks ? chunk : -1;
-}
-
 template <int B, bool USE_BVH>
 __device__ __forceinline__ void trace_body(const TraceArgs& a) {
   constexpr int P = B + 1;
-  constexpr bool kNtRows = RT_NT_ROWS && !USE_BVH;  // see store_row_fixed
+  constexpr bool kNtRows = !USE_BVH;  // see store_row_fixed
   extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
   float4* cone = lds_tab + (size_t)a.env_nf * 18;  // bounce-0 edge normals after the face table
-  const bool use_cone = RT_CONE && !USE_BVH && a.env_nf <= kConeMaxFaces;
+  const bool use_cone = !USE_BVH && a.env_nf <= kConeMaxFaces;
   if (use_cone) stage_cones(a, cone);  // made visible by stage_env's barrier
   stage_env<USE_BVH>(a, lds_tab);
 
   const float qnan = __builtin_nanf("");
   // block-uniform loop over 256-row chunks (the same rows per thread as a grid-stride loop), so a
   // wave can list its part of a chunk's received rows for rt_trace_cir
-#if RT_XCD_WINDOWS
-  const int64_t nchunks = (a.n + 255) / 256;
-  for (int64_t it = 0;; ++it) {
-    const int64_t chunk = a.win_chunks > 0 ? xcd_chunk(a.win_chunks, nchunks, it) : blockIdx.x + it * gridDim.x;
-    if (chunk < 0 || chunk >= nchunks) break;
-#else
   for (int64_t chunk = blockIdx.x; chunk * 256 < a.n; chunk += gridDim.x) {
-#endif
     const int64_t irow = chunk * 256 + threadIdx.x;
     bool got = false;
     if (irow < a.n) {
@@ -469,32 +351,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
     const int64_t gid = a.ray_offset + row;
     float3 dir = rt::ray_dir(gid);
     float3 pos = make_float3(a.tx[0], a.tx[1], a.tx[2]);
-#if RT_PATH_LDS
-    // BVH kernels: the path's points 1..B wait in this thread's LDS column instead of 3B VGPRs
-    // live through every walk (K4: 5 waves per SIMD instead of 4), and come back for the row stores
-    __shared__ float s_path[USE_BVH ? 3 * B : 1][256];
     float path[P][3];
-    int npts = 0;
-    auto set_pt = [&](int i, float3 q) {
-      if constexpr (USE_BVH) {
-        s_path[3 * (i - 1) + 0][threadIdx.x] = q.x;
-        s_path[3 * (i - 1) + 1][threadIdx.x] = q.y;
-        s_path[3 * (i - 1) + 2][threadIdx.x] = q.z;
-        npts = i;
-      } else {
-        path[i][0] = q.x;
-        path[i][1] = q.y;
-        path[i][2] = q.z;
-      }
-    };
-#else
-    float path[P][3];
-    auto set_pt = [&](int i, float3 q) {
-      path[i][0] = q.x;
-      path[i][1] = q.y;
-      path[i][2] = q.z;
-    };
-#endif
 #pragma unroll
     for (int i = 0; i < P; ++i) path[i][0] = path[i][1] = path[i][2] = qnan;
     path[0][0] = pos.x;
@@ -519,7 +376,9 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
           pos.x = fmaf(dir.x, hr.t, pos.x);
           pos.y = fmaf(dir.y, hr.t, pos.y);
           pos.z = fmaf(dir.z, hr.t, pos.z);
-          set_pt(b + 1, pos);
+          path[b + 1][0] = pos.x;
+          path[b + 1][1] = pos.y;
+          path[b + 1][2] = pos.z;
           last_rx = b + 1;
           kind = 2;
           face = hr.face;
@@ -527,7 +386,9 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
           pos.x = fmaf(dir.x, he.t, pos.x);
           pos.y = fmaf(dir.y, he.t, pos.y);
           pos.z = fmaf(dir.z, he.t, pos.z);
-          set_pt(b + 1, pos);
+          path[b + 1][0] = pos.x;
+          path[b + 1][1] = pos.y;
+          path[b + 1][2] = pos.z;
           const float4 n4 = a.env_nrm[he.face];
           const float3 n = make_float3(n4.x, n4.y, n4.z);
           const float sc = 2.0f * rt::dot3(dir, n);
@@ -543,33 +404,12 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
       if (a.hit_kind) a.hit_kind[row * B + b] = kind;
       if (a.hit_face) a.hit_face[row * B + b] = face;
     }
-#if RT_PATH_LDS
-    if constexpr (USE_BVH) {
-#pragma unroll
-      for (int i = 1; i < P; ++i)
-        if (i <= npts) {
-          path[i][0] = s_path[3 * (i - 1) + 0][threadIdx.x];
-          path[i][1] = s_path[3 * (i - 1) + 1][threadIdx.x];
-          path[i][2] = s_path[3 * (i - 1) + 2][threadIdx.x];
-        }
-    }
-#endif
-    // a full wave of consecutive rows (brute force, no row order): transposed 1-KB stores
-    const bool wave_rows = RT_ROW_PERMUTE && P == 4 && !a.order && chunk * 256 + (threadIdx.x | 63) < a.n;
-    if (a.traced) {
-      if constexpr (P == 4) {
-        if (wave_rows) store_rows_wave4(a.traced + (row - (threadIdx.x & 63)) * (P * 3), path);
-        else store_row_fixed<P, kNtRows>(a.traced + row * (P * 3), path);
-      } else {
-        store_row_fixed<P, kNtRows>(a.traced + row * (P * 3), path);
-      }
-    }
-    // BVH kernels (RT_SPARSE_RX): launch_trace fills received (NaN) and row_mask (0) in row order
-    // first, as the reference does on the host (tracer.py:67-72), and only received rays store their
-    // row and mask word here (kernel.py:89-91): a direction-sorted burst scatters its rows, and
-    // writing every ray's NaN row and mask word cost ~0.2 GB of partial-line writes per K4 launch
-    constexpr bool kSparseRx = USE_BVH && RT_SPARSE_RX;
-    if (a.received && (!kSparseRx || last_rx >= 0)) {
+    if (a.traced) store_row_fixed<P, kNtRows>(a.traced + row * (P * 3), path);
+    // BVH kernels: launch_trace fills received (NaN) and row_mask (0) in row order first, as the
+    // reference does on the host (tracer.py:67-72), and only received rays store their row and
+    // mask word here (kernel.py:89-91): a direction-sorted burst scatters its rows, and writing
+    // every ray's NaN row and mask word cost ~0.2 GB of partial-line writes per K4 launch
+    if (a.received && (!USE_BVH || last_rx >= 0)) {
       float rec[P][3];
 #pragma unroll
       for (int i = 0; i < P; ++i) {
@@ -578,14 +418,9 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
         rec[i][1] = keep ? path[i][1] : qnan;
         rec[i][2] = keep ? path[i][2] : qnan;
       }
-      if constexpr (P == 4) {
-        if (wave_rows) store_rows_wave4(a.received + (row - (threadIdx.x & 63)) * (P * 3), rec);
-        else store_row_fixed<P, kNtRows>(a.received + row * (P * 3), rec);
-      } else {
-        store_row_fixed<P, kNtRows>(a.received + row * (P * 3), rec);
-      }
+      store_row_fixed<P, kNtRows>(a.received + row * (P * 3), rec);
     }
-    if (a.mask && (!kSparseRx || last_rx >= 0)) {
+    if (a.mask && (!USE_BVH || last_rx >= 0)) {
       if constexpr (kNtRows) __builtin_nontemporal_store(last_rx >= 0 ? 1u : 0u, a.mask + row);
       else a.mask[row] = last_rx >= 0 ? 1u : 0u;
     }
@@ -604,369 +439,27 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
   }
 }
 
-// ------------------------------------------------------------------ active-ray compaction
-// Brute-force meshes, bounces >= 1.  A wave runs the 44-face loop as long as any of its lanes needs
-// it, and lanes whose ray has escaped (kernel.py:97-98; room.stl K2: 26% of rays at bounce 1, 30%
-// at bounce 2) idle through it.  So each block queues its live rays' (position, direction) in LDS
-// (ballot + mbcnt + one LDS atomic per wave), the first ceil(n_live / 64) waves of the block run
-// the environment query over the queue, and each ray picks its (t, face) back up.  Two block
-// barriers per bounce; waves left without queue entries skip the loop and free their SIMD's issue
-// slots.  Only which lane computes a query changes: same query, same inputs, same bits.
-// Measured (tools/gpu_k2ab.sh, K2, 1M rays): bit-identical, but the trace kernel takes 120.1 us
-// against 115.4 us without it -- the barriers and the queue's LDS (25 KB per block: 6 blocks per
-// CU instead of 7) cost more than the 25% of bounce-1/2 waves it retires.  Off by default
-// (RT_COMPACT=1 builds it for A/B).
-#ifndef RT_COMPACT
-#define RT_COMPACT 0  // measured slower on K2: trace kernel 120.1 vs 115.4 us (profiles/r2za_k2_compaction_ab.jsonl)
-#endif
-constexpr int kQueueFloats = 6 * 256 + 2 * 2 * 256;  // (pos, dir) per slot + (t, face) per slot x 2 bounce parities
-
-template <int B>
-__device__ __forceinline__ void trace_body_compact(const TraceArgs& a) {
-  constexpr int P = B + 1;
-  extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
-  const bool use_cone = RT_CONE && a.env_nf <= kConeMaxFaces;
-  float4* cone = lds_tab + (size_t)a.env_nf * 18;
-  float* qin = reinterpret_cast<float*>(lds_tab + (size_t)a.env_nf * (use_cone ? 21 : 18));  // [6][256]
-  float* qres = qin + 6 * 256;                                                               // [2][2][256]
-  __shared__ int qcnt[2][8];
-  if (threadIdx.x < 16) (&qcnt[0][0])[threadIdx.x] = 0;
-  if (use_cone) stage_cones(a, cone);
-  stage_env<false>(a, lds_tab);  // its barrier publishes the cones and the zeroed counters
-  const int lane = threadIdx.x & 63;
-  const float qnan = __builtin_nanf("");
-  int par = 0;
-  for (int64_t chunk = blockIdx.x; chunk * 256 < a.n; chunk += gridDim.x, par ^= 1) {
-    // the other parity's counters were last read before the previous chunk's final barrier
-    if (threadIdx.x < 8) qcnt[par ^ 1][threadIdx.x] = 0;
-    const int64_t row = chunk * 256 + threadIdx.x;
-    const bool valid = row < a.n;
-    float3 dir = rt::ray_dir(a.ray_offset + (valid ? row : 0));
-    float3 pos = make_float3(a.tx[0], a.tx[1], a.tx[2]);
-    float path[P][3];
-#pragma unroll
-    for (int i = 0; i < P; ++i) path[i][0] = path[i][1] = path[i][2] = qnan;
-    path[0][0] = pos.x;
-    path[0][1] = pos.y;
-    path[0][2] = pos.z;
-    int last_rx = -1;
-    bool alive = valid;
-#pragma unroll
-    for (int b = 0; b < B; ++b) {
-      int kind = 0, face = -1;
-      rt::Hit he;
-      if (b == 0) {
-        if (alive) {
-          const rt::Shear s = rt::make_shear(pos, dir);
-          he = use_cone ? query_cone(lds_tab, cone, a.env_nf, s, dir) : query_faces(lds_tab, a.env_nf, s);
-        }
-      } else {
-        const uint64_t m = __ballot(alive);
-        int base = 0;
-        if (m) {  // wave-uniform
-          if (lane == 0) base = atomicAdd(&qcnt[par][b], (int)__popcll(m));
-          base = __shfl(base, 0, 64);
-        }
-        const int slot = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        if (alive) {
-          qin[0 * 256 + slot] = pos.x;
-          qin[1 * 256 + slot] = pos.y;
-          qin[2 * 256 + slot] = pos.z;
-          qin[3 * 256 + slot] = dir.x;
-          qin[4 * 256 + slot] = dir.y;
-          qin[5 * 256 + slot] = dir.z;
-        }
-        __syncthreads();
-        const int nq = qcnt[par][b];
-        float* res = qres + (b & 1) * 512;
-        if ((int)threadIdx.x < nq) {
-          const int j = threadIdx.x;
-          const float3 qp = make_float3(qin[j], qin[256 + j], qin[512 + j]);
-          const float3 qd = make_float3(qin[768 + j], qin[1024 + j], qin[1280 + j]);
-          const rt::Hit h = query_faces(lds_tab, a.env_nf, rt::make_shear(qp, qd));
-          res[j] = h.t;
-          res[256 + j] = __int_as_float(h.face);
-        }
-        __syncthreads();
-        if (alive) {
-          he.t = res[slot];
-          he.face = __float_as_int(res[256 + slot]);
-        }
-      }
-      if (alive) {
-        const bool env_hit = he.face >= 0;
-        rt::Hit hr;
-        rt::hit_init(hr);
-        if (a.rx_nf > 0 && rx_maybe(a, pos, dir, env_hit ? he.t : RT_MAX_T))
-          hr = query_faces(a.rx_perm, a.rx_nf, rt::make_shear(pos, dir));
-        const bool rx_hit = hr.face >= 0;
-        if (rx_hit && (!env_hit || he.t > hr.t)) {  // kernel.py:85
-          pos.x = fmaf(dir.x, hr.t, pos.x);
-          pos.y = fmaf(dir.y, hr.t, pos.y);
-          pos.z = fmaf(dir.z, hr.t, pos.z);
-          path[b + 1][0] = pos.x;
-          path[b + 1][1] = pos.y;
-          path[b + 1][2] = pos.z;
-          last_rx = b + 1;
-          kind = 2;
-          face = hr.face;
-        } else if (env_hit) {  // kernel.py:93-96
-          pos.x = fmaf(dir.x, he.t, pos.x);
-          pos.y = fmaf(dir.y, he.t, pos.y);
-          pos.z = fmaf(dir.z, he.t, pos.z);
-          path[b + 1][0] = pos.x;
-          path[b + 1][1] = pos.y;
-          path[b + 1][2] = pos.z;
-          const float4 n4 = a.env_nrm[he.face];
-          const float3 n = make_float3(n4.x, n4.y, n4.z);
-          const float sc = 2.0f * rt::dot3(dir, n);
-          dir.x = fmaf(-sc, n.x, dir.x);
-          dir.y = fmaf(-sc, n.y, dir.y);
-          dir.z = fmaf(-sc, n.z, dir.z);
-          kind = 1;
-          face = he.face;
-        } else {
-          alive = false;  // kernel.py:97-98: every later iteration repeats this miss
-        }
-      }
-      if (valid && a.hit_kind) a.hit_kind[row * B + b] = kind;
-      if (valid && a.hit_face) a.hit_face[row * B + b] = face;
-    }
-    if (valid) {
-      if (a.traced) store_row_fixed<P>(a.traced + row * (P * 3), path);
-      if (a.received) {
-        float rec[P][3];
-#pragma unroll
-        for (int i = 0; i < P; ++i) {
-          const bool keep = i <= last_rx;
-          rec[i][0] = keep ? path[i][0] : qnan;
-          rec[i][1] = keep ? path[i][1] : qnan;
-          rec[i][2] = keep ? path[i][2] : qnan;
-        }
-        store_row_fixed<P>(a.received + row * (P * 3), rec);
-      }
-      if (a.mask) {
-#if RT_NT_ROWS
-        __builtin_nontemporal_store(last_rx >= 0 ? 1u : 0u, a.mask + row);
-#else
-        a.mask[row] = last_rx >= 0 ? 1u : 0u;
-#endif
-      }
-    }
-    if (a.fused) {
-      const uint64_t m = __ballot(last_rx >= 0);
-      if (m && lane == 0) {  // wave-uniform: list this wave's received rows (bits of the chunk's row mask)
-        atomicAdd(a.fz.counts + chunk, (int32_t)__popcll(m));
-        atomicAdd(a.fz.gcounts + (chunk >> 6), (int32_t)__popcll(m));
-        atomicOr((unsigned long long*)a.fz.masks + chunk * 4 + (threadIdx.x >> 6), (unsigned long long)m);
-      }
-    }
-  }
-}
+// Active-ray compaction, measured and removed (round 5; last in commit 43de9a4):
+// queueing each block's live rays in LDS between bounces on the brute force (K2 trace kernel 120.1
+// vs 115.4 us: two block barriers per bounce and 25 KB of LDS per block), and a wavefront form of the
+// BVH trace with one launch per bounce over the compacted live-ray list (K4 2353 vs 1333 us: the ray
+// state's HBM round trips and three launches per bounce).  A direction-sorted wave's rays escape
+// together, so whole waves retire early without a queue.
 
 // brute-force kernels up to B = 3 are built for 7 waves per SIMD (72 VGPRs): with the face loop
-// unrolled by two (RT_FACE_UNROLL) the K2 kernel took 73 VGPRs (6 waves); bounded, 164 vs 170 us per
-// launch, bit-identical.  Longer paths keep their registers (their path points would spill).
-#ifndef RT_BF_WAVES
-#define RT_BF_WAVES 7
-#endif
+// unrolled the K2 kernel took 73 VGPRs (6 waves); bounded, 164 vs 170 us per launch,
+// bit-identical.  Longer paths keep their registers (their path points would spill).
 template <int B, bool USE_BVH>
-__global__ __launch_bounds__(256, (B <= 3 ? RT_BF_WAVES : 1)) void k_trace_bf(TraceArgs a) {
-  if constexpr (RT_COMPACT && !USE_BVH && B >= 2)
-    trace_body_compact<B>(a);
-  else
-    trace_body<B, USE_BVH>(a);
+__global__ __launch_bounds__(256, (B <= 3 ? 7 : 1)) void k_trace_bf(TraceArgs a) {
+  trace_body<B, USE_BVH>(a);
 }
 // BVH meshes: traversal is latency-bound (dependent node fetches), so the kernel is built for
-// RT_BVH_WAVES waves per SIMD.  4 (128 VGPRs, no spills beyond the walk stack) beat 6 (80 VGPRs,
-// the path and walk state spilled inside the traversal loop): K4 1416 -> 1077 us per rt_trace
-// with the 4-wide walk; 3 (132 VGPRs) measured 1141 us.
-#ifndef RT_BVH_WAVES
-#define RT_BVH_WAVES 4
-#endif
+// 4 waves per SIMD (128 VGPRs, no spills beyond the walk stack), which beat 6 (80 VGPRs, the path
+// and walk state spilled inside the traversal loop): K4 1416 -> 1077 us per rt_trace with the
+// 4-wide walk; 3 (132 VGPRs) measured 1141 us, 5 (96 VGPRs, 385 spilled) no better.
 template <int B>
-__global__ __launch_bounds__(256, RT_BVH_WAVES) void k_trace_bvh(TraceArgs a) {
+__global__ __launch_bounds__(256, 4) void k_trace_bvh(TraceArgs a) {
   trace_body<B, true>(a);
-}
-
-// ------------------------------------------------------------------ wavefront BVH trace (RT_WAVEFRONT)
-// The north star's "ballot/prefix-sum active-ray compaction between bounces", as an A/B form of
-// k_trace_bvh: one launch per bounce over the compacted list of live rays (in the burst's
-// direction-sorted order), ray state in HBM between bounces, the path points by slot, and one final
-// pass that writes every row.  Per bounce:
-//   k_wf_bounce   one thread per live entry: the same env + receiver query and decision as
-//                 trace_body, the point by slot, the state in place, an alive flag
-//   k_wf_count    per tile of kWfTile entries: its live count
-//   k_wf_scatter  per tile: the live entries, in order (ballot + mbcnt + the tiles before it), into
-//                 the next list; the last tile writes the next count
-// then k_wf_rows writes traced / received / row_mask (and the dead bounces' hit kinds) for every ray.
-// Same operations on the same values per ray, so the same bits.  No atomics: MI355X executes
-// them at the memory side (profiles/r3b_hash_bench.jsonl).
-#ifndef RT_WAVEFRONT
-#define RT_WAVEFRONT 0
-#endif
-constexpr int kWfTile = 4096;
-__device__ __forceinline__ int wf_block_sum(int v, int* s4) {  // 256-thread blocks
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0) s4[threadIdx.x >> 6] = v;
-  __syncthreads();
-  return s4[0] + s4[1] + s4[2] + s4[3];
-}
-struct WfArgs {
-  TraceArgs t;
-  int B;
-  float4* st_a;          // list entries: (pos.xyz, slot bits), (dir.xyz, row bits), 2 float4 each
-  float4* st_b;
-  uint8_t* alive;        // per entry of the current list
-  int32_t* tile_cnt;     // per tile of the current list
-  unsigned* cnt;         // [0..B]: live entries entering bounce b
-  float4* pts;           // [(B + 1) * n]: point k of slot ir at pts[k * n + ir]
-  int8_t* last_rx;       // per slot
-  int8_t* npts;          // per slot: points on the path (B + 1 if it never missed)
-};
-__global__ __launch_bounds__(256) void k_wf_start(WfArgs w) {
-  const TraceArgs& a = w.t;
-  for (int64_t ir = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; ir < a.n; ir += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t row = a.order[ir];
-    const float3 d = rt::ray_dir(a.ray_offset + row);
-    w.st_a[2 * ir] = make_float4(a.tx[0], a.tx[1], a.tx[2], __int_as_float((int)ir));
-    w.st_a[2 * ir + 1] = make_float4(d.x, d.y, d.z, __int_as_float((int)row));
-    w.pts[ir] = make_float4(a.tx[0], a.tx[1], a.tx[2], 0.0f);
-    w.last_rx[ir] = -1;
-    w.npts[ir] = (int8_t)(w.B + 1);
-    if (ir == 0) w.cnt[0] = (unsigned)a.n;
-  }
-}
-__global__ __launch_bounds__(256, RT_BVH_WAVES) void k_wf_bounce(WfArgs w, int b, float4* st) {
-  const TraceArgs& a = w.t;
-  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t nin = w.cnt[b];
-  if (j >= nin) return;
-  const float4 s0 = st[2 * j], s1 = st[2 * j + 1];
-  float3 pos = make_float3(s0.x, s0.y, s0.z), dir = make_float3(s1.x, s1.y, s1.z);
-  const int64_t ir = __float_as_int(s0.w), row = __float_as_int(s1.w);
-  const rt::Shear s = rt::make_shear(pos, dir);
-  const rt::Hit he = env_hit_query<true>(a, nullptr, s, pos, dir);
-  const bool env_hit = he.face >= 0;
-  rt::Hit hr;
-  rt::hit_init(hr);
-  if (a.rx_nf > 0 && rx_maybe(a, pos, dir, env_hit ? he.t : RT_MAX_T)) hr = query_faces(a.rx_perm, a.rx_nf, s);
-  const bool rx_hit = hr.face >= 0;
-  int kind = 0, face = -1;
-  bool live = true;
-  if (rx_hit && (!env_hit || he.t > hr.t)) {  // kernel.py:85
-    pos.x = fmaf(dir.x, hr.t, pos.x);
-    pos.y = fmaf(dir.y, hr.t, pos.y);
-    pos.z = fmaf(dir.z, hr.t, pos.z);
-    w.last_rx[ir] = (int8_t)(b + 1);
-    kind = 2;
-    face = hr.face;
-  } else if (env_hit) {  // kernel.py:93-96
-    pos.x = fmaf(dir.x, he.t, pos.x);
-    pos.y = fmaf(dir.y, he.t, pos.y);
-    pos.z = fmaf(dir.z, he.t, pos.z);
-    const float4 n4 = a.env_nrm[he.face];
-    const float3 n = make_float3(n4.x, n4.y, n4.z);
-    const float sc = 2.0f * rt::dot3(dir, n);
-    dir.x = fmaf(-sc, n.x, dir.x);
-    dir.y = fmaf(-sc, n.y, dir.y);
-    dir.z = fmaf(-sc, n.z, dir.z);
-    kind = 1;
-    face = he.face;
-  } else {
-    live = false;  // kernel.py:97-98: every later iteration repeats this miss
-    w.npts[ir] = (int8_t)(b + 1);
-  }
-  if (live) {
-    w.pts[(int64_t)(b + 1) * a.n + ir] = make_float4(pos.x, pos.y, pos.z, 0.0f);
-    st[2 * j] = make_float4(pos.x, pos.y, pos.z, s0.w);
-    st[2 * j + 1] = make_float4(dir.x, dir.y, dir.z, s1.w);
-  }
-  w.alive[j] = live ? 1 : 0;
-  if (a.hit_kind) a.hit_kind[row * w.B + b] = kind;
-  if (a.hit_face) a.hit_face[row * w.B + b] = face;
-}
-__global__ __launch_bounds__(256) void k_wf_count(WfArgs w, int b) {
-  __shared__ int s4[4];
-  const int64_t nin = w.cnt[b];
-  const int64_t lo = (int64_t)blockIdx.x * kWfTile;
-  if (lo >= nin) return;  // block-uniform
-  const int64_t hi = lo + kWfTile < nin ? lo + kWfTile : nin;
-  int c = 0;
-  for (int64_t j = lo + threadIdx.x; j < hi; j += blockDim.x) c += w.alive[j];
-  c = wf_block_sum(c, s4);
-  if (threadIdx.x == 0) w.tile_cnt[blockIdx.x] = c;
-}
-__global__ __launch_bounds__(256) void k_wf_scatter(WfArgs w, int b, const float4* in, float4* out) {
-  __shared__ int s4[4];
-  __shared__ int w4[4];
-  const int64_t nin = w.cnt[b];
-  const int64_t ntiles = (nin + kWfTile - 1) / kWfTile;
-  const int64_t t = blockIdx.x;
-  if (t >= ntiles) {
-    if (t == 0 && threadIdx.x == 0) w.cnt[b + 1] = 0;  // nothing was live
-    return;
-  }
-  int before = 0;
-  for (int64_t q = threadIdx.x; q < t; q += blockDim.x) before += w.tile_cnt[q];
-  int64_t base = wf_block_sum(before, s4);
-  if (t == ntiles - 1 && threadIdx.x == 0) w.cnt[b + 1] = (unsigned)(base + w.tile_cnt[t]);
-  const int64_t lo = t * kWfTile, hi = lo + kWfTile < nin ? lo + kWfTile : nin;
-  const int wave = threadIdx.x >> 6;
-  for (int64_t j0 = lo; j0 < hi; j0 += blockDim.x) {  // block-uniform
-    const int64_t j = j0 + threadIdx.x;
-    const bool f = j < hi && w.alive[j] != 0;
-    const uint64_t m = __ballot(f);
-    if ((threadIdx.x & 63) == 0) w4[wave] = __popcll(m);
-    __syncthreads();
-    int off = 0;
-    for (int q = 0; q < wave; ++q) off += w4[q];
-    const int step = w4[0] + w4[1] + w4[2] + w4[3];
-    if (f) {
-      const int64_t k = base + off + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-      out[2 * k] = in[2 * j];
-      out[2 * k + 1] = in[2 * j + 1];
-    }
-    base += step;
-    __syncthreads();
-  }
-}
-template <int B>
-__global__ __launch_bounds__(256) void k_wf_rows(WfArgs w) {
-  constexpr int P = B + 1;
-  const TraceArgs& a = w.t;
-  const float qnan = __builtin_nanf("");
-  for (int64_t ir = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; ir < a.n; ir += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t row = a.order[ir];
-    const int np = w.npts[ir], lr = w.last_rx[ir];
-    float path[P][3];
-#pragma unroll
-    for (int k = 0; k < P; ++k) {
-      const float4 q = k < np ? w.pts[(int64_t)k * a.n + ir] : make_float4(qnan, qnan, qnan, 0.0f);
-      path[k][0] = q.x;
-      path[k][1] = q.y;
-      path[k][2] = q.z;
-    }
-    if (a.traced) store_row_fixed<P, false>(a.traced + row * (P * 3), path);
-    if (a.received) {
-      float rec[P][3];
-#pragma unroll
-      for (int i = 0; i < P; ++i) {
-        const bool keep = i <= lr;
-        rec[i][0] = keep ? path[i][0] : qnan;
-        rec[i][1] = keep ? path[i][1] : qnan;
-        rec[i][2] = keep ? path[i][2] : qnan;
-      }
-      store_row_fixed<P, false>(a.received + row * (P * 3), rec);
-    }
-    if (a.mask) a.mask[row] = lr >= 0 ? 1u : 0u;
-    for (int b = np; b < B; ++b) {  // bounces after the miss repeat it: kind 0, no face
-      if (a.hit_kind) a.hit_kind[row * B + b] = 0;
-      if (a.hit_face) a.hit_face[row * B + b] = -1;
-    }
-  }
 }
 
 // Generic fallback for B beyond the register-resident instantiations: the path lives in
@@ -1059,8 +552,8 @@ __device__ __forceinline__ uint16_t dir_cell(int64_t gid) {
   for (int b = 0; b < 8; ++b) k |= ((cx >> b) & 1u) << (2 * b) | ((cy >> b) & 1u) << (2 * b + 1);
   return (uint16_t)k;
 }
-constexpr int kZBandBits = RT_ZBANDS <= 1 ? 0 : 32 - __builtin_clz((unsigned)(RT_ZBANDS - 1));
-// Coverage plans (dir_order_banded): the direction cell under a band of |d.z| (RT_ZBANDS bands, the most
+constexpr int kZBandBits = rt::kZBands <= 1 ? 0 : 32 - __builtin_clz((unsigned)(rt::kZBands - 1));
+// Coverage plans (dir_order_banded): the direction cell under a band of |d.z| (rt::kZBands bands, the most
 // nearly horizontal first).  A terrain's grazing rays walk the longest BVH chains; issued first,
 // their waves run beside the short ones instead of after them (a rank's trajectory pass is two
 // rounds of the GPU's wave slots).  Only the processing order changes.
@@ -1068,43 +561,10 @@ __global__ __launch_bounds__(256) void k_dir_keys_banded(int64_t ray_offset, int
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const float3 d = rt::ray_dir(ray_offset + i);
-  const uint32_t band = (uint32_t)fminf(fabsf(d.z) * (float)RT_ZBANDS, (float)(RT_ZBANDS - 1));
+  const uint32_t band = (uint32_t)fminf(fabsf(d.z) * (float)rt::kZBands, (float)(rt::kZBands - 1));
   keys[i] = band << 16 | dir_cell(ray_offset + i);
   rows[i] = (int32_t)i;
 }
-__global__ __launch_bounds__(256) void k_dir_keys(int64_t ray_offset, int64_t n, uint16_t* keys, int32_t* rows) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  keys[i] = dir_cell(ray_offset + i);
-  rows[i] = (int32_t)i;
-}
-
-// Window-sorted order (xcd_chunk): window w = rows [w W, (w + 1) W), W = 1024 * RT_DIR_WIN_ITEMS,
-// sorted by direction cell inside the window by one 1024-thread block in LDS (stable: a key's rows
-// stay ascending), so one launch replaces the device-wide radix sort's passes.  Rows past n get the
-// largest key and, being last in the input, sort after every valid row of the window.
-#ifndef RT_DIR_WIN_ITEMS
-#define RT_DIR_WIN_ITEMS 8
-#endif
-constexpr int kDirWinRows = 1024 * RT_DIR_WIN_ITEMS;
-__global__ __launch_bounds__(1024) void k_dir_window_sort(int64_t ray_offset, int64_t n, int32_t* order) {
-  using Sort = rocprim::block_radix_sort<uint16_t, 1024, RT_DIR_WIN_ITEMS, int32_t>;
-  __shared__ typename Sort::storage_type st;
-  const int64_t base = (int64_t)blockIdx.x * kDirWinRows + (int64_t)threadIdx.x * RT_DIR_WIN_ITEMS;
-  uint16_t k[RT_DIR_WIN_ITEMS];
-  int32_t v[RT_DIR_WIN_ITEMS];
-#pragma unroll
-  for (int i = 0; i < RT_DIR_WIN_ITEMS; ++i) {
-    const int64_t row = base + i;
-    k[i] = row < n ? dir_cell(ray_offset + row) : (uint16_t)0xFFFF;
-    v[i] = (int32_t)row;
-  }
-  Sort().sort(k, v, st);
-#pragma unroll
-  for (int i = 0; i < RT_DIR_WIN_ITEMS; ++i)
-    if (base + i < n) order[base + i] = v[i];
-}
-
 }  // namespace
 
 // ------------------------------------------------------------------ launch (C++ side of rt_trace)
@@ -1129,37 +589,7 @@ void keep_pool_memory() {
   });
 }
 
-const int32_t* dir_order(int64_t ray_offset, int64_t n, hipStream_t stream, void** ws) {
-  size_t cub_bytes = 0;
-  *ws = nullptr;
-  keep_pool_memory();
-  if (hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (uint16_t*)nullptr, (uint16_t*)nullptr,
-                                         (int32_t*)nullptr, (int32_t*)nullptr, (int)n, 0, 16, stream) != hipSuccess) {
-    set_error("dir_order: hipcub sizing failed");
-    return nullptr;
-  }
-  const size_t kb = ((size_t)n * 2 + 255) / 256 * 256, rb = ((size_t)n * 4 + 255) / 256 * 256;
-  hipError_t e = hipMallocAsync(ws, 2 * kb + 2 * rb + cub_bytes, stream);
-  if (e != hipSuccess) {
-    hip_fail(e, "dir_order workspace");
-    *ws = nullptr;
-    return nullptr;
-  }
-  uint16_t* k_in = (uint16_t*)*ws;
-  uint16_t* k_out = (uint16_t*)((char*)*ws + kb);
-  int32_t* r_in = (int32_t*)((char*)*ws + 2 * kb);
-  int32_t* r_out = (int32_t*)((char*)*ws + 2 * kb + rb);
-  void* tmp = (char*)*ws + 2 * kb + 2 * rb;
-  hipLaunchKernelGGL(k_dir_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, ray_offset, n, k_in, r_in);
-  e = hipcub::DeviceRadixSort::SortPairs(tmp, cub_bytes, k_in, k_out, r_in, r_out, (int)n, 0, 16, stream);
-  if (e != hipSuccess) {
-    hip_fail(e, "dir_order sort");
-    return nullptr;
-  }
-  return r_out;
-}
-
-// dir_order with the |d.z| bands first (k_dir_keys_banded); nullptr on failure
+// rays [ray_offset, ray_offset + n) by |d.z| band, then direction cell (k_dir_keys_banded); nullptr on failure
 const int32_t* dir_order_banded(int64_t ray_offset, int64_t n, hipStream_t stream, void** ws) {
   size_t cub_bytes = 0;
   *ws = nullptr;
@@ -1191,21 +621,77 @@ const int32_t* dir_order_banded(int64_t ray_offset, int64_t n, hipStream_t strea
   return r_out;
 }
 
-// window-sorted order for the BVH trace kernels (xcd_chunk); nullptr on failure
-const int32_t* dir_order_windows(int64_t ray_offset, int64_t n, hipStream_t stream, void** ws) {
-  keep_pool_memory();
-  *ws = nullptr;
-  hipError_t e = hipMallocAsync(ws, ((size_t)n * 4 + 255) / 256 * 256, stream);
-  if (e != hipSuccess) {
-    hip_fail(e, "dir_order_windows workspace");
-    *ws = nullptr;
+// The banded order of a burst depends only on (ray_offset, n): every call traces the same rays
+// (kernel.py:51 seeds each ray with its id alone), so the order is computed once per device and
+// (ray_offset, n) and kept.  rt_trace re-sorted the burst on every call before round 5 (K4: 0.14 ms
+// of a 0.91 ms step).  A few entries per process, least recently used evicted; the first user's
+// stream records an event that later users on other streams wait on.
+namespace {
+struct OrderEntry {
+  int device = -1;
+  int64_t ray_offset = 0, n = 0;
+  int32_t* order = nullptr;
+  hipEvent_t ready = nullptr;
+  hipStream_t made_on = nullptr;
+  uint64_t used = 0;
+};
+constexpr int kOrderCache = 8;
+OrderEntry g_orders[kOrderCache];
+uint64_t g_order_clock = 0;
+std::mutex g_order_mu;
+}  // namespace
+
+const int32_t* dir_order_cached(int64_t ray_offset, int64_t n, hipStream_t stream) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) {
+    set_error("dir_order_cached: hipGetDevice failed");
     return nullptr;
   }
-  hipLaunchKernelGGL(k_dir_window_sort, dim3((unsigned)((n + kDirWinRows - 1) / kDirWinRows)), dim3(1024), 0, stream,
-                     ray_offset, n, (int32_t*)*ws);
-  return (const int32_t*)*ws;
+  std::lock_guard<std::mutex> lock(g_order_mu);
+  for (OrderEntry& e : g_orders)
+    if (e.order && e.device == dev && e.ray_offset == ray_offset && e.n == n) {
+      e.used = ++g_order_clock;
+      if (e.made_on != stream && hipStreamWaitEvent(stream, e.ready, 0) != hipSuccess) {
+        set_error("dir_order_cached: hipStreamWaitEvent failed");
+        return nullptr;
+      }
+      return e.order;
+    }
+  OrderEntry* slot = &g_orders[0];
+  for (OrderEntry& e : g_orders)
+    if (!e.order) {
+      slot = &e;
+      break;
+    } else if (e.used < slot->used) {
+      slot = &e;
+    }
+  if (slot->order) {  // evict (hipFree waits for the device: nothing in flight still reads it)
+    int cur = dev;
+    if (slot->device != dev) (void)hipSetDevice(slot->device);
+    (void)hipFree(slot->order);
+    if (slot->ready) (void)hipEventDestroy(slot->ready);
+    if (slot->device != cur) (void)hipSetDevice(cur);
+    *slot = OrderEntry{};
+  }
+  void* ws = nullptr;
+  const int32_t* o = dir_order_banded(ray_offset, n, stream, &ws);
+  if (!o) return nullptr;
+  int32_t* keep = nullptr;
+  hipError_t e = hipMalloc(&keep, sizeof(int32_t) * (size_t)n);
+  if (e == hipSuccess) e = hipMemcpyAsync(keep, o, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToDevice, stream);
+  if (e == hipSuccess) e = hipFreeAsync(ws, stream);
+  hipEvent_t ev = nullptr;
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventRecord(ev, stream);
+  if (e != hipSuccess) {
+    if (keep) (void)hipFree(keep);
+    if (ev) (void)hipEventDestroy(ev);
+    hip_fail(e, "dir_order_cached");
+    return nullptr;
+  }
+  *slot = OrderEntry{dev, ray_offset, n, keep, ev, stream, ++g_order_clock};
+  return keep;
 }
-
 
 void trace_mark(int i, hipStream_t s);
 void trace_events(hipEvent_t* e0, hipEvent_t* e1);
@@ -1243,10 +729,7 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
   if (a.fused) a.fz = *fused;
   if (fused_done) *fused_done = a.fused;
   // brute force: the face table, then the bounce-0 cone normals (3 float4 per face, <= 64 faces)
-  // and (RT_COMPACT, B >= 2) the block's ray queue
-  const size_t lds = bvh ? 0
-                         : (size_t)env->nf * (env->nf <= kConeMaxFaces ? 21 : 18) * sizeof(float4) +
-                               (RT_COMPACT && B >= 2 && B <= 8 ? kQueueFloats * sizeof(float) : 0);
+  const size_t lds = bvh ? 0 : (size_t)env->nf * (env->nf <= kConeMaxFaces ? 21 : 18) * sizeof(float4);
   int dev_cu = 256;
   const int64_t want = (n + 255) / 256;
   const int64_t cap = (int64_t)dev_cu * 16;
@@ -1257,89 +740,28 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
     set_error("rt_trace: max_bounces > 8 requires the traced buffer (scratch rows)");
     return -1;
   }
-  // BVH meshes: trace the rows in direction-sorted order (K4: 2.98 -> 2.06 ms);
-  // brute-force meshes gain nothing from it (every face is tested anyway) and keep row order.
-  void* sort_ws = nullptr;
+  // BVH meshes: trace the rows in direction-sorted order (K4: 2.98 -> 2.06 ms), the
+  // order cached per (device, ray_offset, n); brute-force meshes gain nothing from it (every face is
+  // tested anyway) and keep row order.
   if (g_poison >= 0) {
     const int rc = poison_pool((size_t)256 << 20, stream);
     if (rc) return rc;
   }
   const bool sort = bvh && n >= kSortMinRays && n <= INT32_MAX;
-  const bool windows = sort && RT_XCD_WINDOWS && n >= 64 * (int64_t)kDirWinRows;
-  if (sort) trace_mark(0, stream);
   if (sort) {
-    a.order = windows          ? dir_order_windows(ray_offset, n, stream, &sort_ws)
-              : RT_TRACE_ZBAND ? dir_order_banded(ray_offset, n, stream, &sort_ws)
-                               : dir_order(ray_offset, n, stream, &sort_ws);
+    trace_mark(0, stream);
+    a.order = dir_order_cached(ray_offset, n, stream);
     if (!a.order) return -1;
-    a.win_chunks = windows ? kDirWinRows / 256 : 0;
     trace_mark(1, stream);
   }
-  // xcd_chunk needs whole groups of 8 blocks (one per XCD)
-  const int grid = windows ? (grid0 + 7) / 8 * 8 : grid0;
-  if (RT_WAVEFRONT && bvh && a.order && B <= 8) {
-    const int64_t tiles = (n + kWfTile - 1) / kWfTile;
-    const size_t st_bytes = (size_t)n * 32, pts_bytes = (size_t)(B + 1) * n * 16;
-    const size_t bytes = 2 * st_bytes + pts_bytes + (size_t)n * 3 + (size_t)tiles * 4 + 64 + 256;
-    void* wf = nullptr;
-    RT_HIP(hipMallocAsync(&wf, bytes, stream));
-    WfArgs w{};
-    w.t = a;
-    w.B = B;
-    char* q = (char*)wf;
-    w.st_a = (float4*)q;
-    q += st_bytes;
-    w.st_b = (float4*)q;
-    q += st_bytes;
-    w.pts = (float4*)q;
-    q += pts_bytes;
-    w.cnt = (unsigned*)q;
-    q += 64;
-    w.tile_cnt = (int32_t*)q;
-    q += (size_t)tiles * 4;
-    w.alive = (uint8_t*)q;
-    q += n;
-    w.last_rx = (int8_t*)q;
-    q += n;
-    w.npts = (int8_t*)q;
-    hipEvent_t wev0 = nullptr, wev1 = nullptr;
-    trace_events(&wev0, &wev1);
-    if (wev0) RT_HIP(hipEventRecord(wev0, stream));
-    const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 8192);
-    hipLaunchKernelGGL(k_wf_start, dim3(g), dim3(256), 0, stream, w);
-    float4* cur = w.st_a;
-    float4* nxt = w.st_b;
-    for (int b = 0; b < B; ++b) {
-      hipLaunchKernelGGL(k_wf_bounce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, w, b, cur);
-      if (b + 1 < B) {
-        hipLaunchKernelGGL(k_wf_count, dim3((unsigned)tiles), dim3(256), 0, stream, w, b);
-        hipLaunchKernelGGL(k_wf_scatter, dim3((unsigned)tiles), dim3(256), 0, stream, w, b, cur, nxt);
-        std::swap(cur, nxt);
-      }
-    }
-    switch (B) {
-#define RT_WF_ROWS(BB) \
-  case BB:             \
-    hipLaunchKernelGGL(k_wf_rows<BB>, dim3(g), dim3(256), 0, stream, w); \
-    break;
-      RT_WF_ROWS(1) RT_WF_ROWS(2) RT_WF_ROWS(3) RT_WF_ROWS(4) RT_WF_ROWS(5) RT_WF_ROWS(6) RT_WF_ROWS(7) RT_WF_ROWS(8)
-#undef RT_WF_ROWS
-      default:
-        break;
-    }
-    if (wev1) RT_HIP(hipEventRecord(wev1, stream));
-    RT_HIP(hipGetLastError());
-    RT_HIP(hipFreeAsync(wf, stream));
-    if (sort_ws) RT_HIP(hipFreeAsync(sort_ws, stream));
-    return 0;
-  }
+  const int grid = grid0;
   // profiling: the kernel's own dispatch packet carries the start/stop timestamps
   // (hipExtLaunchKernelGGL), so timing adds no marker packets -- and no gaps -- to the stream
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   trace_events(&ev0, &ev1);
-  // BVH kernels store only the received rows (RT_SPARSE_RX): the fill comes first, inside the
+  // BVH kernels store only the received rows (trace_body): the fill comes first, inside the
   // profiled span (its start event, the trace kernel's stop event)
-  const bool fill = RT_SPARSE_RX && bvh && B <= 8 && (received || mask);
+  const bool fill = bvh && B <= 8 && (received || mask);
   if (fill) {
     const unsigned gf = (unsigned)std::min<int64_t>((n * (B + 1) * 3 / 4 + 255) / 256, 4096);
     if (ev0) hipExtLaunchKernelGGL(k_fill_received, dim3(gf), dim3(256), 0, stream, ev0, nullptr, 0, received,
@@ -1359,7 +781,7 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
     if (bvh) {                                                                                       \
       RT_LAUNCH((k_trace_bvh<BB>), a);                                                               \
     } else {                                                                                         \
-      if (lds > 48 * 1024) /* up to 192 faces + the ray queue: above the 64 KB default */             \
+      if (lds > 48 * 1024) /* up to 192 faces: above the 48 KB default */                                       \
         RT_HIP(hipFuncSetAttribute((const void*)k_trace_bf<BB, false>,                              \
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));           \
       RT_LAUNCH((k_trace_bf<BB, false>), a);                                                         \
@@ -1375,7 +797,6 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
 #undef RT_LAUNCH
   if (a.fused) hipLaunchKernelGGL(k_trace_cir_tail, dim3(1), dim3(512), 0, stream, a.fz, n, received, B + 1);
   RT_HIP(hipGetLastError());
-  if (sort_ws) RT_HIP(hipFreeAsync(sort_ws, stream));
   return 0;
 }
 
