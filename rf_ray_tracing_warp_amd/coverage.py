@@ -215,7 +215,8 @@ class Coverage:
         """power_from_records for (n, 4) int64 rows of trace_rows' layout arriving as consecutive
         segments, counts[t] rows from rank t (exchange_rows' output).  Each segment must be in
         trace_rows' order (strictly ascending keys): the segments are merged, not sorted, and other
-        orders give a wrong map, not an error (use power_from_records without counts for those)."""
+        orders give a wrong map (the bucketed owner stage flags rows outside their segment's key range,
+        reported by check(); use power_from_records without counts for unordered records)."""
         import torch
         n = int(rows.shape[0]) if rows.dim() == 2 else 0
         if n and (tuple(rows.shape) != (n, 4) or not rows.is_contiguous() or rows.dtype != torch.int64):
@@ -280,10 +281,23 @@ class Coverage:
         self.last_candidates = int(stats[0])
         return self.power
 
+    def check(self):
+        """Raise if the device flagged this plan's earlier asynchronous stages (rt_coverage_check: a
+        look-back wait that gave up, or received rows the owner stage rejected -- those results are
+        wrong).  Synchronizes the plan's stream; run() calls it after every map."""
+        out = np.zeros(2, np.int64)
+        check(lib().rt_coverage_check(self._h, out.ctypes.data, _lib.stream_handle(self.device)), "rt_coverage_check")
+
+    def reduce_path(self):
+        """Which reduce the last calls took: {'records': bucketed?, 'owner': bucketed?} (diagnostic)."""
+        v = int(lib().rt_coverage_reduce_path(self._h))
+        return {"records": bool(v & 1), "owner": bool(v & 2)}
+
     def run(self, tx_pos, tx_power=1, process_group=None):
         """Power map (nz, ny, nx) float64 on the host; with a process group, sum-reduced over ranks."""
         import torch
         p = self.run_device(tx_pos, tx_power, process_group)
+        self.check()
         if process_group is not None or self.shard_count > 1:
             import torch.distributed as dist
             with torch.cuda.device(self.device):
