@@ -182,14 +182,10 @@ int rt_coverage_power_packed(rt_coverage* cov, const uint64_t* rows, const int64
                              int64_t n_bins, double alpha, double* power, void* stream);
 /* Errors the device detected in this plan's earlier asynchronous stages, reported and cleared
  * (synchronises `stream`): out[0] = look-back waits that gave up (the sums of that call are wrong),
- * out[1] = received rows the owner stage rejected (a cell of another owner, or a segment not in
- * ascending key order: that power map is wrong).  RT_EHIP when either is nonzero.  out may be NULL.
+ * out[1] = received rows of a segment not in strictly ascending key order (the owner stage's
+ * precondition: that power map is wrong).  RT_EHIP when either is nonzero.  out may be NULL.
  * (The owner stage returns before the device has run; Coverage.run checks after every map.) */
 int rt_coverage_check(rt_coverage* cov, int64_t* out, void* stream);
-/* Which reduce the plan's last calls took (diagnostic): bit 0 = its last record reduce (trace stage
- * or one-GPU map), bit 1 = its last owner stage, set when the bucketed reduce ran (rt_bucket.h),
- * clear for the sort-based one (RFRT_BUCKETS=0, or inputs beyond the bucketed path's bounds). */
-int rt_coverage_reduce_path(const rt_coverage* cov);
 /* f64 amplitudes (finite, >= 0, below 2^56) -> the exact fixed-point sums of rt_coverage_records
  * (truncated below 2^-136), on the device. */
 int rt_coverage_amps_to_sums(const double* amps, int64_t n, uint64_t* sums, void* stream);

@@ -283,15 +283,10 @@ class Coverage:
 
     def check(self):
         """Raise if the device flagged this plan's earlier asynchronous stages (rt_coverage_check: a
-        look-back wait that gave up, or received rows the owner stage rejected -- those results are
-        wrong).  Synchronizes the plan's stream; run() calls it after every map."""
+        look-back wait that gave up, or an owner-stage segment out of key order -- those results
+        are wrong).  Synchronizes the plan's stream; run() calls it after every map."""
         out = np.zeros(2, np.int64)
         check(lib().rt_coverage_check(self._h, out.ctypes.data, _lib.stream_handle(self.device)), "rt_coverage_check")
-
-    def reduce_path(self):
-        """Which reduce the last calls took: {'records': bucketed?, 'owner': bucketed?} (diagnostic)."""
-        v = int(lib().rt_coverage_reduce_path(self._h))
-        return {"records": bool(v & 1), "owner": bool(v & 2)}
 
     def run(self, tx_pos, tx_power=1, process_group=None):
         """Power map (nz, ny, nx) float64 on the host; with a process group, sum-reduced over ranks."""

@@ -28,7 +28,6 @@
 // cells*N*B*(env + receiver) queries.  Results equal the per-cell reference loop (tests compare
 // against the oracle's per-cell trace + NumPy power); cells are sharded by x column (ix % ranks).
 #include <hipcub/hipcub.hpp>
-#include <rocprim/rocprim.hpp>
 #include <math.h>
 
 #include <algorithm>
@@ -1194,12 +1193,13 @@ struct SegOffsets {
   int nseg;
 };
 __global__ __launch_bounds__(256) void k_merge_segments(const uint64_t* keys, int64_t kstride, SegOffsets so,
-                                                        uint64_t* keys_out, int64_t* idx_out) {
+                                                        uint64_t* keys_out, int64_t* idx_out, unsigned* bad) {
   const int64_t n = so.off[so.nseg];
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     int sg = 0;
     while (sg + 1 < so.nseg && so.off[sg + 1] <= i) ++sg;
     const uint64_t k = keys[i * kstride];
+    if (i > so.off[sg] && keys[(i - 1) * kstride] >= k) atomicAdd(bad, 1u);  // precondition: strictly ascending
     int64_t pos = i - so.off[sg];
     for (int t = 0; t < so.nseg; ++t) {
       if (t == sg) continue;
@@ -1223,12 +1223,14 @@ __global__ __launch_bounds__(256) void k_merge_segments(const uint64_t* keys, in
 // (52 us for a K5 owner's 465k records, profiles/r3zg_k5_rank_timeline.txt).
 template <int NS>
 __global__ __launch_bounds__(256) void k_merge_lockstep(const uint64_t* keys, int64_t kstride, SegOffsets so,
-                                                        int steps, uint64_t* keys_out, int64_t* idx_out) {
+                                                        int steps, uint64_t* keys_out, int64_t* idx_out,
+                                                        unsigned* bad) {
   const int64_t n = so.off[so.nseg];
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     int sg = 0;
     while (sg + 1 < so.nseg && so.off[sg + 1] <= i) ++sg;
     const uint64_t k = keys[i * kstride];
+    if (i > so.off[sg] && keys[(i - 1) * kstride] >= k) atomicAdd(bad, 1u);  // precondition: strictly ascending
     int64_t a[NS], len[NS];
 #pragma unroll
     for (int t = 0; t < NS; ++t) {
@@ -1739,16 +1741,6 @@ struct rt_coverage {
   float* trx = nullptr;
   int64_t* list = nullptr;
   ReplayItem* ritems = nullptr;  // first wins, in candidate order
-  // bucketed reduce (rt_bucket.h), grow-only: staged tile rows, fine-bucket regions, the [tile][fine]
-  // counts and their prefix, region starts, per-segment bounds (owner stage), rocPRIM scan workspace
-  uint64_t *bk_stage = nullptr, *bk_rows = nullptr;
-  int64_t bk_rows_cap = 0;  // rows of bk_stage (and of bk_rows)
-  int32_t *bk_tcnt = nullptr, *bk_pos = nullptr, *bk_tuniq = nullptr, *bk_blk = nullptr;
-  int64_t bk_cnt_cap = 0, bk_tiles_cap = 0;
-  int64_t *bk_fs = nullptr, *bk_lb = nullptr;
-  void* bk_tmp = nullptr;
-  size_t bk_tmp_bytes = 0;
-  int bk_path = 0;  // rt_coverage_reduce_path: bit 0 records, bit 1 owner stage took the buckets
   uint64_t* items = nullptr;
   int64_t item_cap = 0;
   unsigned long long* counters = nullptr;  // [0] candidates, [1] column items, [2] replay list (int64)
@@ -2047,7 +2039,7 @@ struct OwnerRuns {
   int64_t n;
   uint64_t* states;      // [tiles] look-back words
   unsigned long long* ticket;
-  uint64_t ticket_base, tag;
+  uint64_t tag;
   unsigned* errors;
   uint64_t* ukeys;
   double *uamps, *tcos, *tsin, *ev;
@@ -2063,7 +2055,7 @@ __global__ __launch_bounds__(256) void k_owner_runs(OwnerRuns a) {
   __shared__ int s_w[4];
   __shared__ int64_t s_prefix;
   if (threadIdx.x == 0)
-    s_tile = (uint32_t)(atomicAdd(a.ticket, 1ull) - a.ticket_base);
+    s_tile = (uint32_t)atomicAdd(a.ticket, 1ull);
   if (blockIdx.x == 0 && threadIdx.x == 0) *a.nbig = 0u;  // k_power_small lists the big cells afresh
   __syncthreads();
   const int64_t tile = s_tile;
@@ -2212,7 +2204,7 @@ struct SendRuns {
   uint64_t* states;
   uint64_t *agg_tail, *inc_tail;  // [tiles][5] tagged words
   unsigned long long* ticket;
-  uint64_t ticket_base, tag;
+  uint64_t tag;
   unsigned* errors;
   WideKey wk;
   int world, own_shift;
@@ -2232,7 +2224,7 @@ __global__ __launch_bounds__(256) void k_send_runs(SendRuns a) {
   __shared__ SegFx s_ws[4];
   __shared__ int64_t s_prefix;
   __shared__ Fx192 s_carry;
-  if (threadIdx.x == 0) s_tile = (uint32_t)(atomicAdd(a.ticket, 1ull) - a.ticket_base);
+  if (threadIdx.x == 0) s_tile = (uint32_t)atomicAdd(a.ticket, 1ull);
   __syncthreads();
   const int64_t tile = s_tile;
   const int64_t i0 = tile * kSendTile + (int64_t)threadIdx.x * kSendItems;
@@ -2415,20 +2407,19 @@ __global__ __launch_bounds__(256) void k_send_runs(SendRuns a) {
   }
 }
 
-#include "rt_bucket.h"
-
 __global__ __launch_bounds__(256) void k_amps_to_fx(const double* amps, int64_t n, Fx192* sums) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     sums[i] = fx_from_double(amps[i]);
 }
 
-void free_cands(rt_coverage* c) {
+int free_cands(rt_coverage* c, hipStream_t s) {
   // Work still in flight may read these buffers: the early window replay is launched before the
   // host sees the candidate counts, and an overflow regrows the buffers right after (a K3 rank of
   // 4 with 250k rays overflows the initial 8-per-ray capacity on its first run: the replay then
   // read freed memory, an illegal address in the N = 4 rehearsal, profiles/r4zb_rehearse_4.log).
-  // Growth is rare (first runs), so wait for the device here.
-  (void)hipDeviceSynchronize();
+  // Growth is rare (first runs), so wait for the plan's stream here (s: the stream of the call that
+  // grows; the plan's work is ordered on it).  A fault of earlier work surfaces as this call's error.
+  RT_HIP(hipStreamSynchronize(s));
   for (void* q : {(void*)c->keys, (void*)c->keys_sorted, (void*)c->okeys, (void*)c->okeys_sorted, (void*)c->ukeys,
                   (void*)c->oamps, (void*)c->oamps_sorted, (void*)c->uamps, (void*)c->tcos, (void*)c->tsin, (void*)c->ev,
                   (void*)c->win, (void*)c->trx,
@@ -2451,6 +2442,7 @@ void free_cands(rt_coverage* c) {
   c->rord = nullptr;
   c->rord_bytes = 0;
   c->cap = 0;
+  return RT_OK;
 }
 
 
@@ -2479,8 +2471,8 @@ hipError_t sort_records(void* tmp, size_t& bytes, const uint64_t* kin, uint64_t*
   return rocprim::radix_sort_pairs(tmp, bytes, kin, kout, vin, vout, (unsigned)n, 0u, (unsigned)end_bit, s);
 }
 
-int alloc_cands(rt_coverage* c, int64_t cap) {
-  free_cands(c);
+int alloc_cands(rt_coverage* c, int64_t cap, hipStream_t s) {
+  if (int rc = free_cands(c, s)) return rc;
   RT_HIP(hipMalloc(&c->keys, cap * 8));
   RT_HIP(hipMalloc(&c->keys_sorted, cap * 8));
   RT_HIP(hipMalloc(&c->okeys, cap * 8));
@@ -2525,8 +2517,8 @@ int alloc_cands(rt_coverage* c, int64_t cap) {
   return RT_OK;
 }
 
-int alloc_items(rt_coverage* c, int64_t cap) {
-  (void)hipDeviceSynchronize();  // as free_cands: nothing in flight may still read the old list
+int alloc_items(rt_coverage* c, int64_t cap, hipStream_t s) {
+  RT_HIP(hipStreamSynchronize(s));  // as free_cands: nothing in flight may still read the old list
   if (c->items) (void)hipFree(c->items);
   c->items = nullptr;
   RT_HIP(hipMalloc(&c->items, cap * 8));
@@ -2882,11 +2874,11 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
       return RT_EHIP;
     }
     if (nitems > c->item_cap) {
-      int rc = alloc_items(c, nitems + nitems / 4 + 1024);
+      int rc = alloc_items(c, nitems + nitems / 4 + 1024, s);
       if (rc) return rc;
       continue;  // keys were produced from a truncated item list: redo
     }
-    int rc = alloc_cands(c, ncand + ncand / 4 + 1024);
+    int rc = alloc_cands(c, ncand + ncand / 4 + 1024, s);
     if (rc) return rc;
   }
   if (ncand > ((int64_t)1 << 31) - 1) {
@@ -2914,9 +2906,9 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
 
 Fx192* plan_sums(rt_coverage* c) { return reinterpret_cast<Fx192*>(c->ev); }  // 32 B per slot, free until k_terms
 
-int grow_for(rt_coverage* c, int64_t n) {
+int grow_for(rt_coverage* c, int64_t n, hipStream_t s) {
   // records gathered from several ranks can outgrow this rank's candidate buffers
-  return n > c->cap ? alloc_cands(c, n + n / 4 + 1024) : RT_OK;
+  return n > c->cap ? alloc_cands(c, n + n / 4 + 1024, s) : RT_OK;
 }
 
 // exact sums of the runs of sorted records (keys in c->okeys_sorted) into c->ukeys / plan_sums /
@@ -2942,7 +2934,7 @@ int run_sums(rt_coverage* c, Val val, int64_t n, WideKey wk, hipStream_t s) {
 // sort + exact reduce of this plan's records (c->okeys / c->oamps or caller buffers)
 int cov_reduce(rt_coverage* c, const uint64_t* keys, const double* amps, int64_t n, int sort_bits, WideKey wk,
                hipStream_t s) {
-  int rc = grow_for(c, n);
+  int rc = grow_for(c, n, s);
   if (rc) return rc;
   size_t tb = c->tmp_bytes;
   RT_HIP(sort_records(c->tmp, tb, keys, c->okeys_sorted, amps, c->oamps_sorted, n, sort_bits < 64 ? sort_bits : 64, s));
@@ -2952,7 +2944,7 @@ int cov_reduce(rt_coverage* c, const uint64_t* keys, const double* amps, int64_t
 // owner stage: received (compact key, Fx192 sum) records -> sorted by key (index payload), summed
 int cov_reduce_sums(rt_coverage* c, const uint64_t* keys, const Fx192* sums, int64_t n, int sort_bits, WideKey wk,
                     hipStream_t s) {
-  int rc = grow_for(c, n);
+  int rc = grow_for(c, n, s);
   if (rc) return rc;
   int64_t* idx = reinterpret_cast<int64_t*>(c->oamps);  // filled by k_compact_keys
   int64_t* idx_sorted = reinterpret_cast<int64_t*>(c->oamps_sorted);
@@ -3006,175 +2998,6 @@ int cov_power(rt_coverage* c, int64_t nrec, int64_t n_bins, double alpha, double
   RT_HIP(hipGetLastError());
   return RT_OK;
 }
-
-// ---- host side of the bucketed reduce (rt_bucket.h)
-// RFRT_BUCKETS=0: the round-4 sort-based reduce instead (A/B and equivalence tests);
-// RFRT_BUCKET_CAP=k: rows per k_bucket round (default and maximum 4096; small values exercise the
-// key-ordered rounds of oversized ranges in the tests)
-bool bk_enabled() {
-  const char* e = getenv("RFRT_BUCKETS");
-  return !(e && e[0] == '0');
-}
-int bk_cap() {
-  const char* e = getenv("RFRT_BUCKET_CAP");
-  const int v = e ? atoi(e) : kBkTile;
-  return v >= 16 && v <= kBkTile ? v : kBkTile;
-}
-// the whole reduce fits the rounds' guarantee: a key has at most one row per tile, so at most
-// ntiles rows in a range; ranges of one key must fit a round
-// Rank-sized reduces only: at a whole map's size (K3 7.9M records, K5 6.4M) the sort passes run at
-// full throughput and the sort-based reduce measured faster (K3 map 4.2 vs 9.2 ms, r5b/r5c)
-constexpr int64_t kBkMaxRecords = 2 << 20;
-bool bk_fits(int64_t nrec) { return nrec <= kBkMaxRecords && (nrec + kBkTile - 1) / kBkTile <= (int64_t)bk_cap(); }
-
-// Fine buckets of 2^cs consecutive (owner-local) cells, all bins: top = owner + cell bits of the key;
-// about 512 rows per fine bucket, at most kBkMaxFine buckets, never fewer than one per owner.
-struct BkGeom {
-  int cs, nf, fshift;
-};
-BkGeom bk_geom(int own_bits, int cell_bits, int bin_bits, int64_t n) {
-  const int top = own_bits + cell_bits;
-  int want = bits_for((uint64_t)std::max<int64_t>(n / 512, 1));
-  want = std::max(want, own_bits);
-  want = std::min(want, std::min(top, bits_for((uint64_t)kBkMaxFine) - 1));
-  BkGeom g;
-  g.cs = top - want;
-  g.nf = 1 << want;
-  g.fshift = bin_bits + g.cs;
-  return g;
-}
-
-int bk_reserve(rt_coverage* c, int64_t rows, int64_t ntiles, int nf) {
-  if (rows > c->bk_rows_cap) {
-    for (uint64_t* q : {c->bk_stage, c->bk_rows})
-      if (q) (void)hipFree(q);
-    if (c->bk_blk) (void)hipFree(c->bk_blk);
-    c->bk_stage = c->bk_rows = nullptr;
-    c->bk_blk = nullptr;
-    const int64_t r = rows + rows / 4 + kBkTile;
-    RT_HIP(hipMalloc(&c->bk_stage, (size_t)(r + kBkTile) * 32));
-    RT_HIP(hipMalloc(&c->bk_rows, (size_t)r * 32));
-    RT_HIP(hipMalloc(&c->bk_blk, (size_t)(r / kBkTarget + 8) * 4));
-    c->bk_rows_cap = r;
-  }
-  const int64_t ncnt = ntiles * nf + 1;
-  if (ncnt > c->bk_cnt_cap) {
-    for (int32_t* q : {c->bk_tcnt, c->bk_pos})
-      if (q) (void)hipFree(q);
-    if (c->bk_tmp) (void)hipFree(c->bk_tmp);
-    c->bk_tcnt = c->bk_pos = nullptr;
-    c->bk_tmp = nullptr;
-    const int64_t m = ncnt + ncnt / 4 + 4096;
-    RT_HIP(hipMalloc(&c->bk_tcnt, (size_t)m * 4));
-    RT_HIP(hipMalloc(&c->bk_pos, (size_t)m * 4));
-    size_t tb = 0;
-    using It = rocprim::transform_iterator<rocprim::counting_iterator<uint32_t>, TileCountsFT, int32_t>;
-    RT_HIP(rocprim::exclusive_scan(nullptr, tb, It(rocprim::counting_iterator<uint32_t>(0), TileCountsFT{}),
-                                   c->bk_pos, 0, (size_t)m, rocprim::plus<int32_t>()));
-    RT_HIP(hipMalloc(&c->bk_tmp, tb));
-    c->bk_tmp_bytes = tb;
-    c->bk_cnt_cap = m;
-  }
-  if (ntiles > c->bk_tiles_cap) {
-    if (c->bk_tuniq) (void)hipFree(c->bk_tuniq);
-    c->bk_tuniq = nullptr;
-    RT_HIP(hipMalloc(&c->bk_tuniq, (size_t)(ntiles + 1024) * 4));
-    c->bk_tiles_cap = ntiles + 1024;
-  }
-  if (!c->bk_fs) {
-    RT_HIP(hipMalloc(&c->bk_fs, (size_t)(kBkMaxFine + 1) * 8));
-    RT_HIP(hipMalloc(&c->bk_lb, (size_t)kBkMaxSegs * (kBkMaxFine + 1) * 8));
-  }
-  return RT_OK;
-}
-
-// fill the look-back fields of a k_bucket launch (tickets are zeroed by the kernel before it)
-void bk_lookback(rt_coverage* c, BucketArgs& a) {
-  a.states = c->own_states;
-  a.ticket = c->own_aux;
-  a.errors = reinterpret_cast<unsigned*>(c->own_aux + 1);
-  a.tag = (c->own_tag++ % 0xFFFFFEull + 1ull) << 40;
-  a.nuniq = c->nuniq;
-  a.cap = bk_cap();
-}
-
-// The records of this plan's replay (c->okeys / c->oamps, nrec of them, compact keys) through
-// k_tile_reduce, the prefix of the [tile][fine] counts and k_tile_scatter, then k_bucket<MODE> with
-// `a` (its mode's output fields filled by the caller).
-template <int MODE>
-int bk_reduce_records(rt_coverage* c, const KeyBits& kb, int sort_bits, int64_t nrec, BucketArgs a, hipStream_t s) {
-  const int64_t ntiles = (nrec + kBkTile - 1) / kBkTile;
-  const BkGeom g = bk_geom(kb.own, kb.cell, kb.bin, nrec);
-  int rc = bk_reserve(c, nrec, ntiles, g.nf);
-  if (rc) return rc;
-  TileArgs ta{};
-  ta.keys = c->okeys;
-  ta.amps = c->oamps;
-  ta.n = nrec;
-  ta.fshift = g.fshift;
-  ta.fbits = bits_for((uint64_t)g.nf) - 1;
-  ta.ntiles = ntiles;
-  ta.stage = c->bk_stage;
-  ta.tcnt = c->bk_tcnt;
-  ta.tuniq = c->bk_tuniq;
-  ta.ticket = c->own_aux;
-  hipLaunchKernelGGL(k_tile_reduce, dim3((unsigned)ntiles), dim3(kBkThreads), 0, s, ta);
-  using It = rocprim::transform_iterator<rocprim::counting_iterator<uint32_t>, TileCountsFT, int32_t>;
-  size_t tb = c->bk_tmp_bytes;
-  RT_HIP(rocprim::exclusive_scan(c->bk_tmp, tb,
-                                 It(rocprim::counting_iterator<uint32_t>(0), TileCountsFT{c->bk_tcnt, ntiles, g.nf}),
-                                 c->bk_pos, 0, (size_t)(ntiles * g.nf + 1), rocprim::plus<int32_t>(), s));
-  ScatterArgs sa{};
-  sa.stage = c->bk_stage;
-  sa.tuniq = c->bk_tuniq;
-  sa.pos = c->bk_pos;
-  sa.ntiles = ntiles;
-  sa.fshift = g.fshift;
-  sa.nf = g.nf;
-  sa.rows = c->bk_rows;
-  sa.fs = c->bk_fs;
-  const unsigned nblocks = (unsigned)(nrec / kBkTarget + 2);
-  sa.blk_f0 = c->bk_blk;
-  sa.nblocks = (int)nblocks;
-  hipLaunchKernelGGL(k_tile_scatter, dim3((unsigned)ntiles), dim3(kBkThreads), 0, s, sa);
-  a.rows = c->bk_rows;
-  a.fs = c->bk_fs;
-  a.blk_f0 = c->bk_blk;
-  a.lb = nullptr;
-  a.nseg = 0;
-  a.nf = g.nf;
-  a.kk.bin_bits = kb.bin;
-  a.kk.cs = g.cs;
-  a.kk.cell_bits = kb.cell;
-  a.kk.wide_in = 0;
-  a.kk.nx = c->grid.nx;
-  a.kk.world = c->ray_mode ? c->nshard : 1;
-  a.kk.owner = 0;
-  a.kk.wk = wide_key(c, kb);
-  bk_lookback(c, a);
-  hipLaunchKernelGGL(k_bucket<MODE>, dim3(nblocks), dim3(kBkThreads), 0, s, a);
-  RT_HIP(hipGetLastError());
-  return RT_OK;
-}
-
-// the power-mode outputs of k_bucket (terms and cell ranges for k_power_small / k_power)
-void bk_power_fields(rt_coverage* c, BucketArgs& a, int64_t n_bins, double alpha) {
-  a.ukeys = c->ukeys;
-  a.usums = nullptr;  // plan_sums aliases the ev terms
-  a.uamps = c->uamps;
-  a.tcos = c->tcos;
-  a.tsin = c->tsin;
-  a.ev = c->ev;
-  a.ncell = cov_ncell(c);
-  a.cstart = c->cstart;
-  a.cend = c->cend;
-  a.cepoch = c->cepoch;
-  a.epoch = ++c->range_epoch;
-  a.nbig = reinterpret_cast<unsigned*>(c->runs + 3 * c->cap + 1);
-  a.P = power_params(n_bins, alpha);
-  a.world = 1;
-  a.own_shift = 64;
-}
 }  // namespace
 
 extern "C" {
@@ -3223,8 +3046,8 @@ int rt_coverage_create(int device, const rt_mesh* env, int max_bounces, int64_t 
     rt_coverage_destroy(c);
     return rt::hip_fail(e, "rt_coverage_create");
   }
-  rc = alloc_cands(c, std::max<int64_t>(1 << 20, 8 * n_rays));
-  if (!rc) rc = alloc_items(c, std::max<int64_t>(1 << 20, 8 * n_rays));
+  rc = alloc_cands(c, std::max<int64_t>(1 << 20, 8 * n_rays), nullptr);  // nothing in flight yet
+  if (!rc) rc = alloc_items(c, std::max<int64_t>(1 << 20, 8 * n_rays), nullptr);
   if (rc) {
     rt_coverage_destroy(c);
     return rc;
@@ -3236,12 +3059,10 @@ int rt_coverage_create(int device, const rt_mesh* env, int max_bounces, int64_t 
 int rt_coverage_destroy(rt_coverage* c) {
   if (!c) return RT_OK;
   rt::DeviceGuard dg(c->device);
-  free_cands(c);
+  (void)hipDeviceSynchronize();  // the plan does not know its callers' streams; errors are not reported here
+  (void)free_cands(c, nullptr);
   if (c->traj) (void)hipFree(c->traj);
   if (c->ray_order) (void)hipFree(c->ray_order);
-  for (void* q : {(void*)c->bk_stage, (void*)c->bk_rows, (void*)c->bk_tcnt, (void*)c->bk_pos, (void*)c->bk_tuniq,
-                  (void*)c->bk_fs, (void*)c->bk_lb, c->bk_tmp, (void*)c->bk_blk})
-    if (q) (void)hipFree(q);
   if (c->nseg) (void)hipFree(c->nseg);
   if (c->counters) (void)hipFree(c->counters);
   if (c->nuniq) (void)hipFree(c->nuniq);
@@ -3279,24 +3100,14 @@ int rt_coverage_run(rt_coverage* c, const float* tx_pos, double tx_power, double
   if (rc) return rc;
   // records grouped by (cell, bin) and summed exactly (Fx192); dropped records (~0) sort last
   prof_mark(c, 6, s);
-  bool ranges_done = false;
   if (nlist > 0) {
     const KeyBits kb = key_bits(c, n_bins);
-    if (bk_enabled() && bk_fits(nlist)) {  // bucketed reduce: terms and cell ranges written too
-      BucketArgs a{};
-      bk_power_fields(c, a, n_bins, alpha);
-      rc = bk_reduce_records<kBkPower>(c, kb, record_sort_bits(c, kb, n_bins), nlist, a, s);
-      ranges_done = true;
-      c->bk_path |= 1;
-    } else {
-      c->bk_path &= ~1;
-      rc = cov_reduce(c, c->okeys, c->oamps, nlist, record_sort_bits(c, kb, n_bins), wide_key(c, kb), s);
-    }
+    rc = cov_reduce(c, c->okeys, c->oamps, nlist, record_sort_bits(c, kb, n_bins), wide_key(c, kb), s);
     if (rc) return rc;
   } else {
     RT_HIP(hipMemsetAsync(c->nuniq, 0, 8, s));
   }
-  rc = cov_power(c, nlist, n_bins, alpha, power, s, ranges_done);
+  rc = cov_power(c, nlist, n_bins, alpha, power, s);
   if (rc) return rc;
   prof_mark(c, 7, s);
   if (stats) {
@@ -3401,24 +3212,8 @@ int trace_records_impl(rt_coverage* c, const float* tx_pos, double tx_power, dou
   if (nlist > 0) {
     const KeyBits kb = key_bits(c, n_bins);
     // the send buffers are filled before the host synchronizes (no launch after it)
-    if (bk_enabled() && bk_fits(nlist)) {
-      BucketArgs a{};
-      a.ukeys = c->ukeys;
-      a.usums = plan_sums(c);
-      a.uamps = c->uamps;
-      a.out = keys_out;
-      a.sums_out = (Fx192*)sums_out;
-      a.packed = packed ? 1 : 0;
-      a.out_cap = keys_out ? max_out : 0;
-      a.bounds = c->bounds;
-      a.world = world;
-      a.own_shift = own_shift(c);
-      rc = bk_reduce_records<kBkSend>(c, kb, record_sort_bits(c, kb, n_bins), nlist, a, s);
-      if (rc) return rc;
-      c->bk_path |= 1;
-    } else {
-      c->bk_path &= ~1;
-      if ((rc = grow_for(c, nlist))) return rc;
+    {
+      if ((rc = grow_for(c, nlist, s))) return rc;
       RT_HIP(hipMemsetAsync(c->own_aux, 0, 8, s));  // the ticket counter (k_send_runs takes tiles from it)
       size_t tb = c->tmp_bytes;
       const int sb = record_sort_bits(c, kb, n_bins);
@@ -3433,7 +3228,6 @@ int trace_records_impl(rt_coverage* c, const float* tx_pos, double tx_power, dou
       a.inc_tail = a.agg_tail + 5 * (c->cap / kOwnTile + 2);
       a.ticket = c->own_aux;
       a.errors = reinterpret_cast<unsigned*>(c->own_aux + 1);
-      a.ticket_base = 0;
       a.tag = (c->own_tag++ % 0xFFFFFEull + 1ull) << 40;
       a.wk = wide_key(c, kb);
       a.world = world;
@@ -3462,8 +3256,8 @@ int trace_records_impl(rt_coverage* c, const float* tx_pos, double tx_power, dou
       RT_HIP(hipMemset(c->own_aux + 1, 0, 8));
       rt::set_error((c->hbounds[world + 1] & 0xFFFFFFFFll)
                         ? "rt_coverage_trace_records: a look-back wait timed out (results discarded)"
-                        : "rt_coverage_trace_records: the previous owner stage received rows of another owner's "
-                          "cells or out of key order (its power map was wrong)");
+                        : "rt_coverage_trace_records: the previous owner stage received a segment out of key "
+                          "order (its power map was wrong; rt_coverage_check reports it)");
       return RT_EHIP;
     }
   }
@@ -3541,7 +3335,7 @@ int rt_coverage_power_records(rt_coverage* c, const uint64_t* keys, const uint64
   if (n > 0) {
     // received (cell << 32 | bin) keys -> compact [cell | bin]; the partial sums are exact
     // fixed point, so their order is irrelevant
-    if ((rc = grow_for(c, n))) return rc;
+    if ((rc = grow_for(c, n, s))) return rc;
     KeyBits kb = key_bits(c, n_bins);
     kb.ray = 0;
     kb.own = 0;
@@ -3607,53 +3401,8 @@ int power_segments_impl(rt_coverage* c, const uint64_t* keys, const uint64_t* su
   c->ev_rec[6] = c->ev_rec[7] = false;
   prof_mark(c, 6, s);
   bool fused = false;
-  if (n > 0 && stride == 4 && bk_enabled() && nseg <= kBkMaxSegs) {
-    // bucketed owner stage (rt_bucket.h): every fine bucket's range in every segment, then one
-    // block per range of buckets gathers, sorts and sums its rows and writes terms and cell ranges
-    if ((rc = grow_for(c, n))) return rc;
-    const int world = c->nshard;
-    const int64_t nown = (c->grid.nx + world - 1) / world * c->grid.ny * c->grid.nz;
-    const KeyBits kb = key_bits(c, n_bins);
-    const BkGeom g = bk_geom(0, std::max(1, bits_for((uint64_t)(nown - 1))), kb.bin, n);
-    if ((rc = bk_reserve(c, 0, 0, g.nf))) return rc;
-    SegBoundsArgs sb{};
-    sb.ticket = c->own_aux;
-    sb.rows = keys;
-    for (int t = 0; t <= nseg; ++t) sb.off[t] = so.off[t];
-    sb.nseg = nseg;
-    int64_t longest = 0;
-    for (int t = 0; t < nseg; ++t) longest = std::max<int64_t>(longest, seg_counts[t]);
-    sb.steps = bits_for((uint64_t)longest);
-    BucketArgs a{};
-    a.kk.bin_bits = kb.bin;
-    a.kk.cs = g.cs;
-    a.kk.cell_bits = 0;
-    a.kk.wide_in = 1;
-    a.kk.nx = c->grid.nx;
-    a.kk.world = world;
-    a.kk.owner = c->shard;
-    sb.kk = a.kk;
-    sb.nf = g.nf;
-    sb.lb = c->bk_lb;
-    sb.fs = c->bk_fs;
-    const dim3 gsb((unsigned)((g.nf + 1 + 255) / 256));
-    if (nseg <= 8) hipLaunchKernelGGL(k_seg_bounds<8>, gsb, dim3(256), 0, s, sb);
-    else if (nseg <= 16) hipLaunchKernelGGL(k_seg_bounds<16>, gsb, dim3(256), 0, s, sb);
-    else hipLaunchKernelGGL(k_seg_bounds<kBkMaxSegs>, gsb, dim3(256), 0, s, sb);
-    bk_power_fields(c, a, n_bins, alpha);
-    a.rows = keys;
-    a.fs = c->bk_fs;
-    a.lb = c->bk_lb;
-    a.nseg = nseg;
-    a.nf = g.nf;
-    bk_lookback(c, a);
-    hipLaunchKernelGGL(k_bucket<kBkPower>, dim3((unsigned)(n / kBkTarget + 2)), dim3(kBkThreads), 0, s, a);
-    RT_HIP(hipGetLastError());
-    fused = true;
-    c->bk_path |= 2;
-  } else if (n > 0) {
-    c->bk_path &= ~2;
-    if ((rc = grow_for(c, n))) return rc;
+  if (n > 0) {
+    if ((rc = grow_for(c, n, s))) return rc;
     int64_t* idx_sorted = reinterpret_cast<int64_t*>(c->oamps_sorted);
     // (G lanes per element, one binary search each, then a group sum: no faster on K3's 200k
     // records, 46 -> 76 us on K5's 465k -- the searches' loads, not their latency, set the time)
@@ -3661,14 +3410,17 @@ int power_segments_impl(rt_coverage* c, const uint64_t* keys, const uint64_t* su
     for (int t = 0; t < nseg; ++t) longest = std::max<int64_t>(longest, seg_counts[t]);
     const int steps = bits_for((uint64_t)longest);  // a search over len keys takes <= bits(len) halvings
     const dim3 gm((unsigned)std::min<int64_t>((n + 255) / 256, 8192));
+    // segments out of key order: counted in the high word of own_aux[1] (rt_coverage_check)
+    unsigned* bad = reinterpret_cast<unsigned*>(c->own_aux + 1) + 1;
+    RT_HIP(hipMemsetAsync(c->own_aux, 0, 8, s));  // k_owner_runs' ticket counter
     if (nseg <= 2)
-      hipLaunchKernelGGL(k_merge_lockstep<2>, gm, dim3(256), 0, s, keys, stride, so, steps, c->okeys_sorted, idx_sorted);
+      hipLaunchKernelGGL(k_merge_lockstep<2>, gm, dim3(256), 0, s, keys, stride, so, steps, c->okeys_sorted, idx_sorted, bad);
     else if (nseg <= 4)
-      hipLaunchKernelGGL(k_merge_lockstep<4>, gm, dim3(256), 0, s, keys, stride, so, steps, c->okeys_sorted, idx_sorted);
+      hipLaunchKernelGGL(k_merge_lockstep<4>, gm, dim3(256), 0, s, keys, stride, so, steps, c->okeys_sorted, idx_sorted, bad);
     else if (nseg <= 8)
-      hipLaunchKernelGGL(k_merge_lockstep<8>, gm, dim3(256), 0, s, keys, stride, so, steps, c->okeys_sorted, idx_sorted);
+      hipLaunchKernelGGL(k_merge_lockstep<8>, gm, dim3(256), 0, s, keys, stride, so, steps, c->okeys_sorted, idx_sorted, bad);
     else
-      hipLaunchKernelGGL(k_merge_segments, gm, dim3(256), 0, s, keys, stride, so, c->okeys_sorted, idx_sorted);
+      hipLaunchKernelGGL(k_merge_segments, gm, dim3(256), 0, s, keys, stride, so, c->okeys_sorted, idx_sorted, bad);
     RT_HIP(hipGetLastError());
     if (nseg <= 8) {
       OwnerRuns a{};
@@ -3679,8 +3431,6 @@ int power_segments_impl(rt_coverage* c, const uint64_t* keys, const uint64_t* su
       a.ticket = c->own_aux;
       a.errors = reinterpret_cast<unsigned*>(c->own_aux + 1);
       const int64_t ntiles = (n + kOwnTile - 1) / kOwnTile;
-      a.ticket_base = 0;
-      RT_HIP(hipMemsetAsync(c->own_aux, 0, 8, s));  // the ticket counter (tiles in ticket order)
       a.tag = (c->own_tag++ % 0xFFFFFEull + 1ull) << 40;
       a.ukeys = c->ukeys;
       a.uamps = c->uamps;
@@ -3712,8 +3462,6 @@ int power_segments_impl(rt_coverage* c, const uint64_t* keys, const uint64_t* su
 }
 }  // namespace
 
-int rt_coverage_reduce_path(const rt_coverage* c) { return c ? c->bk_path : -1; }
-
 int rt_coverage_check(rt_coverage* c, int64_t* out, void* stream) {
   if (!c) {
     rt::set_error("rt_coverage_check: null plan");
@@ -3734,8 +3482,8 @@ int rt_coverage_check(rt_coverage* c, int64_t* out, void* stream) {
     RT_HIP(hipMemsetAsync(c->own_aux + 1, 0, 8, s));
     RT_HIP(hipStreamSynchronize(s));
     rt::set_error(timeouts ? "rt_coverage_check: a look-back wait timed out (the last results are wrong)"
-                           : "rt_coverage_check: received rows of another owner's cells or out of key order (the "
-                             "last power map is wrong)");
+                           : "rt_coverage_check: an owner-stage segment was out of key order (the last power "
+                             "map is wrong)");
     return RT_EHIP;
   }
   return RT_OK;

@@ -139,10 +139,9 @@ def test_coverage_on_bvh_terrain():
     cov.close()
 
 
-def _ray_sharded_rows(env, grid, tx, B, N, S, win=100e-9, env_mesh=None, paths=None):
+def _ray_sharded_rows(env, grid, tx, B, N, S, win=100e-9, env_mesh=None):
     """_ray_sharded through the packed path run() takes: trace_rows -> each owner's segments of
-    (key, sum) rows in source-rank order -> power_from_rows.  paths: a list that receives every
-    plan's reduce_path() after its owner stage."""
+    (key, sum) rows in source-rank order -> power_from_rows."""
     plans = [Coverage(env, 2.998e8, 100e9, win, B, N, grid, shard_index=r, shard_count=S, shard_mode="rays",
                       env_mesh=env_mesh) for r in range(S)]
     sent = []
@@ -160,8 +159,6 @@ def _ray_sharded_rows(env, grid, tx, B, N, S, win=100e-9, env_mesh=None, paths=N
         total += p.power_from_rows(torch.cat(parts), segs)
         p.check()
         irs.append(p.impulse_responses())
-        if paths is not None:
-            paths.append(p.reduce_path())
     for p in plans:
         p.close()
     return total.cpu().numpy(), irs
@@ -451,150 +448,30 @@ def test_owner_segments_many_cells(room, nseg):
     _owner_segments_case(room, nseg, sizes, 77 + nseg)
 
 
-class _env:
-    """Set environment variables of librfrt's reduce switches for the duration of a block (read by
-    the library at every call: RFRT_BUCKETS, RFRT_BUCKET_CAP)."""
-
-    def __init__(self, **kv):
-        self.kv = kv
-
-    def __enter__(self):
-        self.old = {k: os.environ.get(k) for k in self.kv}
-        os.environ.update(self.kv)
-
-    def __exit__(self, *exc):
-        for k, v in self.old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
-
-
-def _whole(env, grid, tx, B, N, win=100e-9):
-    cov = Coverage(env, 2.998e8, 100e9, win, B, N, grid)
-    p = cov.run_device(tx).cpu().numpy().copy()
-    ir = cov.impulse_responses()
-    path = cov.reduce_path()
-    cov.close()
-    return p, ir, path
-
-
-@pytest.mark.parametrize("S", [1, 3, 8])
-def test_bucketed_reduce_equals_sorted_reduce(room, S):
-    """The bucketed reduce (rt_bucket.h: tile sort-and-sum, fine-bucket regions, per-range LDS sort,
-    look-back) gives the round-4 sort-based reduce's maps and impulse responses bit for bit: the
-    one-GPU map, and the trace and owner stages of S ray shards (trace_rows / power_from_rows)."""
-    grid, tx, B, N = CoverageGrid(8.0, -2.5, 4.6, 0.37, 0.41, 0.4, 13, 12, 2), (10, 0, 5), 3, 60_000
-    with _env(RFRT_BUCKETS="0"):
-        w0, i0, path0 = _whole(room, grid, tx, B, N)
-        t0, irs0 = _ray_sharded_rows(room, grid, tx, B, N, S)
-    w1, i1, path1 = _whole(room, grid, tx, B, N)
-    paths = []
-    t1, irs1 = _ray_sharded_rows(room, grid, tx, B, N, S, paths=paths)
-    assert not path0["records"] and path1["records"]
-    assert all(p["records"] and (S == 1 or p["owner"]) for p in paths), paths
-    assert np.isfinite(w0).sum() >= 20
-    assert w0.tobytes() == w1.tobytes()
-    for x, y in zip(i0, i1):
-        assert x.tobytes() == y.tobytes()
-    assert t0.tobytes() == t1.tobytes()
-    for a, b in zip(irs0, irs1):
-        for x, y in zip(a, b):
-            assert x.tobytes() == y.tobytes()
-
-
-def test_bucketed_reduce_rounds_equal_one_pass(room):
-    """k_bucket's ranges above the per-round capacity go through key-ordered rounds (bisection on the
-    key): with a capacity of 64 rows nearly every range does; maps and impulse responses unchanged."""
-    grid, tx, B, N = CoverageGrid(8.0, -2.5, 4.6, 0.37, 0.41, 0.4, 13, 12, 2), (10, 0, 5), 3, 60_000
-    w1, i1, _ = _whole(room, grid, tx, B, N)
-    t1, irs1 = _ray_sharded_rows(room, grid, tx, B, N, 3)
-    with _env(RFRT_BUCKET_CAP="64"):
-        w2, i2, path = _whole(room, grid, tx, B, N)
-        paths = []
-        t2, irs2 = _ray_sharded_rows(room, grid, tx, B, N, 3, paths=paths)
-    assert path["records"] and all(p["records"] and p["owner"] for p in paths)
-    assert w1.tobytes() == w2.tobytes()
-    for x, y in zip(i1, i2):
-        assert x.tobytes() == y.tobytes()
-    assert t1.tobytes() == t2.tobytes()
-    for a, b in zip(irs1, irs2):
-        for x, y in zip(a, b):
-            assert x.tobytes() == y.tobytes()
-
-
-@pytest.mark.parametrize("nseg,cap", [(1, None), (3, None), (8, None), (8, "64")])
-def test_bucketed_owner_stage_every_sweep_path(room, nseg, cap):
-    """The bucketed owner stage (k_seg_bounds + k_bucket on packed rows, power_from_rows) on cells of
-    0 .. 9999 bins split over nseg sorted segments, against the sorted path on the same records: maps
-    and impulse responses bit for bit (a 9999-bin cell is one fine bucket far above a round's
-    capacity: key-ordered rounds inside one cell)."""
-    rng = np.random.default_rng(31 + nseg)
-    sizes = [0, 1, 2, 5, 16, 17, 64, 191, 192, 193, 400, 2500, 9999]
-    grid = CoverageGrid(0.0, 0.0, 5.0, 1.0, 1.0, 1.0, len(sizes), 1, 1)
-    n, win = 10000, 100e-9
-    keys = []
-    for c, K in enumerate(sizes):
-        for b in np.sort(rng.choice(n, K, replace=False)) if K else []:
-            keys.append((c << 32) | int(b))
-    keys = np.array(keys, np.uint64)
-    cov = Coverage(room, 2.998e8, 100e9, win, 3, 1000, grid, shard_mode="rays")
-    amps = torch.from_numpy(rng.uniform(1e-9, 1e-5, len(keys))).cuda()
-    from rf_ray_tracing_warp_amd.coverage import amps_to_sums
-    full = amps_to_sums(amps).cpu().numpy().view(np.uint64)
-    seg_rows = [[] for _ in range(nseg)]
-    for i, k in enumerate(keys):
-        parts = int(rng.integers(1, min(nseg, 3) + 1))
-        segs = rng.choice(nseg, parts, replace=False)
-        rest = full[i].copy()
-        for j, sg in enumerate(segs):
-            if j == parts - 1:
-                piece = rest.copy()
-            else:
-                piece = np.array([rest[0] & np.uint64(0xFFFFFFFF), 0, 0], np.uint64)
-                rest = rest - piece
-            seg_rows[sg].append((k, piece))
-    rows, counts = [], []
-    for rr in seg_rows:
-        rr.sort(key=lambda r: int(r[0]))
-        counts.append(len(rr))
-        rows += [np.concatenate([[r[0]], r[1]]) for r in rr]
-    rt = torch.from_numpy(np.array(rows, np.uint64).reshape(-1, 4).view(np.int64)).cuda()
-    kt = rt[:, 0].contiguous()
-    st = rt[:, 1:].contiguous()
-    ref = cov.power_from_records(kt, st).cpu().numpy().copy()
-    ri = cov.impulse_responses()
-    with _env(**({"RFRT_BUCKET_CAP": cap} if cap else {})):
-        got = cov.power_from_rows(rt, counts).cpu().numpy().copy()
-        cov.check()
-        assert cov.reduce_path()["owner"]
-    gi = cov.impulse_responses()
-    cov.close()
-    assert got.tobytes() == ref.tobytes()
-    assert np.isfinite(ref).sum() == sum(1 for K in sizes if K)
-    for x, y in zip(gi, ri):
-        assert x.tobytes() == y.tobytes()
-
-
-def test_bucketed_owner_stage_rejects_unordered_segments(room):
-    """Rows that break the segments' key order are flagged (Coverage.check raises) instead of giving a
-    silently wrong map.  (A disorder inside one block's range is harmless -- the block
-    sorts its rows -- so the case spans several blocks: 10000 cells, one row each, descending.)"""
-    n = 10000
+@pytest.mark.parametrize("nseg", [1, 3, 12])
+def test_owner_stage_rejects_unordered_segments(room, nseg):
+    """Received rows that break the owner stage's precondition (each segment strictly ascending) are
+    counted by the merge and reported by Coverage.check (RfrtError) instead of a silently wrong map
+    (ADVICE r4); the report clears, and the same rows in key order pass.  nseg 12 takes the
+    k_merge_segments path, 1 and 3 k_merge_lockstep."""
+    n = 240
     grid = CoverageGrid(0.0, 0.0, 5.0, 1.0, 1.0, 1.0, n, 1, 1)
     cov = Coverage(room, 2.998e8, 100e9, 100e-9, 3, 1000, grid, shard_mode="rays")
-    keys = np.array([(c << 32) | 7 for c in range(n)], np.uint64)[::-1].copy()
+    keys = np.array([(c << 32) | 7 for c in range(n)], np.uint64)
     rows = np.zeros((n, 4), np.uint64)
     rows[:, 0] = keys
     rows[:, 1] = 1 << 40
-    rt = torch.from_numpy(rows.view(np.int64)).cuda()
-    cov.power_from_rows(rt, [n])
+    counts = [n // nseg] * nseg
+    counts[-1] += n - sum(counts)
+    bad = rows.copy()
+    o = counts[0]
+    bad[o - 2], bad[o - 1] = rows[o - 1], rows[o - 2]  # two rows of the first segment swapped
     from rf_ray_tracing_warp_amd._lib import RfrtError
+    cov.power_from_rows(torch.from_numpy(bad.view(np.int64)).cuda(), counts)
     with pytest.raises(RfrtError, match="out of key order"):
         cov.check()
     cov.check()  # reported once, then cleared
-    # the same rows in key order: accepted
-    rt2 = torch.from_numpy(rows[::-1].copy().view(np.int64)).cuda()
-    cov.power_from_rows(rt2, [n])
+    good = cov.power_from_rows(torch.from_numpy(rows.view(np.int64)).cuda(), counts).cpu().numpy()
     cov.check()
+    assert np.isfinite(good).sum() == n
     cov.close()
