@@ -159,6 +159,17 @@ int rt_coverage_trace_records_to(rt_coverage* cov, const float* tx_pos, double t
 int rt_coverage_trace_records_packed(rt_coverage* cov, const float* tx_pos, double tx_power, double light_speed,
                                      double sample_rate, int flags, int64_t n_bins, uint64_t* rows_out,
                                      int64_t max_out, int64_t* counts, int64_t* stats, void* stream);
+/* rt_coverage_trace_records_packed in two halves, so a rank can exchange its send counts on the
+ * device (the RCCL all-to-all of the counts, queued on `stream`) before the host waits once for
+ * both: _async queues the trace stage and leaves the send counts in counts_dev (device int64
+ * [world]) without synchronising; _finish synchronises `stream` and returns the host counts and
+ * stats as rt_coverage_trace_records_packed does (stats[2] = 0: rows_out was too small, fetch with
+ * rt_coverage_records_packed).  Replaces the blocking count read of the reference-side all-to-all
+ * (coverage.py:38-57 has none: its loop is single-process). */
+int rt_coverage_trace_rows_async(rt_coverage* cov, const float* tx_pos, double tx_power, double light_speed,
+                                 double sample_rate, int flags, int64_t n_bins, uint64_t* rows_out, int64_t max_out,
+                                 int64_t* counts_dev, void* stream);
+int rt_coverage_trace_rows_finish(rt_coverage* cov, int64_t* counts, int64_t* stats, void* stream);
 /* keys_out (cell << 32 | bin), sums_out (3 uint64 per record): device, max_out >= sum(counts). */
 int rt_coverage_records(rt_coverage* cov, uint64_t* keys_out, uint64_t* sums_out, int64_t max_out, void* stream);
 /* The last trace's records as rt_coverage_trace_records_packed's 32-B rows (device, 16-B aligned,
@@ -171,9 +182,10 @@ int rt_coverage_power_records(rt_coverage* cov, const uint64_t* keys, const uint
 /* rt_coverage_power_records for records that arrive as nseg (<= 64) segments of seg_counts[t]
  * records (host array), segment t from rank t, each in rt_coverage_records' order (ascending keys,
  * no repeated key): the segments are merged by rank instead of sorted (one launch).
- * PRECONDITION, not checked: every segment strictly ascending -- what rt_coverage_records /
- * _trace_records_packed emit and an all-to-all delivers.  Records in any other order give a wrong
- * map, not an error; send them through rt_coverage_power_records (which sorts) instead. */
+ * PRECONDITION: every segment strictly ascending -- what rt_coverage_records /
+ * _trace_records_packed emit and an all-to-all delivers.  The merge counts violations on the
+ * device (the map is then wrong); rt_coverage_check reports them.  Unordered records go through
+ * rt_coverage_power_records (which sorts) instead. */
 int rt_coverage_power_segments(rt_coverage* cov, const uint64_t* keys, const uint64_t* sums, const int64_t* seg_counts,
                                int nseg, int64_t n_bins, double alpha, double* power, void* stream);
 /* rt_coverage_power_segments on received (key, sum) rows of rt_coverage_trace_records_packed's

@@ -79,6 +79,9 @@ def lib():
     L.rt_power_dense.argtypes = [_vp, _i64, _i64, ctypes.c_double, _vp, _i64, _vp, _vp]
     L.rt_coverage_profile.argtypes = [_vp, _int]
     L.rt_coverage_check.argtypes = [_vp, _vp, _vp]
+    L.rt_coverage_trace_rows_async.argtypes = [_vp, _vp, ctypes.c_double, ctypes.c_double, ctypes.c_double, _int,
+                                               _i64, _vp, _i64, _vp, _vp]
+    L.rt_coverage_trace_rows_finish.argtypes = [_vp, _vp, _vp, _vp]
     L.rt_coverage_last_profile.argtypes = [_vp, _vp, _int]
     L.rt_debug_poison.argtypes = [_int]
     L.rt_profile.argtypes = [_int]
@@ -94,6 +97,7 @@ def lib():
                  "rt_coverage_records_packed",
                  "rt_coverage_power_records", "rt_coverage_power_segments", "rt_coverage_trace_records_packed",
                  "rt_coverage_power_packed", "rt_coverage_amps_to_sums", "rt_coverage_profile", "rt_coverage_check",
+                 "rt_coverage_trace_rows_async", "rt_coverage_trace_rows_finish",
                  "rt_coverage_last_profile", "rt_debug_poison",
                  "rt_profile", "rt_trace_last_profile", "rt_trace_profile_stats",
                  "rt_power_dense", "rt_selftest_math", "rt_ray_dirs", "rt_query", "rt_selftest_fx"):

@@ -211,12 +211,50 @@ class Coverage:
         self.last_candidates = int(stats[0])
         return rows[:n], [int(c) for c in counts]
 
+    def trace_rows_async(self, tx_pos, tx_power=1):
+        """trace_rows without the host wait: queues the trace stage on the current stream and returns
+        the device (world,) int64 send counts; trace_rows_finish() then waits once and returns
+        (rows, counts) as trace_rows does.  Between the two a rank queues the all-to-all of the
+        counts (run_device, "nccl"), so one host wait serves the send and the receive counts."""
+        import torch
+
+        if self.shard_mode != "rays":
+            raise _lib.RfrtError("trace_rows_async needs shard_mode='rays'")
+        tx = np.ascontiguousarray(np.asarray(tx_pos, dtype=np.float64).astype(np.float32))
+        dev = f"cuda:{self.device}"
+        if getattr(self, "_rows", None) is None:
+            self._rows = torch.empty((max(self.ray_count * 2, 1 << 16), 4), dtype=torch.int64, device=dev)
+        if getattr(self, "_send_counts", None) is None:
+            self._send_counts = torch.empty(self.shard_count, dtype=torch.int64, device=dev)
+        check(lib().rt_coverage_trace_rows_async(
+            self._h, tx.ctypes.data, float(tx_power), float(self.light_speed_mps), float(self.sample_rate_hz),
+            cir_flags(self.light_speed_mps, self.sample_rate_hz), self.n_bins, ptr(self._rows), self._rows.shape[0],
+            ptr(self._send_counts), _lib.stream_handle(self.device)), "rt_coverage_trace_rows_async")
+        return self._send_counts
+
+    def trace_rows_finish(self):
+        """The host half of trace_rows_async: waits for the current stream; (rows, counts)."""
+        import torch
+
+        counts = np.zeros(self.shard_count, np.int64)
+        stats = np.zeros(3, np.int64)
+        check(lib().rt_coverage_trace_rows_finish(self._h, counts.ctypes.data, stats.ctypes.data,
+                                                  _lib.stream_handle(self.device)), "rt_coverage_trace_rows_finish")
+        n = int(counts.sum())
+        rows = self._rows
+        if n and not stats[2]:
+            self._rows = rows = torch.empty((n + n // 4 + 1024, 4), dtype=torch.int64, device=rows.device)
+            check(lib().rt_coverage_records_packed(self._h, ptr(rows), rows.shape[0], _lib.stream_handle(self.device)),
+                  "rt_coverage_records_packed")
+        self.last_candidates = int(stats[0])
+        return rows[:n], [int(c) for c in counts]
+
     def power_from_rows(self, rows, counts):
         """power_from_records for (n, 4) int64 rows of trace_rows' layout arriving as consecutive
         segments, counts[t] rows from rank t (exchange_rows' output).  Each segment must be in
-        trace_rows' order (strictly ascending keys): the segments are merged, not sorted, and other
-        orders give a wrong map (the bucketed owner stage flags rows outside their segment's key range,
-        reported by check(); use power_from_records without counts for unordered records)."""
+        trace_rows' order (strictly ascending keys): the segments are merged, not sorted.  The merge
+        counts keys out of order, and check() (run() calls it) raises on them: that map is wrong; use
+        power_from_records without counts for unordered records."""
         import torch
         n = int(rows.shape[0]) if rows.dim() == 2 else 0
         if n and (tuple(rows.shape) != (n, 4) or not rows.is_contiguous() or rows.dtype != torch.int64):
@@ -268,6 +306,14 @@ class Coverage:
 
     def _run_device(self, tx_pos, tx_power, process_group):
         if self.shard_mode == "rays":
+            if self.shard_count > 1 and rdist.device_collectives(process_group):
+                # RCCL: the counts' all-to-all is queued behind the trace stage, and one host wait
+                # (trace_rows_finish) returns the send and the receive counts together
+                sc = self.trace_rows_async(tx_pos, tx_power)
+                rc = rdist.exchange_counts_async(sc, process_group)
+                rows, counts = self.trace_rows_finish()
+                rows, counts = rdist.exchange_rows(rows, counts, process_group, recv_counts=rc.tolist())
+                return self.power_from_rows(rows, counts)
             rows, counts = self.trace_rows(tx_pos, tx_power)
             if self.shard_count > 1:
                 rows, counts = rdist.exchange_rows(rows, counts, process_group)

@@ -79,6 +79,8 @@ struct CovParams {
   // ((cell % nx) % own_world) above the cell, so one sort groups the records by destination
   int own_world, own_shift;
   int bin_bits, cell_bits;
+  // per-cell bits (k_clear_cells): no environment face within r_clear of the cell's centre, or null
+  const uint32_t* clear;
 };
 __device__ __forceinline__ float4 traj_p(const CovParams& p, int64_t r, int k) { return p.traj[2 * (r * p.B + k)]; }
 __device__ __forceinline__ float4 traj_d(const CovParams& p, int64_t r, int k) { return p.traj[2 * (r * p.B + k) + 1]; }
@@ -880,6 +882,14 @@ __device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab
   float rec_dist = acc.dist;
   int rec_nint = acc.nint;
   float3 d = dir;
+  // Clear receiver (k_clear_cells: no environment face within r_clear of the centre).  While pos is
+  // a hit on this cell's receiver, a receiver hit at t means the segment pos -> hit lies inside the
+  // ball (both ends on the icosphere, which is convex and inside the ball), so no environment face
+  // can be hit at t' <= t: the receiver wins (kernel.py:85) whatever the environment query returns,
+  // and it is skipped.  The typical record -- first win on entering the ball, the exit at the next
+  // bounce -- then needs no environment query at all.
+  const bool clear = p.clear && ((p.clear[(uint64_t)cell >> 5] >> (cell & 31)) & 1u);
+  bool inside = true;  // pos is a hit on this cell's receiver (the first win)
   for (int b = k0 + 1; b < p.B; ++b) {  // kernel.py:57-98 with this cell's receiver
     const rt::Shear s = rt::make_shear(pos, d);
     rt::Hit he, hr;
@@ -889,6 +899,15 @@ __device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab
     hr = USE_BVH ? rx_query_culled(L, p.g, cell, p.r_rx, pos, d)
                  : rx_query_culled<true>(L, p.g, cell, p.r_rx, pos, d);
     if (hr.face < 0 && b + 1 >= p.B) break;
+    if (clear && inside && hr.face >= 0) {
+      pos.x = fmaf(d.x, hr.t, pos.x);
+      pos.y = fmaf(d.y, hr.t, pos.y);
+      pos.z = fmaf(d.z, hr.t, pos.z);
+      acc.add(pos.x, pos.y, pos.z);
+      rec_dist = acc.dist;
+      rec_nint = acc.nint;
+      continue;
+    }
     if constexpr (RX_FIRST) {
       // the environment culled at the receiver's t: every environment hit with t <= hr.t is
       // still found exactly (rt_bvh.h), and one beyond it loses to the receiver whatever it is
@@ -905,7 +924,9 @@ __device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab
       acc.add(pos.x, pos.y, pos.z);
       rec_dist = acc.dist;  // received_paths = traced prefix through this point (kernel.py:89-90)
       rec_nint = acc.nint;
+      inside = true;
     } else if (env_hit) {
+      inside = false;
       // after the last bounce only a receiver hit could still change the record: an environment
       // hit there ends the path, its vertex (and its angle's f64 amplitude) unused
       if (b + 1 >= p.B) break;
@@ -937,6 +958,102 @@ __device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab
   const bool keep = bin < p.n_bins && rec_amp != 0.0;
   okey = keep ? record_key(p, cell, bin) : ~0ull;
   oamp = keep ? rec_amp : 0.0;
+}
+
+// ---- clear receivers: cells whose ball of radius r_clear (the receiver radius plus a pad far above
+// the f32 rounding of the icosphere's vertices, of a receiver hit point and of an environment t) holds
+// no point of any environment face.  Squared point-triangle distance in double (closest point by
+// Voronoi region); a degenerate face or a NaN compares as "not clear".  One thread per cell, once per
+// plan: brute force over the faces for table scenes, a ball-box walk of the 4-wide BVH otherwise (a
+// stack overflow also answers "not clear").
+__device__ __forceinline__ double pt_tri_d2(const double p[3], const double a[3], const double b[3], const double c[3]) {
+  double ab[3], ac[3], ap[3], bp[3], cp[3];
+  for (int i = 0; i < 3; ++i) {
+    ab[i] = b[i] - a[i];
+    ac[i] = c[i] - a[i];
+    ap[i] = p[i] - a[i];
+    bp[i] = p[i] - b[i];
+    cp[i] = p[i] - c[i];
+  }
+  auto dot = [](const double* x, const double* y) { return x[0] * y[0] + x[1] * y[1] + x[2] * y[2]; };
+  auto d2of = [&](double x, double y, double z) { return x * x + y * y + z * z; };
+  const double d1 = dot(ab, ap), d2 = dot(ac, ap);
+  if (d1 <= 0.0 && d2 <= 0.0) return dot(ap, ap);  // vertex a
+  const double d3 = dot(ab, bp), d4 = dot(ac, bp);
+  if (d3 >= 0.0 && d4 <= d3) return dot(bp, bp);  // vertex b
+  const double vc = d1 * d4 - d3 * d2;
+  if (vc <= 0.0 && d1 >= 0.0 && d3 <= 0.0) {  // edge ab
+    const double v = d1 / (d1 - d3);
+    return d2of(ap[0] - v * ab[0], ap[1] - v * ab[1], ap[2] - v * ab[2]);
+  }
+  const double d5 = dot(ab, cp), d6 = dot(ac, cp);
+  if (d6 >= 0.0 && d5 <= d6) return dot(cp, cp);  // vertex c
+  const double vb = d5 * d2 - d1 * d6;
+  if (vb <= 0.0 && d2 >= 0.0 && d6 <= 0.0) {  // edge ac
+    const double w = d2 / (d2 - d6);
+    return d2of(ap[0] - w * ac[0], ap[1] - w * ac[1], ap[2] - w * ac[2]);
+  }
+  const double va = d3 * d6 - d5 * d4;
+  if (va <= 0.0 && d4 - d3 >= 0.0 && d5 - d6 >= 0.0) {  // edge bc
+    const double w = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+    return d2of(bp[0] - w * (c[0] - b[0]), bp[1] - w * (c[1] - b[1]), bp[2] - w * (c[2] - b[2]));
+  }
+  const double den = 1.0 / (va + vb + vc), v = vb * den, w = vc * den;  // inside the face
+  return d2of(ap[0] - ab[0] * v - ac[0] * w, ap[1] - ab[1] * v - ac[1] * w, ap[2] - ab[2] * v - ac[2] * w);
+}
+__device__ __forceinline__ bool face_far(const double p[3], const float4 q0, const float4 q1, float c2z, double R2) {
+  const double a[3] = {q0.x, q0.y, q0.z}, b[3] = {q0.w, q1.x, q1.y}, c[3] = {q1.z, q1.w, c2z};
+  return pt_tri_d2(p, a, b, c) > R2;  // NaN: not far
+}
+template <bool USE_BVH>
+__global__ __launch_bounds__(256) void k_clear_cells(CovParams p, double r_clear, uint32_t* clear) {
+  const int64_t nc = ncells(p.g);
+  const double R2 = r_clear * r_clear;
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < nc; base += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t cell = base + threadIdx.x;
+    bool ok = cell < nc;
+    if (ok) {
+      double c[3];
+      cell_center(p.g, cell, c);
+      if constexpr (!USE_BVH) {
+        for (int f = 0; f < p.env_nf && ok; ++f)  // case 4 of the table: kx, ky, kz = x, y, z (raw corners)
+          ok = face_far(c, p.env_perm[f * 18 + 12], p.env_perm[f * 18 + 13], p.env_perm[f * 18 + 14].x, R2);
+      } else {
+        int st[RT_BVH_STACK];
+        int sp = 0;
+        st[sp++] = 0;
+        while (ok && sp > 0) {
+          const float4* w = p.env_bvh.wide + 8 * (int64_t)st[--sp];
+          const float4 lx = w[0], hx = w[1], ly = w[2], hy = w[3], lz = w[4], hz = w[5], rf = w[6];
+          const float L[3][4] = {{lx.x, lx.y, lx.z, lx.w}, {ly.x, ly.y, ly.z, ly.w}, {lz.x, lz.y, lz.z, lz.w}};
+          const float H[3][4] = {{hx.x, hx.y, hx.z, hx.w}, {hy.x, hy.y, hy.z, hy.w}, {hz.x, hz.y, hz.z, hz.w}};
+          const int ref[4] = {__float_as_int(rf.x), __float_as_int(rf.y), __float_as_int(rf.z), __float_as_int(rf.w)};
+          for (int q = 0; q < 4 && ok; ++q) {
+            if (ref[q] == -1) continue;
+            double d2 = 0.0;
+            for (int k = 0; k < 3; ++k) {
+              const double e = fmax(fmax((double)L[k][q] - c[k], c[k] - (double)H[k][q]), 0.0);
+              d2 += e * e;
+            }
+            if (!(d2 <= R2)) continue;  // the child's box misses the ball
+            if (ref[q] >= 0) {
+              if (sp < RT_BVH_STACK) st[sp++] = ref[q];
+              else ok = false;
+            } else {
+              const int pk = ~ref[q], first = pk >> 3, count = pk & 7;
+              for (int j = 0; j < count && ok; ++j) {
+                const float4* fr = p.env_bvh.lcomp + (int64_t)(first + j) * 3;
+                ok = face_far(c, fr[0], fr[1], fr[2].x, R2);
+              }
+            }
+          }
+        }
+      }
+    }
+    const uint64_t m = __ballot(ok);  // one 32-bit word per half wave (cells base + 32 h ..)
+    const int lane = threadIdx.x & 63;
+    if ((lane & 31) == 0 && cell < nc) clear[(uint64_t)cell >> 5] = (uint32_t)(m >> lane);
+  }
 }
 
 // Per candidate (cell, ray, k), in whatever order k_cells appended them: the exact receiver test
@@ -1741,6 +1858,8 @@ struct rt_coverage {
   float* trx = nullptr;
   int64_t* list = nullptr;
   ReplayItem* ritems = nullptr;  // first wins, in candidate order
+  uint32_t* clear = nullptr;      // clear receivers, one bit per cell (k_clear_cells), on the first run
+  bool clear_on = true;           // RFRT_COV_CLEAR=0 at creation: the replay always queries the environment
   uint64_t* items = nullptr;
   int64_t item_cap = 0;
   unsigned long long* counters = nullptr;  // [0] candidates, [1] column items, [2] replay list (int64)
@@ -1755,6 +1874,7 @@ struct rt_coverage {
   size_t rord_bytes = 0;
   int64_t* bounds = nullptr;   // ray mode: [world + 1] starts of each owner's run in the reduced records
   int64_t n_out = 0;           // ray mode: valid reduced records of the last rt_coverage_trace_records
+  int64_t pend_ncand = 0, pend_nlist = 0, pend_max_out = -1;  // trace stage awaiting its host half
   // rt_coverage_profile: stage events of the last run and its work counts (device, [0] traced
   // ray-bounces = sum of the trajectories' segments, [1] replayed ray-bounces)
   bool profile = false;
@@ -2407,6 +2527,11 @@ __global__ __launch_bounds__(256) void k_send_runs(SendRuns a) {
   }
 }
 
+// send counts from the owner bounds (rt_coverage_trace_rows_async: they stay on the device)
+__global__ __launch_bounds__(64) void k_bounds_to_counts(const int64_t* bounds, int world, int64_t* counts) {
+  for (int o = threadIdx.x; o < world; o += blockDim.x) counts[o] = bounds[o + 1] - bounds[o];
+}
+
 __global__ __launch_bounds__(256) void k_amps_to_fx(const double* amps, int64_t n, Fx192* sums) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     sums[i] = fx_from_double(amps[i]);
@@ -2716,6 +2841,20 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
   p.fs64 = sample_rate;
   p.flags = flags;
   p.n_bins = n_bins;
+  if (c->clear_on && !c->clear) {  // once per plan: the clear receivers (k_clear_cells)
+    const int64_t nc = c->grid.nx * c->grid.ny * c->grid.nz;
+    RT_HIP(hipMalloc(&c->clear, sizeof(uint32_t) * (size_t)((nc + 31) / 32)));
+    const double amax = fmax(fabs(c->grid.x0) + fabs(c->grid.dx) * (double)c->grid.nx,
+                             fmax(fabs(c->grid.y0) + fabs(c->grid.dy) * (double)c->grid.ny,
+                                  fabs(c->grid.z0) + fabs(c->grid.dz) * (double)c->grid.nz));
+    // the pad: 2e-3 r + 1e-4 (1 + |coordinates|), against ~1e-5 of f32 rounding in a hit point
+    const double r_clear = c->r_rx * (1.0 + 2e-3) + 1e-4 * (1.0 + amax);
+    const dim3 gcl((unsigned)std::min<int64_t>((nc + 255) / 256, 8192));
+    if (bvh) hipLaunchKernelGGL(k_clear_cells<true>, gcl, dim3(256), 0, s, p, r_clear, c->clear);
+    else hipLaunchKernelGGL(k_clear_cells<false>, gcl, dim3(256), 0, s, p, r_clear, c->clear);
+    RT_HIP(hipGetLastError());
+  }
+  p.clear = c->clear_on ? c->clear : nullptr;
   const size_t lds = bvh ? 0 : (size_t)p.env_nf * 18 * sizeof(float4);
   // k_replay: the deferred amplitude's B - 1 cosine columns follow the environment table
   const size_t lds_replay = lds + (size_t)std::max(p.B - 1, 1) * 256 * sizeof(float);
@@ -3028,6 +3167,10 @@ int rt_coverage_create(int device, const rt_mesh* env, int max_bounces, int64_t 
   c->r_rx = rx_radius;
   c->shard = shard_index;
   c->nshard = shard_count;
+  {
+    const char* e = getenv("RFRT_COV_CLEAR");  // A/B and equivalence tests
+    c->clear_on = !(e && e[0] == '0');
+  }
   hipError_t e = hipMalloc(&c->traj, sizeof(float4) * 2 * max_bounces * n_rays);
   if (e == hipSuccess) e = hipMalloc(&c->nseg, n_rays);
   if (e == hipSuccess) e = hipMalloc(&c->counters, 32);
@@ -3063,6 +3206,7 @@ int rt_coverage_destroy(rt_coverage* c) {
   (void)free_cands(c, nullptr);
   if (c->traj) (void)hipFree(c->traj);
   if (c->ray_order) (void)hipFree(c->ray_order);
+  if (c->clear) (void)hipFree(c->clear);
   if (c->nseg) (void)hipFree(c->nseg);
   if (c->counters) (void)hipFree(c->counters);
   if (c->nuniq) (void)hipFree(c->nuniq);
@@ -3162,9 +3306,10 @@ int rt_coverage_trace_records(rt_coverage* c, const float* tx_pos, double tx_pow
 }
 
 namespace {
-int trace_records_impl(rt_coverage* c, const float* tx_pos, double tx_power, double light_speed, double sample_rate,
+static int trace_records_impl(rt_coverage* c, const float* tx_pos, double tx_power, double light_speed, double sample_rate,
                        int flags, int64_t n_bins, uint64_t* keys_out, uint64_t* sums_out, bool packed,
-                       int64_t max_out, int64_t* counts, int64_t* stats, void* stream);
+                       int64_t max_out, int64_t* counts, int64_t* stats, void* stream, int64_t* counts_dev = nullptr);
+static int trace_rows_finish(rt_coverage* c, int64_t* counts, int64_t* stats, hipStream_t s);
 }
 
 int rt_coverage_trace_records_to(rt_coverage* c, const float* tx_pos, double tx_power, double light_speed,
@@ -3190,10 +3335,10 @@ int rt_coverage_trace_records_packed(rt_coverage* c, const float* tx_pos, double
 }
 
 namespace {
-int trace_records_impl(rt_coverage* c, const float* tx_pos, double tx_power, double light_speed, double sample_rate,
+static int trace_records_impl(rt_coverage* c, const float* tx_pos, double tx_power, double light_speed, double sample_rate,
                        int flags, int64_t n_bins, uint64_t* keys_out, uint64_t* sums_out, bool packed,
-                       int64_t max_out, int64_t* counts, int64_t* stats, void* stream) {
-  if (!c || !c->ray_mode || !tx_pos || !counts || n_bins < 1 || n_bins >= ((int64_t)1 << 32)) {
+                       int64_t max_out, int64_t* counts, int64_t* stats, void* stream, int64_t* counts_dev) {
+  if (!c || !c->ray_mode || !tx_pos || (!counts && !counts_dev) || n_bins < 1 || n_bins >= ((int64_t)1 << 32)) {
     rt::set_error("rt_coverage_trace_records: invalid arguments (needs a plan from rt_coverage_create_rays)");
     return RT_EINVAL;
   }
@@ -3207,7 +3352,6 @@ int trace_records_impl(rt_coverage* c, const float* tx_pos, double tx_power, dou
   rc = cov_records(c, tx_pos, tx_power, light_speed, sample_rate, flags, n_bins, s, &ncand, &nlist);
   if (rc) return rc;
   // local exact sum per (owner, cell, bin); runs of each owner are then contiguous
-  std::vector<int64_t> b(world + 1, 0);
   prof_mark(c, 6, s);
   if (nlist > 0) {
     const KeyBits kb = key_bits(c, n_bins);
@@ -3250,27 +3394,71 @@ int trace_records_impl(rt_coverage* c, const float* tx_pos, double tx_power, dou
     // an earlier owner stage): their sums would be wrong, so the run fails instead
     RT_HIP(hipMemcpyAsync(c->hbounds, c->bounds, sizeof(int64_t) * (world + 1), hipMemcpyDeviceToHost, s));
     RT_HIP(hipMemcpyAsync(c->hbounds + world + 1, c->own_aux + 1, 8, hipMemcpyDeviceToHost, s));
-    RT_HIP(hipStreamSynchronize(s));
-    for (int o = 0; o <= world; ++o) b[o] = c->hbounds[o];
-    if (c->hbounds[world + 1]) {
-      RT_HIP(hipMemset(c->own_aux + 1, 0, 8));
-      rt::set_error((c->hbounds[world + 1] & 0xFFFFFFFFll)
-                        ? "rt_coverage_trace_records: a look-back wait timed out (results discarded)"
-                        : "rt_coverage_trace_records: the previous owner stage received a segment out of key "
-                          "order (its power map was wrong; rt_coverage_check reports it)");
-      return RT_EHIP;
-    }
+  } else {
+    for (int o = 0; o <= world + 1; ++o) c->hbounds[o] = 0;  // nothing sent (no copy in flight)
   }
-  for (int o = 0; o < world; ++o) counts[o] = b[o + 1] - b[o];
-  c->n_out = b[world];
+  c->pend_ncand = ncand;
+  c->pend_nlist = nlist;
+  c->pend_max_out = keys_out ? max_out : -1;
+  if (counts_dev) {  // deferred: the send counts on the device now, the host reads them at the finish
+    if (nlist > 0)
+      hipLaunchKernelGGL(k_bounds_to_counts, dim3(1), dim3(64), 0, s, c->bounds, world, counts_dev);
+    else
+      RT_HIP(hipMemsetAsync(counts_dev, 0, sizeof(int64_t) * world, s));
+    RT_HIP(hipGetLastError());
+    return RT_OK;
+  }
+  const int rcf = trace_rows_finish(c, counts, stats, s);
+  c->pend_max_out = -1;
+  return rcf;
+}
+
+// The host half of a trace stage: waits for the stream, then the bounds and the look-back error
+// word copied to pinned memory by trace_records_impl give the send counts.
+static int trace_rows_finish(rt_coverage* c, int64_t* counts, int64_t* stats, hipStream_t s) {
+  const int world = c->nshard;
+  RT_HIP(hipStreamSynchronize(s));
+  if (const int64_t w = c->hbounds[world + 1]) {
+    c->hbounds[world + 1] = 0;
+    RT_HIP(hipMemset(c->own_aux + 1, 0, 8));
+    rt::set_error((w & 0xFFFFFFFFll) ? "rt_coverage_trace_records: a look-back wait timed out (results discarded)"
+                                     : "rt_coverage_trace_records: the previous owner stage received a segment out "
+                                       "of key order (its power map was wrong)");
+    return RT_EHIP;
+  }
+  for (int o = 0; o < world; ++o) counts[o] = c->hbounds[o + 1] - c->hbounds[o];
+  c->n_out = c->hbounds[world];
   if (stats) {
-    stats[0] = ncand;
-    stats[1] = nlist;
-    stats[2] = keys_out && c->n_out <= max_out ? 1 : 0;  // the records are in keys_out / sums_out
+    stats[0] = c->pend_ncand;
+    stats[1] = c->pend_nlist;
+    stats[2] = c->pend_max_out >= 0 && c->n_out <= c->pend_max_out ? 1 : 0;  // the records are in the caller's buffer
   }
   return RT_OK;
 }
 }  // namespace
+
+int rt_coverage_trace_rows_async(rt_coverage* c, const float* tx_pos, double tx_power, double light_speed,
+                                 double sample_rate, int flags, int64_t n_bins, uint64_t* rows_out, int64_t max_out,
+                                 int64_t* counts_dev, void* stream) {
+  if (!rows_out || max_out < 0 || (reinterpret_cast<uintptr_t>(rows_out) & 15) || !counts_dev) {
+    rt::set_error("rt_coverage_trace_rows_async: invalid arguments (16-B aligned rows_out, max_out >= 0, counts_dev)");
+    return RT_EINVAL;
+  }
+  return trace_records_impl(c, tx_pos, tx_power, light_speed, sample_rate, flags, n_bins, rows_out, nullptr, true,
+                            max_out, nullptr, nullptr, stream, counts_dev);
+}
+
+int rt_coverage_trace_rows_finish(rt_coverage* c, int64_t* counts, int64_t* stats, void* stream) {
+  if (!c || !c->ray_mode || !counts || c->pend_max_out < 0) {
+    rt::set_error("rt_coverage_trace_rows_finish: invalid arguments (after rt_coverage_trace_rows_async)");
+    return RT_EINVAL;
+  }
+  rt::DeviceGuard dg(c->device);
+  RT_HIP(dg.err);
+  const int rc = trace_rows_finish(c, counts, stats, (hipStream_t)stream);
+  c->pend_max_out = -1;
+  return rc;
+}
 
 int rt_coverage_records(rt_coverage* c, uint64_t* keys_out, uint64_t* sums_out, int64_t max_out, void* stream) {
   if (!c || !c->ray_mode || (c->n_out > 0 && (!keys_out || !sums_out)) || max_out < c->n_out) {
@@ -3356,7 +3544,7 @@ int rt_coverage_power_records(rt_coverage* c, const uint64_t* keys, const uint64
 }
 
 namespace {
-int power_segments_impl(rt_coverage* c, const uint64_t* keys, const uint64_t* sums, int64_t stride,
+static int power_segments_impl(rt_coverage* c, const uint64_t* keys, const uint64_t* sums, int64_t stride,
                         const int64_t* seg_counts, int nseg, int64_t n_bins, double alpha, double* power, void* stream);
 }
 
@@ -3372,7 +3560,7 @@ int rt_coverage_power_packed(rt_coverage* c, const uint64_t* rows, const int64_t
 
 namespace {
 // stride 1: keys[n] and Fx192 sums[n]; stride 4: (key, sum) rows, keys = rows, sums = rows + 1
-int power_segments_impl(rt_coverage* c, const uint64_t* keys, const uint64_t* sums, int64_t stride,
+static int power_segments_impl(rt_coverage* c, const uint64_t* keys, const uint64_t* sums, int64_t stride,
                         const int64_t* seg_counts, int nseg, int64_t n_bins, double alpha, double* power, void* stream) {
   if (!c || !c->ray_mode || nseg < 1 || nseg > kMaxSegs || !seg_counts || !power || n_bins < 1 ||
       n_bins >= ((int64_t)1 << 32)) {

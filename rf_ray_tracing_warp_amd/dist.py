@@ -135,11 +135,37 @@ def reduce_max(value: float, device, group=None) -> float:
     return value
 
 
-def exchange_rows(rows, send_counts, group=None):
+def device_collectives(group=None):
+    """True when the group's collectives run on the GPU ("nccl" = RCCL): device tensors go in
+    as they are and the collectives are queued on the stream (gloo stages through the host)."""
+    import torch.distributed as dist
+    return dist.get_backend(group) == "nccl"
+
+
+def exchange_counts_async(send_counts_dev, group=None):
+    """All-to-all of the per-destination send counts, queued on the device (RCCL) behind the trace
+    stage that wrote them (Coverage.trace_rows_async).  Returns the receive counts in pinned host
+    memory, filled once the current stream reaches this point: read them after the stream has
+    been waited for (Coverage.trace_rows_finish does), so one host wait serves both counts."""
+    import torch
+    import torch.distributed as dist
+    rc = torch.empty_like(send_counts_dev)
+    dist.all_to_all_single(rc, send_counts_dev, group=group)
+    host = torch.empty(rc.shape, dtype=rc.dtype, pin_memory=True)
+    host.copy_(rc, non_blocking=True)
+    return host
+
+
+def exchange_rows(rows, send_counts, group=None, recv_counts=None):
     """Sparse all-to-all of packed coverage records: rows (n, w) int64 grouped by destination rank,
     send_counts[d] rows for rank d (Coverage.trace_rows).  One collective for the counts, one for
     the rows, nothing packed or unpacked around them.  Returns (received rows, in source-rank order;
-    the number of rows from each rank)."""
+    the number of rows from each rank).  recv_counts: the receive counts when the caller has them
+    already (exchange_counts_async), so only the rows move here.
+    The host needs the receive counts before the rows move: all_to_all_single takes its split sizes
+    and the output's size on the host (there is no device-side split form), so either this
+    function reads them (one blocking read) or the caller reads them in the same wait as its own
+    send counts (run_device on "nccl")."""
     import torch
     import torch.distributed as dist
     home = rows.device
@@ -147,10 +173,12 @@ def exchange_rows(rows, send_counts, group=None):
     send_counts = [int(c) for c in send_counts]
     n = sum(send_counts)
     w = int(rows.shape[1]) if rows.dim() == 2 else 4
-    sc = torch.tensor(send_counts, dtype=torch.int64, device=wire)
-    rc = torch.empty_like(sc)
-    dist.all_to_all_single(rc, sc, group=group)
-    recv_counts = [int(c) for c in rc.tolist()]
+    if recv_counts is None:
+        sc = torch.tensor(send_counts, dtype=torch.int64, device=wire)
+        rc = torch.empty_like(sc)
+        dist.all_to_all_single(rc, sc, group=group)
+        recv_counts = rc.tolist()
+    recv_counts = [int(c) for c in recv_counts]
     out = torch.empty((sum(recv_counts), w), dtype=torch.int64, device=wire)
     dist.all_to_all_single(out, rows[:n].reshape(n, w).to(wire), recv_counts, send_counts, group=group)
     return out.to(home), recv_counts

@@ -475,3 +475,82 @@ def test_owner_stage_rejects_unordered_segments(room, nseg):
     cov.check()
     assert np.isfinite(good).sum() == n
     cov.close()
+
+
+def _map_and_irs(env, grid, tx, B, N, clear):
+    old = os.environ.get("RFRT_COV_CLEAR")
+    os.environ["RFRT_COV_CLEAR"] = "1" if clear else "0"  # read at plan creation
+    try:
+        cov = Coverage(env, 2.998e8, 100e9, 100e-9, B, N, grid)
+    finally:
+        if old is None:
+            os.environ.pop("RFRT_COV_CLEAR")
+        else:
+            os.environ["RFRT_COV_CLEAR"] = old
+    p = cov.run_device(tx).cpu().numpy().copy()
+    irs = cov.impulse_responses()
+    cov.close()
+    return p, irs
+
+
+@pytest.mark.parametrize("grid,N,least", [
+    (CoverageGrid(-0.75, 1.55, 5.0, 0.125, 0.1, 1.0, 12, 10, 1), 20_000, 5),   # across the partition (x in +-0.4, y < 2)
+    (CoverageGrid(14.62, -14.95, 0.05, 0.09, 0.1, 0.11, 5, 4, 3), 50_000, 1),  # a corner: wall, wall and floor
+])
+def test_clear_receivers_equal_full_replay(room, grid, N, least):
+    """Cells whose receiver ball holds no environment face skip the replay's environment query while
+    the path is inside their receiver (k_clear_cells); cells at or inside walls keep it.  Maps and
+    impulse responses equal the replay that always queries (RFRT_COV_CLEAR=0) bit for bit, on grids
+    with both kinds of cell, and the oracle's per-cell loop within the coverage bar."""
+    tx, B = (10.0, 0.0, 5.0), 3
+    p0, i0 = _map_and_irs(room, grid, tx, B, N, clear=False)
+    p1, i1 = _map_and_irs(room, grid, tx, B, N, clear=True)
+    assert p0.tobytes() == p1.tobytes()
+    for x, y in zip(i0, i1):
+        assert x.tobytes() == y.tobytes()
+    cov = Coverage(room, 2.998e8, 100e9, 100e-9, B, N, grid)
+    power, ref = _compare(cov, grid, room, tx, B, N)
+    assert np.isfinite(ref).sum() >= least
+    cov.close()
+
+
+@pytest.mark.parametrize("S", [1, 3])
+def test_trace_rows_async_equals_trace_rows(room, S):
+    """The two-halves trace stage (trace_rows_async: no host wait, send counts left on the device;
+    trace_rows_finish: one wait) gives trace_rows' rows and counts bit for bit, and the device send
+    counts equal the host ones; a small first row buffer takes the fetch path in both."""
+    grid, tx, B, N = CoverageGrid(8.0, -2.5, 4.6, 0.37, 0.41, 0.4, 13, 12, 2), (10, 0, 5), 3, 60_000
+    for r in range(S):
+        a = Coverage(room, 2.998e8, 100e9, 100e-9, B, N, grid, shard_index=r, shard_count=S, shard_mode="rays")
+        b = Coverage(room, 2.998e8, 100e9, 100e-9, B, N, grid, shard_index=r, shard_count=S, shard_mode="rays")
+        b._rows = torch.empty((16, 4), dtype=torch.int64, device="cuda:0")  # forces the fetch
+        for _ in range(2):
+            r0, c0 = a.trace_rows(tx, 1)
+            r0 = r0.clone()
+            sc = b.trace_rows_async(tx, 1)
+            r1, c1 = b.trace_rows_finish()
+            assert c0 == c1 and sum(c0) > 0
+            assert sc.cpu().tolist() == c1
+            assert r0.cpu().numpy().tobytes() == r1.cpu().numpy().tobytes()
+        a.close()
+        b.close()
+
+
+def test_exchange_counts_async_over_rccl(room):
+    """dist.exchange_counts_async on a one-rank "nccl" (RCCL) group: the counts' all-to-all queued
+    on the stream and copied to pinned memory, read after one stream wait."""
+    import socket
+    import torch.distributed as dist
+    from rf_ray_tracing_warp_amd import dist as rdist
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        assert rdist.device_collectives()
+        sc = torch.tensor([12345], dtype=torch.int64, device="cuda:0")
+        host = rdist.exchange_counts_async(sc)
+        torch.cuda.current_stream().synchronize()
+        assert host.is_pinned() and host.tolist() == [12345]
+    finally:
+        dist.destroy_process_group()
