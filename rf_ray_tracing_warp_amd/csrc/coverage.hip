@@ -229,9 +229,18 @@ __device__ __forceinline__ void rx_group(const RxLds& L, const double c[3], cons
 // ROLLED: the 20-group ball test as a loop over the table (constants by scalar loads) instead of
 // unrolled -- fewer VGPRs (K3 k_replay 167 -> 125, so 4 waves per SIMD without spills), slower where
 // the occupancy does not change (k_win 0.95 -> 1.01 ms, K5 replay 1.23 -> 1.30 ms; r3zc)
+// lmask: the groups to consider, when a query on the same line from an earlier origin found them
+// already (its line_out: the groups whose padded ball the line passes and that are not wholly
+// behind that origin).  A query from a later origin on the line -- a replay that continues through
+// its receiver with the direction unchanged -- needs only those groups' origin-dependent tests
+// (behind the new origin, near / far): any other group's ball misses the line or lies behind the
+// earlier origin, so it holds no face the ray can meet.  The two origins' rounding moves the line by
+// ~1e-6 of the coordinates, far inside the pad.
+constexpr uint32_t kAllGroups = (1u << (RT_ICO1_NF / 4)) - 1;
 template <bool ROLLED = false>
 __device__ __forceinline__ rt::Hit rx_query_culled(const RxLds& L, const rt_grid& g, int64_t cell, double r, float3 o,
-                                                   float3 d) {
+                                                   float3 d, uint32_t lmask = kAllGroups,
+                                                   uint32_t* line_out = nullptr) {
   const rt::Shear s = rt::make_shear(o, d);
   double c[3];
   cell_center(g, cell, c);
@@ -261,18 +270,34 @@ __device__ __forceinline__ rt::Hit rx_query_culled(const RxLds& L, const rt_grid
   asm volatile("" : "+v"(z));
   const float4* gb = L.gb + z;
   const float* gmm = L.gmm + z;
+  if (lmask == kAllGroups) {
 #pragma unroll(ROLLED ? 1 : 4)
-  for (int gi = 0; gi < RT_ICO1_NF / 4; ++gi) {
-    const float4 m = gb[gi];
-    const float me = fmaf(m.x, ex, fmaf(m.y, ey, m.z * ez));
-    const float mu = fmaf(m.x, ux, fmaf(m.y, uy, m.z * uz));
-    const float R = m.w + pad;
-    const float dist2 = fmaf(-me, me, fmaf(-2.0f, mu, gmm[gi] + uu));
-    const bool ok = dist2 <= R * R && fmaf(me + R, inv_len, t0f) >= 0.0f;
-    if (ok && me <= 0.0f) near |= 1u << gi;
-    if (ok && me > 0.0f) {
-      far |= 1u << gi;
-      far_tmin = fminf(far_tmin, fmaf(me - R, inv_len, t0f));
+    for (int gi = 0; gi < RT_ICO1_NF / 4; ++gi) {
+      const float4 m = gb[gi];
+      const float me = fmaf(m.x, ex, fmaf(m.y, ey, m.z * ez));
+      const float mu = fmaf(m.x, ux, fmaf(m.y, uy, m.z * uz));
+      const float R = m.w + pad;
+      const float dist2 = fmaf(-me, me, fmaf(-2.0f, mu, gmm[gi] + uu));
+      const bool ok = dist2 <= R * R && fmaf(me + R, inv_len, t0f) >= 0.0f;
+      if (ok && me <= 0.0f) near |= 1u << gi;
+      if (ok && me > 0.0f) {
+        far |= 1u << gi;
+        far_tmin = fminf(far_tmin, fmaf(me - R, inv_len, t0f));
+      }
+    }
+    if (line_out) *line_out = near | far;
+  } else {
+    for (uint32_t q = lmask; q; q &= q - 1) {
+      const int gi = __builtin_ctz(q);
+      const float4 m = gb[gi];
+      const float me = fmaf(m.x, ex, fmaf(m.y, ey, m.z * ez));
+      const float R = m.w + pad;
+      const bool ok = fmaf(me + R, inv_len, t0f) >= 0.0f;
+      if (ok && me <= 0.0f) near |= 1u << gi;
+      if (ok && me > 0.0f) {
+        far |= 1u << gi;
+        far_tmin = fminf(far_tmin, fmaf(me - R, inv_len, t0f));
+      }
     }
   }
   rt::Hit h;
@@ -814,11 +839,24 @@ struct PathAccD {
     ++npts;
   }
 };
+// The factor of a vertex whose cosine is one of the kAmpTab floats at and just below 1 -- a path
+// through a receiver (its entry point is collinear with the points either side: the cosine
+// rounds to 1 or a few ulp below it) -- comes from a table that each block fills with the same
+// function of the same values, so the bits are the same; other cosines evaluate it.
+constexpr int kAmpTab = 128;
+__device__ __forceinline__ void stage_amp_tab(double* tab) {
+  for (int i = threadIdx.x; i < kAmpTab; i += blockDim.x)
+    tab[i] = bounce_amp((float)acos((double)__uint_as_float(0x3F800000u - (uint32_t)i)));
+}
 // amp0 times the factors of the first n interior vertices, in path order (tracer.py:104-113)
-__device__ __forceinline__ double amp_product(const float* cosv, int n, double amp0) {
+__device__ __forceinline__ double amp_product(const float* cosv, int n, double amp0, const double* tab) {
   double amp = amp0;
 #pragma unroll 1
-  for (int i = 0; i < n; ++i) amp *= bounce_amp((float)acos((double)cosv[256 * i]));
+  for (int i = 0; i < n; ++i) {
+    const float c = cosv[256 * i];
+    const uint32_t u = 0x3F800000u - __float_as_uint(c);  // ulps below 1 (wraps for c > 1, c < 0, NaN)
+    amp *= u < (uint32_t)kAmpTab ? tab[u] : bounce_amp((float)acos((double)c));
+  }
   return amp;
 }
 
@@ -843,9 +881,10 @@ __device__ __forceinline__ uint64_t record_key(const CovParams& p, int64_t cell,
 // Does the receiver of `cell` win bounce k of ray r (kernel.py:85: hit, and the environment missed
 // or is strictly farther)?  tr: the receiver's t.
 __device__ __forceinline__ bool rx_wins(const CovParams& p, const RxLds& L, int64_t cell, int64_t r, int k,
-                                        float& tr) {
+                                        float& tr, uint32_t* line_out) {
   const float4 tp = traj_p(p, r, k), td = traj_d(p, r, k);
-  const rt::Hit hr = rx_query_culled(L, p.g, cell, p.r_rx, make_float3(tp.x, tp.y, tp.z), make_float3(td.x, td.y, td.z));
+  const rt::Hit hr = rx_query_culled(L, p.g, cell, p.r_rx, make_float3(tp.x, tp.y, tp.z), make_float3(td.x, td.y, td.z),
+                                     kAllGroups, line_out);
   tr = hr.t;
   return hr.face >= 0 && (isinf(tp.w) || tp.w > hr.t);
 }
@@ -859,8 +898,9 @@ __device__ __forceinline__ bool rx_wins(const CovParams& p, const RxLds& L, int6
 // semantics of kernel.py:57-98, then the CIR body of tracer.py:101-117: the record's key (~0 when
 // the path adds nothing: delay past the window, or amplitude 0) and amplitude.
 template <bool USE_BVH, bool RX_FIRST>
-__device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab, const RxLds& L, int64_t cell,
-                                       int64_t r, int k0, float tr, uint64_t& okey, double& oamp) {
+__device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab, const RxLds& L, const double* amp_tab,
+                                       int64_t cell, int64_t r, int k0, float tr, uint32_t line, uint64_t& okey,
+                                       double& oamp) {
   // the B - 1 columns after the environment table in dynamic LDS (k_replay's launch sizes it)
   PathAccD acc;
   acc.cosv = reinterpret_cast<float*>(const_cast<float4*>(lds_tab) + (USE_BVH ? 0 : (size_t)p.env_nf * 18)) + threadIdx.x;
@@ -890,14 +930,17 @@ __device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab
   // bounce -- then needs no environment query at all.
   const bool clear = p.clear && ((p.clear[(uint64_t)cell >> 5] >> (cell & 31)) & 1u);
   bool inside = true;  // pos is a hit on this cell's receiver (the first win)
+  // while no environment hit has turned the ray, it is still on the first win's line: the receiver
+  // query needs only the groups that line passes (k_win found them)
+  uint32_t lmask = line ? line : kAllGroups;
   for (int b = k0 + 1; b < p.B; ++b) {  // kernel.py:57-98 with this cell's receiver
     const rt::Shear s = rt::make_shear(pos, d);
     rt::Hit he, hr;
     // receiver first: at the last bounce only a receiver hit can still change the record, so a
     // miss there ends the path without the environment query (K3: most first wins at bounce 0
     // leave their receiver at bounce 1 and miss it at bounce 2)
-    hr = USE_BVH ? rx_query_culled(L, p.g, cell, p.r_rx, pos, d)
-                 : rx_query_culled<true>(L, p.g, cell, p.r_rx, pos, d);
+    hr = USE_BVH ? rx_query_culled(L, p.g, cell, p.r_rx, pos, d, lmask)
+                 : rx_query_culled<true>(L, p.g, cell, p.r_rx, pos, d, lmask);
     if (hr.face < 0 && b + 1 >= p.B) break;
     if (clear && inside && hr.face >= 0) {
       pos.x = fmaf(d.x, hr.t, pos.x);
@@ -927,6 +970,7 @@ __device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab
       inside = true;
     } else if (env_hit) {
       inside = false;
+      lmask = kAllGroups;  // reflected: a new line
       // after the last bounce only a receiver hit could still change the record: an environment
       // hit there ends the path, its vertex (and its angle's f64 amplitude) unused
       if (b + 1 >= p.B) break;
@@ -944,7 +988,7 @@ __device__ __forceinline__ void replay(const CovParams& p, const float4* lds_tab
       break;
     }
   }
-  const double rec_amp = amp_product(acc.cosv, rec_nint, p.amp0);
+  const double rec_amp = amp_product(acc.cosv, rec_nint, p.amp0, amp_tab);
   double dl;
   if (p.flags & RT_CIR_C_F64) {
     dl = ((double)rec_dist / p.c64) * p.fs64;
@@ -1071,8 +1115,9 @@ __device__ __forceinline__ int64_t cand_count(const unsigned long long* n_dev, i
   return n > cap ? 0 : n;
 }
 __global__ __launch_bounds__(256, 6) void k_win(CovParams p, const uint64_t* keys, const unsigned long long* nkeys_dev,
-                                             int64_t cap, uint8_t* first_flag, float* trx) {
+                                             int64_t cap, uint8_t* first_flag, float* trx, uint32_t* gmask) {
   __shared__ RxLds L;
+  __shared__ uint32_t s_line[256];  // this lane's line groups, parked during the group tests
   stage_rx(L, p.r_rx);
   // the candidate count; past the capacity the keys have holes (k_cells skips a lane's keys that
   // would cross it) and the host reruns the attempt, so this one tests nothing
@@ -1095,7 +1140,9 @@ __global__ __launch_bounds__(256, 6) void k_win(CovParams p, const uint64_t* key
         if (!seg_ball(sq.o, sq.d, sq.tmax, cc, rp2)) continue;
       }
       float t;
-      const bool w = rx_wins(p, L, cell, r, q, t);
+      // the line's groups parked in LDS (no register held across the group tests); a winning
+      // earlier bounce leaves its own mask, unused: that candidate is no first win
+      const bool w = rx_wins(p, L, cell, r, q, t, s_line + threadIdx.x);
       if (q == k) {
         first = w;
         tr = t;
@@ -1106,6 +1153,7 @@ __global__ __launch_bounds__(256, 6) void k_win(CovParams p, const uint64_t* key
     }
     first_flag[i] = first ? 1 : 0;
     trx[i] = tr;
+    gmask[i] = s_line[threadIdx.x];
   }
 }
 
@@ -1122,7 +1170,7 @@ __global__ __launch_bounds__(256, 6) void k_win(CovParams p, const uint64_t* key
 struct ReplayItem {
   uint64_t key;
   float trx;
-  int32_t pad;
+  uint32_t line;  // the receiver groups the first win's line passes (rx_query_culled's lmask)
 };
 __device__ __forceinline__ int64_t sel_tile(int64_t n, int G) { return ((n + G - 1) / G + 255) / 256 * 256; }
 __device__ __forceinline__ int block_sum(int v, int* s4) {
@@ -1144,7 +1192,8 @@ __global__ __launch_bounds__(256) void k_sel_count(const uint8_t* flag, const un
 }
 __global__ __launch_bounds__(256) void k_sel_scatter(const uint8_t* flag, const unsigned long long* n_dev, int64_t cap,
                                                      const int32_t* counts, const uint64_t* keys, const float* trx,
-                                                     ReplayItem* items, unsigned long long* nlist) {
+                                                     const uint32_t* gmask, ReplayItem* items,
+                                                     unsigned long long* nlist) {
   __shared__ int s4[4];
   __shared__ int w4[4];
   const int64_t n = cand_count(n_dev, cap), tile = sel_tile(n, gridDim.x);
@@ -1165,7 +1214,7 @@ __global__ __launch_bounds__(256) void k_sel_scatter(const uint8_t* flag, const 
     const int step = w4[0] + w4[1] + w4[2] + w4[3];
     if (f) {
       const int64_t k = base + off + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-      items[k] = ReplayItem{keys[i], trx[i], 0};
+      items[k] = ReplayItem{keys[i], trx[i], gmask[i]};
     }
     base += step;
     __syncthreads();  // w4 is rewritten by the next step
@@ -1254,8 +1303,10 @@ __global__ __launch_bounds__(256, USE_BVH ? kReplayWavesBvh : kReplayWaves) void
                                                 const int32_t* order, uint64_t* out_key, double* out_amp) {
   extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
   __shared__ RxLds L;
+  __shared__ double s_amp[kAmpTab];
   if (nl_dev) nl = min(nl, (int64_t)*nl_dev);  // see k_replay_order
   if ((int64_t)blockIdx.x * blockDim.x >= nl) return;
+  stage_amp_tab(s_amp);  // made visible by stage_rx's barrier
   stage_rx(L, p.r_rx);
   stage_env<USE_BVH>(p, lds_tab);
   for (int64_t jl = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; jl < nl; jl += (int64_t)gridDim.x * blockDim.x) {
@@ -1265,7 +1316,8 @@ __global__ __launch_bounds__(256, USE_BVH ? kReplayWavesBvh : kReplayWaves) void
     // records at the processing position jl: their order is irrelevant (they are sorted by key
     // and summed exactly), and consecutive lanes then write consecutive 8-B words instead of
     // scattering them (K3 k_replay wrote 445 MB for 126 MB of records, r2zm)
-    replay<USE_BVH, RX_FIRST>(p, lds_tab, L, cell, r, (int)(key & 15), it.trx, out_key[jl], out_amp[jl]);
+    replay<USE_BVH, RX_FIRST>(p, lds_tab, L, s_amp, cell, r, (int)(key & 15), it.trx, it.line, out_key[jl],
+                              out_amp[jl]);
   }
 }
 
@@ -1856,7 +1908,7 @@ struct rt_coverage {
   uint8_t* win = nullptr;
   uint8_t* first_flag = nullptr;
   float* trx = nullptr;
-  int64_t* list = nullptr;
+  uint32_t* gmask = nullptr;  // per candidate: the receiver groups its line passes (k_win)
   ReplayItem* ritems = nullptr;  // first wins, in candidate order
   uint32_t* clear = nullptr;      // clear receivers, one bit per cell (k_clear_cells), on the first run
   bool clear_on = true;           // RFRT_COV_CLEAR=0 at creation: the replay always queries the environment
@@ -2548,14 +2600,14 @@ int free_cands(rt_coverage* c, hipStream_t s) {
   for (void* q : {(void*)c->keys, (void*)c->keys_sorted, (void*)c->okeys, (void*)c->okeys_sorted, (void*)c->ukeys,
                   (void*)c->oamps, (void*)c->oamps_sorted, (void*)c->uamps, (void*)c->tcos, (void*)c->tsin, (void*)c->ev,
                   (void*)c->win, (void*)c->trx,
-                  (void*)c->list, (void*)c->first_flag, c->tmp, c->rord, (void*)c->runs, (void*)c->ritems})
+                  (void*)c->gmask, (void*)c->first_flag, c->tmp, c->rord, (void*)c->runs, (void*)c->ritems})
     if (q) (void)hipFree(q);
   c->keys = c->keys_sorted = c->okeys = c->okeys_sorted = c->ukeys = nullptr;
   c->oamps = c->oamps_sorted = c->uamps = c->tcos = c->tsin = c->ev = nullptr;
   c->win = nullptr;
   c->first_flag = nullptr;
   c->trx = nullptr;
-  c->list = nullptr;
+  c->gmask = nullptr;
   c->ritems = nullptr;
   c->runs = nullptr;
   if (c->own_states) (void)hipFree(c->own_states);
@@ -2611,7 +2663,7 @@ int alloc_cands(rt_coverage* c, int64_t cap, hipStream_t s) {
   RT_HIP(hipMalloc(&c->ev, cap * 32));
   RT_HIP(hipMalloc(&c->first_flag, cap));
   RT_HIP(hipMalloc(&c->trx, cap * 4));
-  RT_HIP(hipMalloc(&c->list, cap * 8));
+  RT_HIP(hipMalloc(&c->gmask, cap * 4));
   RT_HIP(hipMalloc(&c->ritems, cap * sizeof(ReplayItem)));
   RT_HIP(hipMalloc(&c->runs, (cap * 3 + 64) * 4));  // tile heads / open-run indices (run_sums), counters
   // k_owner_runs' states: zero = no tag (tags start at 1 << 40)
@@ -2664,7 +2716,7 @@ int poison_plan(rt_coverage* c, hipStream_t s) {
               {c->okeys_sorted, (size_t)c->cap * 8}, {c->ukeys, (size_t)c->cap * 8}, {c->oamps, (size_t)c->cap * 8},
               {c->oamps_sorted, (size_t)c->cap * 8}, {c->uamps, (size_t)c->cap * 8}, {c->tcos, (size_t)c->cap * 8},
               {c->tsin, (size_t)c->cap * 8}, {c->ev, (size_t)c->cap * 32}, {c->first_flag, (size_t)c->cap},
-              {c->trx, (size_t)c->cap * 4}, {c->list, (size_t)c->cap * 8},
+              {c->trx, (size_t)c->cap * 4}, {c->gmask, (size_t)c->cap * 4},
               {c->ritems, (size_t)c->cap * sizeof(ReplayItem)}, {c->items, (size_t)c->item_cap * 8},
               {c->tmp, c->tmp_bytes}, {c->rord, c->rord_bytes}, {c->counters, 32}, {c->nuniq, 8},
               {c->cstart, sizeof(int32_t) * (size_t)nc}, {c->cend, sizeof(int32_t) * (size_t)nc},
@@ -2974,7 +3026,7 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
     const unsigned grid_c = (unsigned)std::min<int64_t>((c->cap + 255) / 256, 8192);
     prof_mark(c, 2, s);
     hipLaunchKernelGGL(k_win, dim3(grid_c), dim3(256), 0, s, p, c->keys, (const unsigned long long*)c->counters,
-                       c->cap, c->first_flag, c->trx);
+                       c->cap, c->first_flag, c->trx, c->gmask);
     prof_mark(c, 3, s);
     {  // ordered first-win list; tile counts in c->tcos (free until the run sums)
       const unsigned G = (unsigned)std::max<int64_t>(1, std::min<int64_t>(1024, c->cap / 2048));
@@ -2982,7 +3034,7 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
       hipLaunchKernelGGL(k_sel_count, dim3(G), dim3(256), 0, s, c->first_flag, (const unsigned long long*)c->counters,
                          c->cap, tiles);
       hipLaunchKernelGGL(k_sel_scatter, dim3(G), dim3(256), 0, s, c->first_flag,
-                         (const unsigned long long*)c->counters, c->cap, tiles, c->keys, c->trx, c->ritems,
+                         (const unsigned long long*)c->counters, c->cap, tiles, c->keys, c->trx, c->gmask, c->ritems,
                          c->counters + 2);
     }
     RT_HIP(hipGetLastError());
