@@ -2205,6 +2205,15 @@ constexpr int kOwnItems = 4, kOwnTile = 256 * kOwnItems;
 // r4zf_ticket_*.log).  Removed in round 5 (last in commit 43de9a4).
 constexpr uint64_t kOwnAgg = 1ull << 38, kOwnInc = 2ull << 38, kOwnCount = (1ull << 38) - 1;
 constexpr uint64_t kOwnTagMask = ~(kOwnInc | kOwnAgg | kOwnCount);
+// Look-back tiles are numbered by a ticket counter, not by the block index (blocks of different XCDs
+// start in no fixed order; waiting on a tile that is not running deadlocked in the round-4 N = 4
+// rehearsal).  The counter is zero before every launch: the block that draws the last ticket (one
+// per block) sets it back, so no fill precedes the launch and a launch that never ran leaves it 0.
+__device__ __forceinline__ uint32_t take_ticket(unsigned long long* ticket) {
+  const uint32_t t = (uint32_t)atomicAdd(ticket, 1ull);
+  if (t == gridDim.x - 1) atomicExch(ticket, 0ull);  // every other block holds its ticket already
+  return t;
+}
 struct OwnerRuns {
   const uint64_t* keys;  // merged wide keys [n]
   SumVal val;            // the record sums in merged order
@@ -2226,8 +2235,7 @@ __global__ __launch_bounds__(256) void k_owner_runs(OwnerRuns a) {
   __shared__ uint32_t s_tile;
   __shared__ int s_w[4];
   __shared__ int64_t s_prefix;
-  if (threadIdx.x == 0)
-    s_tile = (uint32_t)atomicAdd(a.ticket, 1ull);
+  if (threadIdx.x == 0) s_tile = take_ticket(a.ticket);
   if (blockIdx.x == 0 && threadIdx.x == 0) *a.nbig = 0u;  // k_power_small lists the big cells afresh
   __syncthreads();
   const int64_t tile = s_tile;
@@ -2396,7 +2404,7 @@ __global__ __launch_bounds__(256) void k_send_runs(SendRuns a) {
   __shared__ SegFx s_ws[4];
   __shared__ int64_t s_prefix;
   __shared__ Fx192 s_carry;
-  if (threadIdx.x == 0) s_tile = (uint32_t)atomicAdd(a.ticket, 1ull);
+  if (threadIdx.x == 0) s_tile = take_ticket(a.ticket);
   __syncthreads();
   const int64_t tile = s_tile;
   const int64_t i0 = tile * kSendTile + (int64_t)threadIdx.x * kSendItems;
@@ -2639,12 +2647,112 @@ using OnesweepCfg =
                                         rocprim::block_radix_rank_algorithm::match>;
 using OnesweepOnly = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, OnesweepCfg, 0>;
 constexpr int64_t kOnesweepMinItems = 300000;
+bool onesweep_fused();
+
+// rocPRIM's Onesweep with its host loop rewritten (the kernels are rocPRIM's own, rocprim::detail, so
+// the sort is the same): rocPRIM's driver fills the digit histogram, then before every pass the
+// pass's look-back states and its ordered block id -- 1 + 2 x passes fills of ~5 us each (a K5 rank
+// of 8: 9 of its 17 sort launches).  Here one fill zeroes the histogram and every pass's states and
+// block id together, then the histogram, the scan and one launch per pass.  Keys in kout after an
+// odd pass count, else in the key scratch (returned through *in_out: true = kout holds them).
+template <class Cfg, typename V>
+hipError_t onesweep_pairs(void* temp, size_t& storage, const uint64_t* kin, uint64_t* kout, const V* vin, V* vout,
+                          unsigned n, unsigned end_bit, hipStream_t s) {
+  namespace rd = rocprim::detail;
+  using config = rd::wrapped_radix_sort_onesweep_config<Cfg, uint64_t, V>;
+  using bid_t = rd::block_id_wrapper<unsigned int, true>;
+  using state_t = rd::onesweep_lookback_state;
+  rd::target_arch arch;
+  hipError_t e = rd::host_target_arch(s, arch);
+  if (e != hipSuccess) return e;
+  constexpr rd::radix_sort_onesweep_config_params params = Cfg();
+  const unsigned rb = params.radix_bits_per_place, radix = 1u << rb;
+  const unsigned hist_ipb = params.histogram.block_size * params.histogram.items_per_thread;
+  const unsigned sort_ipb = params.sort.block_size * params.sort.items_per_thread;
+  const unsigned places = (end_bit + rb - 1) / rb;
+  const unsigned sblocks = (n + sort_ipb - 1) / sort_ipb;
+  const size_t al = 256;
+  auto up = [&](size_t b) { return (b + al - 1) / al * al; };
+  const size_t b_off = up(sizeof(unsigned) * radix * places), b_tmp = up(sizeof(unsigned) * radix);
+  const size_t b_states = up(sizeof(state_t) * (size_t)radix * sblocks * places), b_bid = up(sizeof(unsigned) * places);
+  const size_t b_keys = up(sizeof(uint64_t) * n), b_vals = up(sizeof(V) * n);
+  const size_t zero_bytes = b_off + b_tmp + b_states + b_bid;
+  if (!temp) {
+    storage = zero_bytes + b_keys + b_vals;
+    return hipSuccess;
+  }
+  if (storage < zero_bytes + b_keys + b_vals || n == 0 || places == 0) return hipErrorInvalidValue;
+  char* base = static_cast<char*>(temp);
+  unsigned* offsets = reinterpret_cast<unsigned*>(base);
+  unsigned* offsets_tmp = reinterpret_cast<unsigned*>(base + b_off);
+  state_t* states = reinterpret_cast<state_t*>(base + b_off + b_tmp);
+  unsigned* bids = reinterpret_cast<unsigned*>(base + b_off + b_tmp + b_states);
+  uint64_t* ktmp = reinterpret_cast<uint64_t*>(base + zero_bytes);
+  V* vtmp = reinterpret_cast<V*>(base + zero_bytes + b_keys);
+  if ((e = hipMemsetAsync(base, 0, zero_bytes, s)) != hipSuccess) return e;
+  const rocprim::identity_decomposer dec{};
+  {
+    const unsigned hblocks = (n + hist_ipb - 1) / hist_ipb, hfull = n % hist_ipb == 0 ? hblocks : hblocks - 1;
+    auto hist = [=](auto arch_config) {
+      static constexpr rd::radix_sort_onesweep_config_params P = decltype(arch_config)::params;
+      rd::onesweep_histograms<P.histogram.block_size, P.histogram.items_per_thread, P.radix_bits_per_place, false>(
+          kin, offsets, n, hfull, dec, 0u, end_bit);
+    };
+    e = rd::execute_launch_plan<config, decltype(hist), rd::radix_sort_onesweep_histogram_config_selector>(
+        arch, hist, dim3(hblocks), dim3(params.histogram.block_size), 0, s);
+    if (e != hipSuccess) return e;
+    auto scan = [=](auto arch_config) {
+      static constexpr rd::radix_sort_onesweep_config_params P = decltype(arch_config)::params;
+      rd::onesweep_scan_histograms<P.histogram.block_size, P.radix_bits_per_place>(offsets);
+    };
+    e = rd::execute_launch_plan<config, decltype(scan), rd::radix_sort_onesweep_histogram_config_selector>(
+        arch, scan, dim3(places), dim3(params.histogram.block_size), 0, s);
+    if (e != hipSuccess) return e;
+  }
+  const unsigned sfull = n % sort_ipb == 0 ? sblocks : sblocks - 1;
+  // pass p reads the previous pass's output; the last pass writes kout / vout
+  for (unsigned p = 0; p < places; ++p) {
+    const unsigned bit = p * rb, cur_bits = std::min(rb, end_bit - bit);
+    const bool into_out = ((places - 1 - p) % 2) == 0;  // the pass that ends in kout alternates back from the last
+    const uint64_t* ki = p == 0 ? kin : (into_out ? ktmp : kout);
+    const V* vi = p == 0 ? vin : (into_out ? vtmp : vout);
+    uint64_t* ko = into_out ? kout : ktmp;
+    V* vo = into_out ? vout : vtmp;
+    bid_t bid = bid_t::create(bids + p);
+    state_t* st = states + (size_t)radix * sblocks * p;
+    unsigned* off_in = offsets + p * radix;
+    auto iter = [=](auto arch_config) {
+      static constexpr rd::radix_sort_onesweep_config_params P = decltype(arch_config)::params;
+      rd::onesweep_iteration<P.sort.block_size, P.sort.items_per_thread, P.radix_bits_per_place, false,
+                             P.radix_rank_algorithm>(ki, ko, vi, vo, n, off_in, offsets_tmp, st, dec, bit, cur_bits,
+                                                     sfull, bid);
+    };
+    e = rd::execute_launch_plan<config, decltype(iter), rd::radix_sort_onesweep_sort_config_selector>(
+        arch, iter, dim3(sblocks), dim3(params.sort.block_size), 0, s);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
 template <typename V>
 hipError_t sort_records(void* tmp, size_t& bytes, const uint64_t* kin, uint64_t* kout, const V* vin, V* vout,
                         int64_t n, int end_bit, hipStream_t s) {
-  if (n >= kOnesweepMinItems)
+  if (n >= kOnesweepMinItems) {
+    if (onesweep_fused() && n < ((int64_t)1 << 30)) {  // (one batch: rocPRIM splits at 2^30 items)  // rocPRIM's Onesweep kernels, one fill (onesweep_pairs)
+      if (!tmp) {  // the workspace of either driver (the plan sizes it once for both)
+        size_t b1 = 0, b2 = 0;
+        hipError_t e = onesweep_pairs<OnesweepCfg>(nullptr, b1, kin, kout, vin, vout, (unsigned)n, (unsigned)end_bit, s);
+        if (e == hipSuccess)
+          e = rocprim::radix_sort_pairs<OnesweepOnly>(nullptr, b2, kin, kout, vin, vout, (unsigned)n, 0u,
+                                                      (unsigned)end_bit, s);
+        bytes = std::max(b1, b2);
+        return e;
+      }
+      return onesweep_pairs<OnesweepCfg>(tmp, bytes, kin, kout, vin, vout, (unsigned)n, (unsigned)end_bit, s);
+    }
     return rocprim::radix_sort_pairs<OnesweepOnly>(tmp, bytes, kin, kout, vin, vout, (unsigned)n, 0u,
                                                    (unsigned)end_bit, s);
+  }
   return rocprim::radix_sort_pairs(tmp, bytes, kin, kout, vin, vout, (unsigned)n, 0u, (unsigned)end_bit, s);
 }
 
@@ -2759,6 +2867,13 @@ int64_t traj_split_max_rays() {
     return e ? (int64_t)atoll(e) : (int64_t)262144;
   }();
   return v;
+}
+
+// record sorts through onesweep_pairs (default) or rocPRIM's own Onesweep driver (RFRT_ONESWEEP_FUSED=0,
+// for A/B checks); read at every call
+bool onesweep_fused() {
+  const char* e = getenv("RFRT_ONESWEEP_FUSED");
+  return !(e && e[0] == '0');
 }
 
 // replay on BVH scenes: the environment traversal culled at the receiver's t (default), or not
@@ -3410,7 +3525,6 @@ static int trace_records_impl(rt_coverage* c, const float* tx_pos, double tx_pow
     // the send buffers are filled before the host synchronizes (no launch after it)
     {
       if ((rc = grow_for(c, nlist, s))) return rc;
-      RT_HIP(hipMemsetAsync(c->own_aux, 0, 8, s));  // the ticket counter (k_send_runs takes tiles from it)
       size_t tb = c->tmp_bytes;
       const int sb = record_sort_bits(c, kb, n_bins);
       RT_HIP(sort_records(c->tmp, tb, c->okeys, c->okeys_sorted, c->oamps, c->oamps_sorted, nlist, sb < 64 ? sb : 64, s));
@@ -3652,7 +3766,6 @@ static int power_segments_impl(rt_coverage* c, const uint64_t* keys, const uint6
     const dim3 gm((unsigned)std::min<int64_t>((n + 255) / 256, 8192));
     // segments out of key order: counted in the high word of own_aux[1] (rt_coverage_check)
     unsigned* bad = reinterpret_cast<unsigned*>(c->own_aux + 1) + 1;
-    RT_HIP(hipMemsetAsync(c->own_aux, 0, 8, s));  // k_owner_runs' ticket counter
     if (nseg <= 2)
       hipLaunchKernelGGL(k_merge_lockstep<2>, gm, dim3(256), 0, s, keys, stride, so, steps, c->okeys_sorted, idx_sorted, bad);
     else if (nseg <= 4)
