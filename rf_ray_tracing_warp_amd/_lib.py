@@ -78,10 +78,12 @@ def lib():
     L.rt_coverage_received.argtypes = [_vp, _vp, _vp, _i64, ctypes.POINTER(_i64), _vp]
     L.rt_power_dense.argtypes = [_vp, _i64, _i64, ctypes.c_double, _vp, _i64, _vp, _vp]
     L.rt_coverage_profile.argtypes = [_vp, _int]
-    L.rt_coverage_check.argtypes = [_vp, _vp, _vp]
-    L.rt_coverage_trace_rows_async.argtypes = [_vp, _vp, ctypes.c_double, ctypes.c_double, ctypes.c_double, _int,
-                                               _i64, _vp, _i64, _vp, _vp]
-    L.rt_coverage_trace_rows_finish.argtypes = [_vp, _vp, _vp, _vp]
+    # round-5 entry points; an A/B library of an older tree (tools/_var, RFRT_LIB_PATH) lacks them
+    if hasattr(L, "rt_coverage_check"):
+        L.rt_coverage_check.argtypes = [_vp, _vp, _vp]
+        L.rt_coverage_trace_rows_async.argtypes = [_vp, _vp, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                                   _int, _i64, _vp, _i64, _vp, _vp]
+        L.rt_coverage_trace_rows_finish.argtypes = [_vp, _vp, _vp, _vp]
     L.rt_coverage_last_profile.argtypes = [_vp, _vp, _int]
     L.rt_debug_poison.argtypes = [_int]
     L.rt_profile.argtypes = [_int]
@@ -101,7 +103,8 @@ def lib():
                  "rt_coverage_last_profile", "rt_debug_poison",
                  "rt_profile", "rt_trace_last_profile", "rt_trace_profile_stats",
                  "rt_power_dense", "rt_selftest_math", "rt_ray_dirs", "rt_query", "rt_selftest_fx"):
-        getattr(L, name).restype = _int
+        if hasattr(L, name):
+            getattr(L, name).restype = _int
     _lib = L
     return L
 
