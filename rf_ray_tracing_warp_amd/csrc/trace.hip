@@ -333,7 +333,8 @@ __global__ __launch_bounds__(512) void k_trace_cir_tail(rt::TraceCirFused fz, in
 template <int B, bool USE_BVH>
 __device__ __forceinline__ void trace_body(const TraceArgs& a) {
   constexpr int P = B + 1;
-  constexpr bool kNtRows = !USE_BVH;  // see store_row_fixed
+  // row stores: ordinary (L2 merges a row's pieces; see store_row_fixed) -- the bursts that matter
+  // run in direction-sorted order (launch_trace), brute force included
   extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
   float4* cone = lds_tab + (size_t)a.env_nf * 18;  // bounce-0 edge normals after the face table
   const bool use_cone = !USE_BVH && a.env_nf <= kConeMaxFaces;
@@ -345,7 +346,6 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
   // wave can list its part of a chunk's received rows for rt_trace_cir
   for (int64_t chunk = blockIdx.x; chunk * 256 < a.n; chunk += gridDim.x) {
     const int64_t irow = chunk * 256 + threadIdx.x;
-    bool got = false;
     if (irow < a.n) {
     const int64_t row = a.order ? (int64_t)a.order[irow] : irow;
     const int64_t gid = a.ray_offset + row;
@@ -404,7 +404,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
       if (a.hit_kind) a.hit_kind[row * B + b] = kind;
       if (a.hit_face) a.hit_face[row * B + b] = face;
     }
-    if (a.traced) store_row_fixed<P, kNtRows>(a.traced + row * (P * 3), path);
+    if (a.traced) store_row_fixed<P, false>(a.traced + row * (P * 3), path);
     // BVH kernels: launch_trace fills received (NaN) and row_mask (0) in row order first, as the
     // reference does on the host (tracer.py:67-72), and only received rays store their row and
     // mask word here (kernel.py:89-91): a direction-sorted burst scatters its rows, and writing
@@ -418,23 +418,15 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
         rec[i][1] = keep ? path[i][1] : qnan;
         rec[i][2] = keep ? path[i][2] : qnan;
       }
-      store_row_fixed<P, kNtRows>(a.received + row * (P * 3), rec);
+      store_row_fixed<P, false>(a.received + row * (P * 3), rec);
     }
-    if (a.mask && (!USE_BVH || last_rx >= 0)) {
-      if constexpr (kNtRows) __builtin_nontemporal_store(last_rx >= 0 ? 1u : 0u, a.mask + row);
-      else a.mask[row] = last_rx >= 0 ? 1u : 0u;
+    if (a.mask && (!USE_BVH || last_rx >= 0)) a.mask[row] = last_rx >= 0 ? 1u : 0u;
+    if (!USE_BVH && a.fused && last_rx >= 0) {  // list the received row under its own chunk (rare)
+      const int64_t c = row >> 8;
+      atomicAdd(a.fz.counts + c, 1);
+      atomicAdd(a.fz.gcounts + (c >> 6), 1);
+      atomicOr((unsigned long long*)a.fz.masks + c * 4 + ((row & 255) >> 6), 1ull << (row & 63));
     }
-    got = last_rx >= 0;
-    }
-    if (!USE_BVH && a.fused) {  // row order == chunk order here (no direction sort)
-      const uint64_t m = __ballot(got);
-      if (m) {  // wave-uniform: list this wave's received rows (bits of the chunk's row mask)
-        if ((threadIdx.x & 63) == 0) {
-          atomicAdd(a.fz.counts + chunk, (int32_t)__popcll(m));
-          atomicAdd(a.fz.gcounts + (chunk >> 6), (int32_t)__popcll(m));
-          atomicOr((unsigned long long*)a.fz.masks + chunk * 4 + (threadIdx.x >> 6), (unsigned long long)m);
-        }
-      }
     }
   }
 }
@@ -740,14 +732,19 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
     set_error("rt_trace: max_bounces > 8 requires the traced buffer (scratch rows)");
     return -1;
   }
-  // BVH meshes: trace the rows in direction-sorted order (K4: 2.98 -> 2.06 ms), the
-  // order cached per (device, ray_offset, n); brute-force meshes gain nothing from it (every face is
-  // tested anyway) and keep row order.
+  // Rows in direction-sorted order (the banded order, cached per (device, ray_offset, n)).  BVH
+  // meshes: coherent traversal (K4: 2.98 -> 2.06 ms).  Brute force (register-resident
+  // kernels): the lanes of a wave share their bounce-0 cone candidates and their branches, K2
+  // rt_trace 143 -> 136 us (r5l); the rows are then stored like the BVH kernels' (no streaming
+  // stores) and the fused CIR lists each received row under its own chunk.  (A cull of faces whose
+  // corners all lie beyond the best t so far -- T / det is a convex combination of the corners'
+  // sheared z -- was bit-identical and slower even on sorted rows, 138 us: in ascending face order a
+  // wave reaches its last lane's hit face before it can skip anything.)
   if (g_poison >= 0) {
     const int rc = poison_pool((size_t)256 << 20, stream);
     if (rc) return rc;
   }
-  const bool sort = bvh && n >= kSortMinRays && n <= INT32_MAX;
+  const bool sort = (bvh || B <= 8) && n >= kSortMinRays && n <= INT32_MAX;
   if (sort) {
     trace_mark(0, stream);
     a.order = dir_order_cached(ray_offset, n, stream);
