@@ -60,6 +60,10 @@ def _compare(cov, grid, env_np, tx, B, N, win=100e-9):
     (CoverageGrid.square(12, 15, 5), (10, 0, 5), 3, 30_000),                  # K3 shape, coarse
     (CoverageGrid(8.0, -0.5, 4.6, 0.13, 0.11, 0.2, 10, 10, 5), (10, 0, 5), 3, 20_000),  # around/at the TX
     (CoverageGrid.from_ranges(range(-15, 16, 6), range(-15, 16, 6), range(0, 16, 5)), (10, 0, 5), 2, 20_000),
+    # longer paths: the replay continues through its receiver on the first win's line for several
+    # bounces (the receiver-group mask of k_win, the clear-receiver shortcut), then reflects
+    (CoverageGrid(7.0, -1.6, 4.6, 0.5, 0.45, 0.4, 8, 8, 2), (10, 0, 5), 5, 15_000),
+    (CoverageGrid(7.0, -1.6, 4.6, 0.5, 0.45, 0.4, 8, 8, 2), (10, 0, 5), 1, 15_000),
 ])
 def test_coverage_matches_per_cell_loop(room, grid, tx, B, N):
     cov = Coverage(room, 2.998e8, 100e9, 100e-9, B, N, grid)
