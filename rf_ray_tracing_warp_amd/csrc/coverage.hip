@@ -187,35 +187,45 @@ static_assert(ico_groups_ok(), "rt_icosphere1.h is not in trimesh's subdivide or
 // average, ~5 for the slowest lane of a wave, against 20 for the full test), with the group's
 // vertices computed as make_rx_perm computes them -- (float)(unit * r + centre) in double, the
 // products unit * r staged in LDS -- so every hit is bit-identical to rx_query's.
+// The shear cases' axis orders (kx, ky, kz) by rt::Shear::kcase = kz * 2 + swap (make_shear).
+constexpr int kCaseAxes[6][3] = {{1, 2, 0}, {2, 1, 0}, {2, 0, 1}, {0, 2, 1}, {0, 1, 2}, {1, 0, 2}};
 struct RxLds {
-  double ur[RT_ICO1_NV][4];      // rt_ico1_v * r, the double product of make_rx_perm (w unused)
+  double ur[6][RT_ICO1_NV][4];   // rt_ico1_v * r (make_rx_perm's double product), per shear case in
+                                 // that case's (kx, ky, kz) order (w unused): a vertex needs no selects
   uint64_t vid[RT_ICO1_NF / 4];  // the group's vertex ids c0 c1 c2 m01 m12 m20, 6 bits each
   float4 gb[RT_ICO1_NF / 4];     // group ball: centre * r (f32) and radius * r
-  float gmm[RT_ICO1_NF / 4];     // |centre * r|^2
+  float gmw[RT_ICO1_NF / 4];     // |centre * r|^2 - (radius * r)^2
 };
 __device__ __forceinline__ void stage_rx(RxLds& L, double r) {
-  for (int i = threadIdx.x; i < RT_ICO1_NV * 3; i += blockDim.x) L.ur[i / 3][i % 3] = rt_ico1_v[i / 3][i % 3] * r;
+  for (int i = threadIdx.x; i < 6 * RT_ICO1_NV * 3; i += blockDim.x) {
+    const int kc = i / (RT_ICO1_NV * 3), rem = i % (RT_ICO1_NV * 3), v = rem / 3, k = rem % 3;
+    L.ur[kc][v][k] = rt_ico1_v[v][kCaseAxes[kc][k]] * r;
+  }
   const float rf = (float)r;
   for (int g = threadIdx.x; g < RT_ICO1_NF / 4; g += blockDim.x) {
     uint64_t w = 0;
     for (int j = 0; j < 6; ++j) w |= (uint64_t)kIcoGroup.v[g][j] << (6 * j);
     L.vid[g] = w;
     const float mx = rt_ico1_gball[g][0] * rf, my = rt_ico1_gball[g][1] * rf, mz = rt_ico1_gball[g][2] * rf;
-    L.gb[g] = make_float4(mx, my, mz, rt_ico1_gball[g][3] * rf);
-    L.gmm[g] = mx * mx + my * my + mz * mz;
+    const float mw = rt_ico1_gball[g][3] * rf;
+    L.gb[g] = make_float4(mx, my, mz, mw);
+    L.gmw[g] = (mx * mx + my * my + mz * mz) - mw * mw;
   }
   __syncthreads();
 }
 
-__device__ __forceinline__ void rx_group(const RxLds& L, const double c[3], const rt::Shear& s, int gi, rt::Hit& h) {
+// cp: the cell centre in the query's (kx, ky, kz) order.  The vertices come from the LDS table of
+// the query's shear case, already in that order: three adds per vertex instead of three adds and
+// six selects (K3 map 3.80 -> 3.67 ms, K5 3.61 -> 3.50 ms, bit-identical; r5p / r5q)
+__device__ __forceinline__ void rx_group(const RxLds& L, const double cp[3], const rt::Shear& s, int gi, rt::Hit& h) {
   const uint64_t w = L.vid[gi];
   float3 v[6];
+  const double(*ur)[4] = L.ur[s.kcase];
 #pragma unroll
   for (int j = 0; j < 6; ++j) {
     const int vi = (int)((w >> (6 * j)) & 63);
-    const double2 xy = *reinterpret_cast<const double2*>(&L.ur[vi][0]);
-    const float x = (float)(xy.x + c[0]), y = (float)(xy.y + c[1]), z = (float)(L.ur[vi][2] + c[2]);
-    v[j] = make_float3(rt::pick(x, y, z, s.kx), rt::pick(x, y, z, s.ky), rt::pick(x, y, z, s.kz));
+    const double2 xy = *reinterpret_cast<const double2*>(&ur[vi][0]);
+    v[j] = make_float3((float)(xy.x + cp[0]), (float)(xy.y + cp[1]), (float)(ur[vi][2] + cp[2]));
   }
 #pragma unroll
   for (int f = 0; f < 4; ++f) {
@@ -253,8 +263,6 @@ __device__ __forceinline__ rt::Hit rx_query_culled(const RxLds& L, const rt_grid
   // pad: f32 vertices (half an ulp of the coordinates) and the watertight test's rounding
   const double amax = fmax(fmax(fabs(c[0]), fabs(c[1])), fmax(fabs(c[2]), fmax(fmax(fabs(o.x), fabs(o.y)), fabs(o.z))));
   const float pad = (float)(1e-3 * r + 2e-5 * (1.0 + amax) + 4e-6 * fabs(t0) * sqrt(dd));
-  uint32_t near = 0, far = 0;
-  float far_tmin = INFINITY;
   // Per group, with the unit direction e = d / |d| and u perpendicular to it: the squared distance
   // from the ball centre m to the line is |m - u|^2 - (m.e)^2 = |m|^2 + |u|^2 - 2 m.u - (m.e)^2, and
   // the centre's line parameter is t0 + (m.e) / |d|.  ~20 VALU per group against ~45 for the cross
@@ -263,55 +271,58 @@ __device__ __forceinline__ rt::Hit rx_query_culled(const RxLds& L, const rt_grid
   (void)ddf;
   (void)inv_dd;
   const float ex = d.x * inv_len, ey = d.y * inv_len, ez = d.z * inv_len;
-  const float uu = ux * ux + uy * uy + uz * uz;
+  // per query: dist^2 <= R^2 with R = m.w + pad is (|m|^2 - m.w^2) + (|u|^2 - pad^2) - 2 m.u - (m.e)^2
+  // - 2 pad m.w <= 0; the ball's far end is not behind the origin when m.e + m.w >= -t0 |d| - pad
+  const float uq = fmaf(-pad, pad, ux * ux + uy * uy + uz * uz), pad2 = 2.0f * pad;
+  const float tback = fmaf(-t0f, (float)sqrt(dd), -pad);
   // an opaque offset per query: otherwise the 100 loop-invariant LDS words are hoisted out of the
   // callers' loops into registers (k_win 129 VGPRs spilled)
   int z = 0;
   asm volatile("" : "+v"(z));
   const float4* gb = L.gb + z;
-  const float* gmm = L.gmm + z;
+  const float* gmw = L.gmw + z;
+  uint32_t ok_bits = 0, pos_bits = 0;  // groups that pass; groups beyond the closest approach (m.e > 0)
+  float far_tmin = INFINITY;           // the nearest ball entry of the passing far groups
   if (lmask == kAllGroups) {
 #pragma unroll(ROLLED ? 1 : 4)
     for (int gi = 0; gi < RT_ICO1_NF / 4; ++gi) {
       const float4 m = gb[gi];
       const float me = fmaf(m.x, ex, fmaf(m.y, ey, m.z * ez));
       const float mu = fmaf(m.x, ux, fmaf(m.y, uy, m.z * uz));
-      const float R = m.w + pad;
-      const float dist2 = fmaf(-me, me, fmaf(-2.0f, mu, gmm[gi] + uu));
-      const bool ok = dist2 <= R * R && fmaf(me + R, inv_len, t0f) >= 0.0f;
-      if (ok && me <= 0.0f) near |= 1u << gi;
-      if (ok && me > 0.0f) {
-        far |= 1u << gi;
-        far_tmin = fminf(far_tmin, fmaf(me - R, inv_len, t0f));
-      }
+      const float v = fmaf(-me, me, fmaf(-2.0f, mu, fmaf(-m.w, pad2, gmw[gi] + uq)));
+      const bool ok = (v <= 0.0f) & (me + m.w >= tback);
+      ok_bits |= (ok ? 1u : 0u) << gi;
+      pos_bits |= (me > 0.0f ? 1u : 0u) << gi;
+      if (ok & (me > 0.0f)) far_tmin = fminf(far_tmin, fmaf(me - (m.w + pad), inv_len, t0f));
     }
-    if (line_out) *line_out = near | far;
+    if (line_out) *line_out = ok_bits;
   } else {
     for (uint32_t q = lmask; q; q &= q - 1) {
       const int gi = __builtin_ctz(q);
       const float4 m = gb[gi];
       const float me = fmaf(m.x, ex, fmaf(m.y, ey, m.z * ez));
-      const float R = m.w + pad;
-      const bool ok = fmaf(me + R, inv_len, t0f) >= 0.0f;
-      if (ok && me <= 0.0f) near |= 1u << gi;
-      if (ok && me > 0.0f) {
-        far |= 1u << gi;
-        far_tmin = fminf(far_tmin, fmaf(me - R, inv_len, t0f));
-      }
+      const bool ok = me + m.w >= tback;
+      ok_bits |= (ok ? 1u : 0u) << gi;
+      pos_bits |= (me > 0.0f ? 1u : 0u) << gi;
+      if (ok & (me > 0.0f)) far_tmin = fminf(far_tmin, fmaf(me - (m.w + pad), inv_len, t0f));
     }
   }
+  uint32_t near = ok_bits & ~pos_bits, far = ok_bits & pos_bits;
+  // the centre in the query's axis order (rx_group's vertices come permuted from LDS)
+  auto pickd = [&](int k) { return k == 0 ? c[0] : (k == 1 ? c[1] : c[2]); };
+  const double cp[3] = {pickd(s.kx), pickd(s.ky), pickd(s.kz)};
   rt::Hit h;
   rt::hit_init(h);
   while (near) {
     const int gi = __builtin_ctz(near);
     near &= near - 1;
-    rx_group(L, c, s, gi, h);
+    rx_group(L, cp, s, gi, h);
   }
   if (far_tmin > h.t) far = 0;  // every far face's t is beyond the near hit (ties kept)
   while (far) {
     const int gi = __builtin_ctz(far);
     far &= far - 1;
-    rx_group(L, c, s, gi, h);
+    rx_group(L, cp, s, gi, h);
   }
   return h;
 }
@@ -1106,7 +1117,10 @@ __global__ __launch_bounds__(256) void k_clear_cells(CovParams p, double r_clear
 // measured 37% slower on K3, 10.1 vs 7.4 ms per map: the replay's divergent tail and registers
 // held every candidate's wave.)
 // 6 waves per SIMD: 80 VGPRs, spill-free with the dot-form ball test: K3 k_win 0.935 -> 0.895 ms, K5
-// 0.79 -> 0.76 (r3ze); before it, 5 waves (96 VGPRs, 60 B scratch) beat 4 and 6: 1.03 -> 0.98 ms (r2zj)
+// 0.79 -> 0.76 (r3ze); before it, 5 waves (96 VGPRs, 60 B scratch) beat 4 and 6: 1.03 -> 0.98 ms (r2zj).
+// With the per-case receiver vertices (RxLds::ur) it spills 9 VGPRs (40 B) at 6 waves and still
+// beats the spill-free form: K3 k_win 0.90-0.91 -> 0.85 ms; at 5 waves (94 VGPRs, no spills) 0.86 ms
+// (profiles/r5q_cov_rx_perm_ab.jsonl)
 // candidates of this attempt, 0 if they overflowed the buffers (k_win, the first-win list and the
 // early replay then do nothing: a lane's keys that would cross the capacity are not written, and
 // reading the hole took the replay to illegal addresses in the N = 4 one-GPU rehearsal)
