@@ -723,8 +723,8 @@ __device__ __forceinline__ unsigned column_cells(const CovParams& p, uint64_t it
   for (int64_t ib = ibs; ib <= ib1; ib += step) {
     const int64_t ix = s.A == 0 ? ia : ib, iy = s.A == 0 ? ib : ia;
     const int64_t cell = (kz * g.ny + iy) * g.nx + ix;
-    double cc[3];
-    cell_center(g, cell, cc);
+    // cell_center's values from the indices at hand (its divisions recover exactly these)
+    const double cc[3] = {g.x0 + (double)ix * g.dx, g.y0 + (double)iy * g.dy, g.z0 + (double)kz * g.dz};
     if (seg_ball(s.o, s.d, s.tmax, cc, rp2)) {
       sink(c, ((uint64_t)cell << 28) | ((uint64_t)r << 4) | (uint64_t)k);
       ++c;
