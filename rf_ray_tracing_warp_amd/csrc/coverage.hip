@@ -1236,41 +1236,26 @@ __global__ __launch_bounds__(256) void k_sel_scatter(const uint8_t* flag, const 
 }
 
 // Replay order key of list entry li.  A wave runs as long as its lane with the most bounces left
-// after the first win, so the remaining bounce count (2 bits) leads; then the ray's direction at
-// its first win (8x8 octahedral cell) and the cell's coarse position (16x16 Morton), so the lanes
-// of a wave walk nearby BVH paths.  Only the processing order changes: records are written at li.
-// (Direction over a 32x32 Morton cell, the ray slot instead of direction and cell on brute-force
-// scenes, and the longest replays first were measured no better and removed in round 5.)
+// after the first win, so the remaining bounce count (2 bits) leads; then the receiver groups the
+// first win's line passes (k_win's mask, 20 bits folded to 14): the replay's receiver queries on
+// that line test those groups, so lanes with the same mask run the same group loops and read the
+// same LDS entries.  Only the processing order changes: records are written at li.  Against the
+// round-4 key (initial direction on an 8x8 octahedral grid, then a 16x16 Morton cell of the
+// receiver): K3 replay 1.355 -> 1.21 ms, K5 1.03 -> 0.87 ms on one GPU (device-wide sort); a rank's
+// 4096-entry windows gain nothing either way (r5s, r5t, r5u; lowest / highest group as the key:
+// no better).  (The ray slot instead of direction and cell on brute-force scenes, 32x32 direction
+// cells and longest replays first were measured no better in round 4 and removed in round 5.)
 template <bool USE_BVH>
-__device__ __forceinline__ uint16_t replay_key(const CovParams& p, uint64_t key) {
-  {
-    const int64_t cell = (int64_t)(key >> 28), r = (int64_t)((key >> 4) & 0xFFFFFF);
-    const int k0 = (int)(key & 15);
-    const float4 d = traj_d(p, r, k0);
-    const float sabs = fabsf(d.x) + fabsf(d.y) + fabsf(d.z);
-    float x = d.x / sabs, y = d.y / sabs;
-    if (d.z < 0.0f) {
-      const float ox = x;
-      x = (1.0f - fabsf(y)) * (ox < 0.0f ? -1.0f : 1.0f);
-      y = (1.0f - fabsf(ox)) * (y < 0.0f ? -1.0f : 1.0f);
-    }
-    const uint32_t dx = (uint32_t)fminf(fmaxf((x + 1.0f) * 4.0f, 0.0f), 7.0f);
-    const uint32_t dy = (uint32_t)fminf(fmaxf((y + 1.0f) * 4.0f, 0.0f), 7.0f);
-    uint32_t ix, iy, iz;
-    cell_ijk(p.g, cell, ix, iy, iz);
-    const uint32_t cx = (uint32_t)((uint64_t)ix * 32 / (uint64_t)p.g.nx), cy = (uint32_t)((uint64_t)iy * 32 / (uint64_t)p.g.ny);
-    uint32_t mz = 0;
-#pragma unroll
-    for (int b = 0; b < 5; ++b) mz |= ((cx >> b) & 1u) << (2 * b) | ((cy >> b) & 1u) << (2 * b + 1);
-    const uint32_t rem = (uint32_t)min(max(p.B - 1 - k0, 0), 3);  // bounces left, in 2 bits
-    return (uint16_t)(rem << 14 | (dy * 8 + dx) << 8 | mz >> 2);
-  }
+__device__ __forceinline__ uint16_t replay_key(const CovParams& p, uint64_t key, uint32_t line) {
+  const int k0 = (int)(key & 15);
+  const uint32_t rem = (uint32_t)min(max(p.B - 1 - k0, 0), 3);  // bounces left, in 2 bits
+  return (uint16_t)(rem << 14 | ((line & 0x3FFFu) ^ (line >> 14)));
 }
 template <bool USE_BVH>
 __global__ __launch_bounds__(256) void k_replay_keys(CovParams p, const ReplayItem* items, int64_t nl,
                                                      uint16_t* okey, int32_t* oval) {
   for (int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; li < nl; li += (int64_t)gridDim.x * blockDim.x) {
-    okey[li] = replay_key<USE_BVH>(p, items[li].key);
+    okey[li] = replay_key<USE_BVH>(p, items[li].key, items[li].line);
     oval[li] = (int32_t)li;
   }
 }
@@ -1302,7 +1287,7 @@ __global__ __launch_bounds__(1024) void k_replay_order(CovParams p, const Replay
 #pragma unroll
   for (int i = 0; i < kReplayWinItems; ++i) {
     const int64_t li = base + i;
-    k[i] = li < nl ? replay_key<USE_BVH>(p, items[li].key) : (uint16_t)0xFFFF;
+    k[i] = li < nl ? replay_key<USE_BVH>(p, items[li].key, items[li].line) : (uint16_t)0xFFFF;
     v[i] = (int32_t)li;
   }
   Sort().sort(k, v, st);
