@@ -1186,6 +1186,21 @@ struct ReplayItem {
   float trx;
   uint32_t line;  // the receiver groups the first win's line passes (rx_query_culled's lmask)
 };
+// Replay order key of list entry li.  A wave runs as long as its lane with the most bounces left
+// after the first win, so the remaining bounce count (2 bits) leads; then the receiver groups the
+// first win's line passes (k_win's mask, 20 bits folded to 14): the replay's receiver queries on
+// that line test those groups, so lanes with the same mask run the same group loops and read the
+// same LDS entries.  Only the processing order changes: records are written at li.  Against the
+// round-4 key (initial direction on an 8x8 octahedral grid, then a 16x16 Morton cell of the
+// receiver): K3 replay 1.355 -> 1.21 ms, K5 1.03 -> 0.87 ms on one GPU (device-wide sort); a rank's
+// 4096-entry windows gain nothing either way (r5s, r5t, r5u; lowest / highest group as the key:
+// no better).  (The ray slot instead of direction and cell on brute-force scenes, 32x32 direction
+// cells and longest replays first were measured no better in round 4 and removed in round 5.)
+__device__ __forceinline__ uint16_t replay_key(int B, uint64_t key, uint32_t line) {
+  const int k0 = (int)(key & 15);
+  const uint32_t rem = (uint32_t)min(max(B - 1 - k0, 0), 3);  // bounces left, in 2 bits
+  return (uint16_t)(rem << 14 | ((line & 0x3FFFu) ^ (line >> 14)));
+}
 __device__ __forceinline__ int64_t sel_tile(int64_t n, int G) { return ((n + G - 1) / G + 255) / 256 * 256; }
 __device__ __forceinline__ int block_sum(int v, int* s4) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -1207,7 +1222,8 @@ __global__ __launch_bounds__(256) void k_sel_count(const uint8_t* flag, const un
 __global__ __launch_bounds__(256) void k_sel_scatter(const uint8_t* flag, const unsigned long long* n_dev, int64_t cap,
                                                      const int32_t* counts, const uint64_t* keys, const float* trx,
                                                      const uint32_t* gmask, ReplayItem* items,
-                                                     unsigned long long* nlist) {
+                                                     unsigned long long* nlist, int B, uint16_t* okey,
+                                                     int32_t* oval) {
   __shared__ int s4[4];
   __shared__ int w4[4];
   const int64_t n = cand_count(n_dev, cap), tile = sel_tile(n, gridDim.x);
@@ -1228,34 +1244,22 @@ __global__ __launch_bounds__(256) void k_sel_scatter(const uint8_t* flag, const 
     const int step = w4[0] + w4[1] + w4[2] + w4[3];
     if (f) {
       const int64_t k = base + off + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-      items[k] = ReplayItem{keys[i], trx[i], gmask[i]};
+      const ReplayItem it{keys[i], trx[i], gmask[i]};
+      items[k] = it;
+      if (okey) {  // the device-wide replay order's (key, entry) pairs, as k_replay_keys writes them
+        okey[k] = replay_key(B, it.key, it.line);
+        oval[k] = (int32_t)k;
+      }
     }
     base += step;
     __syncthreads();  // w4 is rewritten by the next step
   }
 }
 
-// Replay order key of list entry li.  A wave runs as long as its lane with the most bounces left
-// after the first win, so the remaining bounce count (2 bits) leads; then the receiver groups the
-// first win's line passes (k_win's mask, 20 bits folded to 14): the replay's receiver queries on
-// that line test those groups, so lanes with the same mask run the same group loops and read the
-// same LDS entries.  Only the processing order changes: records are written at li.  Against the
-// round-4 key (initial direction on an 8x8 octahedral grid, then a 16x16 Morton cell of the
-// receiver): K3 replay 1.355 -> 1.21 ms, K5 1.03 -> 0.87 ms on one GPU (device-wide sort); a rank's
-// 4096-entry windows gain nothing either way (r5s, r5t, r5u; lowest / highest group as the key:
-// no better).  (The ray slot instead of direction and cell on brute-force scenes, 32x32 direction
-// cells and longest replays first were measured no better in round 4 and removed in round 5.)
-template <bool USE_BVH>
-__device__ __forceinline__ uint16_t replay_key(const CovParams& p, uint64_t key, uint32_t line) {
-  const int k0 = (int)(key & 15);
-  const uint32_t rem = (uint32_t)min(max(p.B - 1 - k0, 0), 3);  // bounces left, in 2 bits
-  return (uint16_t)(rem << 14 | ((line & 0x3FFFu) ^ (line >> 14)));
-}
-template <bool USE_BVH>
 __global__ __launch_bounds__(256) void k_replay_keys(CovParams p, const ReplayItem* items, int64_t nl,
                                                      uint16_t* okey, int32_t* oval) {
   for (int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; li < nl; li += (int64_t)gridDim.x * blockDim.x) {
-    okey[li] = replay_key<USE_BVH>(p, items[li].key, items[li].line);
+    okey[li] = replay_key(p.B, items[li].key, items[li].line);
     oval[li] = (int32_t)li;
   }
 }
@@ -1287,7 +1291,7 @@ __global__ __launch_bounds__(1024) void k_replay_order(CovParams p, const Replay
 #pragma unroll
   for (int i = 0; i < kReplayWinItems; ++i) {
     const int64_t li = base + i;
-    k[i] = li < nl ? replay_key<USE_BVH>(p, items[li].key, items[li].line) : (uint16_t)0xFFFF;
+    k[i] = li < nl ? replay_key(p.B, items[li].key, items[li].line) : (uint16_t)0xFFFF;
     v[i] = (int32_t)li;
   }
   Sort().sort(k, v, st);
@@ -2654,17 +2658,17 @@ bool onesweep_fused();
 // of 8: 9 of its 17 sort launches).  Here one fill zeroes the histogram and every pass's states and
 // block id together, then the histogram, the scan and one launch per pass.  Keys in kout after an
 // odd pass count, else in the key scratch (returned through *in_out: true = kout holds them).
-template <class Cfg, typename V>
-hipError_t onesweep_pairs(void* temp, size_t& storage, const uint64_t* kin, uint64_t* kout, const V* vin, V* vout,
-                          unsigned n, unsigned end_bit, hipStream_t s) {
+template <class Cfg, typename K, typename V>
+hipError_t onesweep_pairs(void* temp, size_t& storage, const K* kin, K* kout, const V* vin, V* vout, unsigned n,
+                          unsigned end_bit, hipStream_t s) {
   namespace rd = rocprim::detail;
-  using config = rd::wrapped_radix_sort_onesweep_config<Cfg, uint64_t, V>;
+  using config = rd::wrapped_radix_sort_onesweep_config<Cfg, K, V>;
   using bid_t = rd::block_id_wrapper<unsigned int, true>;
   using state_t = rd::onesweep_lookback_state;
   rd::target_arch arch;
   hipError_t e = rd::host_target_arch(s, arch);
   if (e != hipSuccess) return e;
-  constexpr rd::radix_sort_onesweep_config_params params = Cfg();
+  const rd::radix_sort_onesweep_config_params params = rd::dispatch_target_arch<config, false>(arch);
   const unsigned rb = params.radix_bits_per_place, radix = 1u << rb;
   const unsigned hist_ipb = params.histogram.block_size * params.histogram.items_per_thread;
   const unsigned sort_ipb = params.sort.block_size * params.sort.items_per_thread;
@@ -2674,7 +2678,7 @@ hipError_t onesweep_pairs(void* temp, size_t& storage, const uint64_t* kin, uint
   auto up = [&](size_t b) { return (b + al - 1) / al * al; };
   const size_t b_off = up(sizeof(unsigned) * radix * places), b_tmp = up(sizeof(unsigned) * radix);
   const size_t b_states = up(sizeof(state_t) * (size_t)radix * sblocks * places), b_bid = up(sizeof(unsigned) * places);
-  const size_t b_keys = up(sizeof(uint64_t) * n), b_vals = up(sizeof(V) * n);
+  const size_t b_keys = up(sizeof(K) * n), b_vals = up(sizeof(V) * n);
   const size_t zero_bytes = b_off + b_tmp + b_states + b_bid;
   if (!temp) {
     storage = zero_bytes + b_keys + b_vals;
@@ -2686,7 +2690,7 @@ hipError_t onesweep_pairs(void* temp, size_t& storage, const uint64_t* kin, uint
   unsigned* offsets_tmp = reinterpret_cast<unsigned*>(base + b_off);
   state_t* states = reinterpret_cast<state_t*>(base + b_off + b_tmp);
   unsigned* bids = reinterpret_cast<unsigned*>(base + b_off + b_tmp + b_states);
-  uint64_t* ktmp = reinterpret_cast<uint64_t*>(base + zero_bytes);
+  K* ktmp = reinterpret_cast<K*>(base + zero_bytes);
   V* vtmp = reinterpret_cast<V*>(base + zero_bytes + b_keys);
   if ((e = hipMemsetAsync(base, 0, zero_bytes, s)) != hipSuccess) return e;
   const rocprim::identity_decomposer dec{};
@@ -2713,9 +2717,9 @@ hipError_t onesweep_pairs(void* temp, size_t& storage, const uint64_t* kin, uint
   for (unsigned p = 0; p < places; ++p) {
     const unsigned bit = p * rb, cur_bits = std::min(rb, end_bit - bit);
     const bool into_out = ((places - 1 - p) % 2) == 0;  // the pass that ends in kout alternates back from the last
-    const uint64_t* ki = p == 0 ? kin : (into_out ? ktmp : kout);
+    const K* ki = p == 0 ? kin : (into_out ? ktmp : kout);
     const V* vi = p == 0 ? vin : (into_out ? vtmp : vout);
-    uint64_t* ko = into_out ? kout : ktmp;
+    K* ko = into_out ? kout : ktmp;
     V* vo = into_out ? vout : vtmp;
     bid_t bid = bid_t::create(bids + p);
     state_t* st = states + (size_t)radix * sblocks * p;
@@ -2737,17 +2741,20 @@ template <typename V>
 hipError_t sort_records(void* tmp, size_t& bytes, const uint64_t* kin, uint64_t* kout, const V* vin, V* vout,
                         int64_t n, int end_bit, hipStream_t s) {
   if (n >= kOnesweepMinItems) {
-    if (onesweep_fused() && n < ((int64_t)1 << 30)) {  // (one batch: rocPRIM splits at 2^30 items)  // rocPRIM's Onesweep kernels, one fill (onesweep_pairs)
+    // rocPRIM's Onesweep kernels with one fill (onesweep_pairs); one batch: rocPRIM splits at 2^30
+    if (onesweep_fused() && n < ((int64_t)1 << 30)) {
       if (!tmp) {  // the workspace of either driver (the plan sizes it once for both)
         size_t b1 = 0, b2 = 0;
-        hipError_t e = onesweep_pairs<OnesweepCfg>(nullptr, b1, kin, kout, vin, vout, (unsigned)n, (unsigned)end_bit, s);
+        hipError_t e =
+            onesweep_pairs<OnesweepCfg, uint64_t, V>(nullptr, b1, kin, kout, vin, vout, (unsigned)n, (unsigned)end_bit, s);
         if (e == hipSuccess)
           e = rocprim::radix_sort_pairs<OnesweepOnly>(nullptr, b2, kin, kout, vin, vout, (unsigned)n, 0u,
                                                       (unsigned)end_bit, s);
         bytes = std::max(b1, b2);
         return e;
       }
-      return onesweep_pairs<OnesweepCfg>(tmp, bytes, kin, kout, vin, vout, (unsigned)n, (unsigned)end_bit, s);
+      return onesweep_pairs<OnesweepCfg, uint64_t, V>(tmp, bytes, kin, kout, vin, vout, (unsigned)n, (unsigned)end_bit,
+                                                      s);
     }
     return rocprim::radix_sort_pairs<OnesweepOnly>(tmp, bytes, kin, kout, vin, vout, (unsigned)n, 0u,
                                                    (unsigned)end_bit, s);
@@ -2793,8 +2800,9 @@ int alloc_cands(rt_coverage* c, int64_t cap, hipStream_t s) {
   RT_HIP(hipMalloc(&c->tmp, c->tmp_bytes));
   // replay-order sort workspace for up to cap records (one allocation per growth, not per run)
   size_t b5 = 0;
-  RT_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, b5, (uint16_t*)nullptr, (uint16_t*)nullptr, (int32_t*)nullptr,
-                                            (int32_t*)nullptr, (int)cap, 0, 16));
+  RT_HIP((onesweep_pairs<rocprim::default_config, uint16_t, int32_t>(nullptr, b5, (uint16_t*)nullptr, (uint16_t*)nullptr,
+                                                                     (int32_t*)nullptr, (int32_t*)nullptr, (unsigned)cap, 16u,
+                                                                     nullptr)));
   c->rord_bytes = 2 * rord_key_bytes(cap) + 2 * rord_row_bytes(cap) + b5;
   RT_HIP(hipMalloc(&c->rord, c->rord_bytes));
   c->cap = cap;
@@ -3084,15 +3092,30 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
   // of 8, profiles/r3j_k3.timeline.txt) overlap the replay instead of idling the GPU.  Only for
   // lists the window order takes (a rank's share); the whole-map lists keep the device-wide sort,
   // which needs the length on the host.  The previous run's length sizes the grid.
+  // The replay-order workspace, laid out for the plan's capacity (k_sel_scatter fills its first half
+  // before the list length is known): keys in / out, entries in / out, then the sort's scratch.
+  // Taken afresh at every use: an overflowing attempt regrows the buffers (alloc_cands).
+  struct Rord {
+    uint16_t *k_in, *k_out;
+    int32_t *v_in, *v_out;
+    void* tmp;
+    size_t tmp_bytes;
+  };
+  auto rord = [c]() {
+    const size_t rkb = rord_key_bytes(c->cap), rrb = rord_row_bytes(c->cap);
+    char* w = (char*)c->rord;
+    return Rord{(uint16_t*)w, (uint16_t*)(w + rkb), (int32_t*)(w + 2 * rkb), (int32_t*)(w + 2 * rkb + rrb),
+                w + 2 * rkb + 2 * rrb, c->rord_bytes - 2 * rkb - 2 * rrb};
+  };
+  // whole-map lists (plans not replayed early) get their order keys from k_sel_scatter
+  const bool pre_keys = !(c->ray_mode && c->nshard > 1);
   auto launch_replay = [&](int64_t nl, const unsigned long long* nl_dev, bool windows, int64_t grid_hint) {
     const unsigned grid_l = (unsigned)std::max<int64_t>(1, std::min<int64_t>((grid_hint + 255) / 256, 8192));
-    const size_t kbs = rord_key_bytes(nl), rbs = rord_row_bytes(nl);
-    size_t cub_bytes = c->rord_bytes - 2 * kbs - 2 * rbs;  // the workspace was sized for cap >= nl
-    void* ws = c->rord;
-    uint16_t* k_in = (uint16_t*)ws;
-    uint16_t* k_out = (uint16_t*)((char*)ws + kbs);
-    int32_t* v_in = (int32_t*)((char*)ws + 2 * kbs);
-    int32_t* v_out = (int32_t*)((char*)ws + 2 * kbs + rbs);
+    const Rord ro = rord();
+    uint16_t* k_in = ro.k_in;
+    uint16_t* k_out = ro.k_out;
+    int32_t* v_in = ro.v_in;
+    int32_t* v_out = ro.v_out;
     if (windows) {
       const unsigned grid_w = (unsigned)((nl + kReplayWin - 1) / kReplayWin);
       if (bvh)
@@ -3100,12 +3123,11 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
       else
         hipLaunchKernelGGL(k_replay_order<false>, dim3(grid_w), dim3(1024), 0, s, p, c->ritems, nl, nl_dev, v_out);
     } else {
-      if (bvh)
-        hipLaunchKernelGGL(k_replay_keys<true>, dim3(grid_l), dim3(256), 0, s, p, c->ritems, nl, k_in, v_in);
-      else
-        hipLaunchKernelGGL(k_replay_keys<false>, dim3(grid_l), dim3(256), 0, s, p, c->ritems, nl, k_in, v_in);
-      RT_HIP(hipcub::DeviceRadixSort::SortPairs((char*)ws + 2 * kbs + 2 * rbs, cub_bytes, k_in, k_out, v_in, v_out,
-                                                (int)nl, 0, 16, s));
+      if (!pre_keys)  // (k_sel_scatter wrote them for plans whose lists are not replayed early)
+        hipLaunchKernelGGL(k_replay_keys, dim3(grid_l), dim3(256), 0, s, p, c->ritems, nl, k_in, v_in);
+      size_t sb = ro.tmp_bytes;
+      RT_HIP((onesweep_pairs<rocprim::default_config, uint16_t, int32_t>(ro.tmp, sb, k_in, k_out, v_in, v_out,
+                                                                         (unsigned)nl, 16u, s)));
     }
     prof_mark(c, 4, s);
     // the processing order (window order or the device-wide sort) of the items
@@ -3149,7 +3171,7 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
                          c->cap, tiles);
       hipLaunchKernelGGL(k_sel_scatter, dim3(G), dim3(256), 0, s, c->first_flag,
                          (const unsigned long long*)c->counters, c->cap, tiles, c->keys, c->trx, c->gmask, c->ritems,
-                         c->counters + 2);
+                         c->counters + 2, p.B, pre_keys ? rord().k_in : nullptr, pre_keys ? rord().v_in : nullptr);
     }
     RT_HIP(hipGetLastError());
     // the counters go to pinned memory ahead of the replay, and the host waits for that copy only;
