@@ -1334,9 +1334,9 @@ struct WideKey {
     const uint64_t bin = (k >> ray_bits) & ((1ull << bin_bits) - 1);
     uint64_t cell = (k >> (ray_bits + bin_bits)) & ((1ull << cell_bits) - 1);
     const uint64_t own = k >> (ray_bits + bin_bits + cell_bits);
-    if (world > 1) {
-      const uint64_t nxo = (uint64_t)((nx + world - 1) / world);
-      cell = (cell / nxo) * (uint64_t)nx + (cell % nxo) * (uint64_t)world + own;
+    if (world > 1) {  // 32-bit division (cells < 2^32): a 64-bit one is ~100 instructions
+      const uint32_t nxo = (uint32_t)((nx + world - 1) / world), c32 = (uint32_t)cell, q = c32 / nxo;
+      cell = (uint64_t)q * (uint64_t)nx + (uint64_t)(c32 - q * nxo) * (uint64_t)world + own;
     }
     return own << own_shift | cell << 32 | bin;
   }
@@ -1655,8 +1655,13 @@ __global__ __launch_bounds__(64) void k_power_small(TermArrays G, const int32_t*
     bool is_big = false;
     int64_t c = 0;
     if (t < nown) {
-      const int64_t jx = t % nxo, rest = t / nxo;
-      c = rest * g.nx + shard + jx * nshard;
+      // the owned cell of index t (32-bit: cells < 2^32; a 64-bit division is ~100 instructions)
+      if (nshard == 1) {
+        c = t;
+      } else {
+        const uint32_t tt = (uint32_t)t, nx32 = (uint32_t)nxo, rest = tt / nx32, jx = tt - rest * nx32;
+        c = (int64_t)rest * g.nx + shard + (int64_t)jx * nshard;
+      }
       const bool has = cepoch[c] == epoch;
       const int64_t lo = has ? cstart[c] : 0, hi = has ? cend[c] : 0;
       if (hi - lo <= kPowSmall) {
