@@ -47,6 +47,7 @@ struct TraceArgs {
   const int32_t* order;  // processing order of the rows (null = identity), see launch_trace
   bool fused;             // brute-force kernels under rt_trace_cir: list received rows, per-path CIR
   rt::TraceCirFused fz;
+  bool sparse_rx;  // received rows / mask words filled beforehand (k_fill_received): store only received rays'
 };
 
 // Closest hit over a brute-force face list whose permuted table lives at `tab`
@@ -405,11 +406,11 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
       if (a.hit_face) a.hit_face[row * B + b] = face;
     }
     if (a.traced) store_row_fixed<P, false>(a.traced + row * (P * 3), path);
-    // BVH kernels: launch_trace fills received (NaN) and row_mask (0) in row order first, as the
+    // Direction-sorted launches: launch_trace fills received (NaN) and row_mask (0) in row order first, as the
     // reference does on the host (tracer.py:67-72), and only received rays store their row and
     // mask word here (kernel.py:89-91): a direction-sorted burst scatters its rows, and writing
     // every ray's NaN row and mask word cost ~0.2 GB of partial-line writes per K4 launch
-    if (a.received && (!USE_BVH || last_rx >= 0)) {
+    if (a.received && (!a.sparse_rx || last_rx >= 0)) {
       float rec[P][3];
 #pragma unroll
       for (int i = 0; i < P; ++i) {
@@ -420,7 +421,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
       }
       store_row_fixed<P, false>(a.received + row * (P * 3), rec);
     }
-    if (a.mask && (!USE_BVH || last_rx >= 0)) a.mask[row] = last_rx >= 0 ? 1u : 0u;
+    if (a.mask && (!a.sparse_rx || last_rx >= 0)) a.mask[row] = last_rx >= 0 ? 1u : 0u;
     if (!USE_BVH && a.fused && last_rx >= 0) {  // list the received row under its own chunk (rare)
       const int64_t c = row >> 8;
       atomicAdd(a.fz.counts + c, 1);
@@ -758,7 +759,10 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
   trace_events(&ev0, &ev1);
   // BVH kernels store only the received rows (trace_body): the fill comes first, inside the
   // profiled span (its start event, the trace kernel's stop event)
-  const bool fill = bvh && B <= 8 && (received || mask);
+  // direction-sorted launches (BVH, and brute force since round 5: K2 rt_trace 130.7 -> 127.8 us,
+  // r5aa) fill received / row_mask in row order first and store only the received rays' rows
+  const bool fill = (bvh || a.order) && B <= 8 && (received || mask);
+  a.sparse_rx = fill;
   if (fill) {
     const unsigned gf = (unsigned)std::min<int64_t>((n * (B + 1) * 3 / 4 + 255) / 256, 4096);
     if (ev0) hipExtLaunchKernelGGL(k_fill_received, dim3(gf), dim3(256), 0, stream, ev0, nullptr, 0, received,
