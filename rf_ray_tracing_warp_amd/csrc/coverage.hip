@@ -3032,6 +3032,7 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
     if (bvh) hipLaunchKernelGGL(k_clear_cells<true>, gcl, dim3(256), 0, s, p, r_clear, c->clear);
     else hipLaunchKernelGGL(k_clear_cells<false>, gcl, dim3(256), 0, s, p, r_clear, c->clear);
     RT_HIP(hipGetLastError());
+    RT_HIP(hipStreamSynchronize(s));  // once: later runs may come on other streams
   }
   p.clear = c->clear_on ? c->clear : nullptr;
   const size_t lds = bvh ? 0 : (size_t)p.env_nf * 18 * sizeof(float4);
