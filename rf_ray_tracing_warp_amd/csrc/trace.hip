@@ -48,6 +48,8 @@ struct TraceArgs {
   bool fused;             // brute-force kernels under rt_trace_cir: list received rows, per-path CIR
   rt::TraceCirFused fz;
   bool sparse_rx;  // received rows / mask words filled beforehand (k_fill_received): store only received rays'
+  bool box_cull;   // bounces >= 1 of sorted brute-force bursts: the wave's candidate faces (wave_boxes)
+  float env_pad;   // face boxes padded by 1e-5 * (1 + scene's largest |coordinate|), as the BVH's boxes
 };
 
 // Closest hit over a brute-force face list whose permuted table lives at `tab`
@@ -223,6 +225,115 @@ __device__ __forceinline__ uint64_t wave_cones(const float4* cone, int nf, float
   return __ballot(in);
 }
 
+// closest hit over the candidate faces `cand` (bit f = face f), ascending (LazyHit's order rule)
+__device__ __forceinline__ rt::Hit query_list(const float4* tab, const rt::Shear& s, uint64_t cand) {
+  rt::LazyHit h;
+  rt::lazy_init(h);
+  const int off = s.kcase * 3;
+  while (cand) {
+    const int f = __builtin_ctzll(cand);
+    cand &= cand - 1;
+    const float4 q0 = tab[f * 18 + off + 0];
+    const float4 q1 = tab[f * 18 + off + 1];
+    const float c2 = tab[f * 18 + off + 2].x;
+    float T, det;
+    if (rt::tri_test(s, q0, q1, c2, T, det)) rt::lazy_consider(h, T, det, f);
+  }
+  return rt::lazy_finish(h);
+}
+
+// ------------------------------------------------------------------ bounce >= 1 candidate faces
+// After a reflection the rays of a direction-sorted wave still start close together (on the patch
+// their bounce-0 rays hit) and point in similar directions.  wave_boxes bounds the wave's live rays by
+// an origin box [ol, oh] and per-axis direction intervals [dl, dh], and lane j tests face j's box
+// against that bundle: per axis with dl > 0, every ray of the bundle is inside the face's slab only
+// for t in [(fl - oh) / dh, (fh - ol) / dl] (mirrored for dh < 0; no bound when the interval holds
+// 0).  A ray's own per-axis intervals lie inside the bundle's, so a face some lane could hit passes;
+// the lanes then run the exact test over the wave's candidates only, in ascending face order, and
+// every output bit is unchanged.  The face boxes are padded by 1e-5 * (1 + scene scale) and rounded
+// outward, the same invariant the BVH's boxes rest on (rt_bvh.h: an accepted hit lies inside its
+// face's padded box), and the compare keeps the BVH slab's slack.
+__device__ __forceinline__ void stage_boxes(const TraceArgs& a, float4* box) {
+  for (int f = threadIdx.x; f < a.env_nf; f += blockDim.x) {
+    const float4 q0 = a.env_perm[f * 18 + 12], q1 = a.env_perm[f * 18 + 13];  // case 4: x, y, z
+    const float c2 = a.env_perm[f * 18 + 14].x;
+    const float p = a.env_pad;
+    box[2 * f] = make_float4(nextafterf(fminf(fminf(q0.x, q0.w), q1.z) - p, -INFINITY),
+                             nextafterf(fminf(fminf(q0.y, q1.x), q1.w) - p, -INFINITY),
+                             nextafterf(fminf(fminf(q0.z, q1.y), c2) - p, -INFINITY), 0.0f);
+    box[2 * f + 1] = make_float4(nextafterf(fmaxf(fmaxf(q0.x, q0.w), q1.z) + p, INFINITY),
+                                 nextafterf(fmaxf(fmaxf(q0.y, q1.x), q1.w) + p, INFINITY),
+                                 nextafterf(fmaxf(fmaxf(q0.z, q1.y), c2) + p, INFINITY), 0.0f);
+  }
+}
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ void bundle_axis(float fl, float fh, float ol, float oh, float dl, float dh, float& tlo,
+                                            float& thi) {
+  if (dl > 0.0f) {
+    thi = fminf(thi, (fh - ol) / dl);
+    const float e = fl - oh;
+    if (e > 0.0f) tlo = fmaxf(tlo, e / dh);
+  } else if (dh < 0.0f) {
+    thi = fminf(thi, (oh - fl) / -dh);
+    const float e = ol - fh;
+    if (e > 0.0f) tlo = fmaxf(tlo, e / -dl);
+  }
+}
+
+#ifndef RT_BOX_GROUP
+#define RT_BOX_GROUP 64
+#endif
+// minimum over each group of G lanes (every lane active): DPP within rows of 16, then lane swaps
+template <int G>
+__device__ __forceinline__ float group_min(float x) {
+  x = fminf(x, dpp_f<0xB1>(x));   // quad_perm [1,0,3,2]
+  x = fminf(x, dpp_f<0x4E>(x));   // quad_perm [2,3,0,1]
+  x = fminf(x, dpp_f<0x141>(x));  // row_half_mirror
+  x = fminf(x, dpp_f<0x140>(x));  // row_mirror
+  if constexpr (G >= 32) x = fminf(x, __shfl_xor(x, 16, 64));
+  if constexpr (G >= 64) x = fminf(x, __shfl_xor(x, 32, 64));
+  return x;
+}
+
+// every lane of the wave must call it; lanes with alive == false do not constrain the bundle.
+// Bundles of G lanes (G = 16, 32, 64): lane j of a group tests faces j, j + G, ... for its group
+template <int G>
+__device__ __forceinline__ uint64_t wave_boxes(const float4* box, int nf, bool alive, float3 o, float3 d) {
+  const float inf = INFINITY;
+  const float olx = group_min<G>(alive ? o.x : inf), ohx = -group_min<G>(alive ? -o.x : inf);
+  const float oly = group_min<G>(alive ? o.y : inf), ohy = -group_min<G>(alive ? -o.y : inf);
+  const float olz = group_min<G>(alive ? o.z : inf), ohz = -group_min<G>(alive ? -o.z : inf);
+  const float dlx = group_min<G>(alive ? d.x : inf), dhx = -group_min<G>(alive ? -d.x : inf);
+  const float dly = group_min<G>(alive ? d.y : inf), dhy = -group_min<G>(alive ? -d.y : inf);
+  const float dlz = group_min<G>(alive ? d.z : inf), dhz = -group_min<G>(alive ? -d.z : inf);
+  const int lane = threadIdx.x & 63;
+  uint64_t cand = 0;
+  for (int r = 0; r * G < nf; ++r) {
+    const int f = (lane & (G - 1)) + r * G;
+    bool in = false;
+    if (f < nf) {
+      const float4 bl = box[2 * f], bh = box[2 * f + 1];
+      float tlo = 0.0f, thi = INFINITY;
+      bundle_axis(bl.x, bh.x, olx, ohx, dlx, dhx, tlo, thi);
+      bundle_axis(bl.y, bh.y, oly, ohy, dly, dhy, tlo, thi);
+      bundle_axis(bl.z, bh.z, olz, ohz, dlz, dhz, tlo, thi);
+      in = tlo <= fmaf(thi, 1.00002f, 1e-6f);
+    }
+    const uint64_t bal = __ballot(in);
+    if constexpr (G == 64) {
+      cand = bal;
+    } else {
+      const uint64_t mine = (bal >> (lane & ~(G - 1))) & ((1ull << G) - 1);
+      cand |= mine << (r * G);
+    }
+  }
+  return cand;
+}
+
 __device__ __forceinline__ rt::Hit query_cone(const float4* tab, const float4* cone, int nf, const rt::Shear& s,
                                               float3 d, uint64_t wave_cand = 0, bool use_wave = false) {
   uint64_t cand = 0;
@@ -239,19 +350,7 @@ __device__ __forceinline__ rt::Hit query_cone(const float4* tab, const float4* c
       cand |= (uint64_t)in << f;
     }
   }
-  rt::LazyHit h;
-  rt::lazy_init(h);
-  const int off = s.kcase * 3;
-  while (cand) {
-    const int f = __builtin_ctzll(cand);
-    cand &= cand - 1;
-    const float4 q0 = tab[f * 18 + off + 0];
-    const float4 q1 = tab[f * 18 + off + 1];
-    const float c2 = tab[f * 18 + off + 2].x;
-    float T, det;
-    if (rt::tri_test(s, q0, q1, c2, T, det)) rt::lazy_consider(h, T, det, f);
-  }
-  return rt::lazy_finish(h);
+  return query_list(tab, s, cand);
 }
 
 template <bool USE_BVH>
@@ -364,7 +463,10 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
   extern __shared__ __attribute__((aligned(16))) float4 lds_tab[];
   float4* cone = lds_tab + (size_t)a.env_nf * 18;  // bounce-0 edge normals after the face table
   const bool use_cone = !USE_BVH && a.env_nf <= kConeMaxFaces;
+  float4* box = cone + (size_t)a.env_nf * 3;  // bounce >= 1 face boxes after the cone normals
+  const bool use_box = use_cone && a.order && a.box_cull;  // block-uniform
   if (use_cone) stage_cones(a, cone);  // made visible by stage_env's barrier
+  if (use_box) stage_boxes(a, box);
   stage_env<USE_BVH>(a, lds_tab);
 
   const float qnan = __builtin_nanf("");
@@ -388,7 +490,8 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
       use_wave = rho < 0.05f;  // wave-uniform (an invalid lane makes it +inf)
       if (use_wave) wave_cand = wave_cones(cone, a.env_nf, dir0, d0, fmaf(rho, 1.001f, 1e-6f));
     }
-    if (valid) {
+    // every lane runs the bounce loop (an invalid lane as a dead ray, storing nothing), so the wave-wide
+    // steps (wave_boxes) see the whole wave
     float3 dir = dir0;
     float3 pos = make_float3(a.tx[0], a.tx[1], a.tx[2]);
     float path[P][3];
@@ -398,13 +501,16 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
     path[0][1] = pos.y;
     path[0][2] = pos.z;
     int last_rx = -1;
-    bool alive = true;
+    bool alive = valid;
 #pragma unroll
     for (int b = 0; b < B; ++b) {
       int kind = 0, face = -1;
+      uint64_t box_cand = 0;
+      if (use_box && b > 0) box_cand = wave_boxes<RT_BOX_GROUP>(box, a.env_nf, alive, pos, dir);
       if (alive) {
         const rt::Shear s = rt::make_shear(pos, dir);
         const rt::Hit he = (b == 0 && use_cone) ? query_cone(lds_tab, cone, a.env_nf, s, dir, wave_cand, use_wave)
+                           : (use_box && b > 0) ? query_list(lds_tab, s, box_cand)
                                                 : env_hit_query<USE_BVH>(a, lds_tab, s, pos, dir);
         const bool env_hit = he.face >= 0;
         rt::Hit hr;
@@ -441,9 +547,10 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
           alive = false;  // kernel.py:97-98: every later iteration repeats this miss
         }
       }
-      if (a.hit_kind) a.hit_kind[row * B + b] = kind;
-      if (a.hit_face) a.hit_face[row * B + b] = face;
+      if (valid && a.hit_kind) a.hit_kind[row * B + b] = kind;
+      if (valid && a.hit_face) a.hit_face[row * B + b] = face;
     }
+    if (!valid) continue;  // block-uniform loop: the last chunk's spare lanes store nothing
     if (a.traced) store_row_fixed<P, false>(a.traced + row * (P * 3), path);
     // Direction-sorted launches: launch_trace fills received (NaN) and row_mask (0) in row order first, as the
     // reference does on the host (tracer.py:67-72), and only received rays store their row and
@@ -466,7 +573,6 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
       atomicAdd(a.fz.counts + c, 1);
       atomicAdd(a.fz.gcounts + (c >> 6), 1);
       atomicOr((unsigned long long*)a.fz.masks + c * 4 + ((row & 255) >> 6), 1ull << (row & 63));
-    }
     }
   }
 }
@@ -761,7 +867,18 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
   if (a.fused) a.fz = *fused;
   if (fused_done) *fused_done = a.fused;
   // brute force: the face table, then the bounce-0 cone normals (3 float4 per face, <= 64 faces)
-  const size_t lds = bvh ? 0 : (size_t)env->nf * (env->nf <= kConeMaxFaces ? 21 : 18) * sizeof(float4);
+  // then the bounce >= 1 face boxes (2 float4 per face, same meshes)
+  const size_t lds = bvh ? 0 : (size_t)env->nf * (env->nf <= kConeMaxFaces ? 23 : 18) * sizeof(float4);
+  {
+    float amax = 0.0f;
+    for (int k = 0; k < 3; ++k) amax = std::max(amax, std::max(std::fabs(env->lo[k]), std::fabs(env->hi[k])));
+    a.env_pad = 1e-5f * (1.0f + amax);
+  }
+  static const bool box_cull = [] {  // RFRT_K2_BOX=0: every face at bounces >= 1 (A/B checks)
+    const char* e = getenv("RFRT_K2_BOX");
+    return !(e && e[0] == '0');
+  }();
+  a.box_cull = box_cull;
   int dev_cu = 256;
   const int64_t want = (n + 255) / 256;
   const int64_t cap = (int64_t)dev_cu * 16;
