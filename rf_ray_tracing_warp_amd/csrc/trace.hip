@@ -25,6 +25,10 @@
 #include "rt_device.h"
 #include "rt_internal.h"
 
+#ifndef RT_DIAG_CAND  // diagnostics builds only (tools/k2_cand_stats.py)
+#define RT_DIAG_CAND 0
+#endif
+
 namespace {
 
 struct TraceArgs {
@@ -50,6 +54,11 @@ struct TraceArgs {
   bool sparse_rx;  // received rows / mask words filled beforehand (k_fill_received): store only received rays'
   bool box_cull;   // bounces >= 1 of sorted brute-force bursts: the wave's candidate faces (wave_boxes)
   float env_pad;   // face boxes padded by 1e-5 * (1 + scene's largest |coordinate|), as the BVH's boxes
+  // bounce 0: the receiver ball seen from the TX, unit axis rx_u and half-angle (sin, cos); rx_all0 when the
+  // TX is inside (or nearly inside) the ball
+  float rx_u[3], rx_sin, rx_cos;
+  bool rx_all0;
+  float cone_rho_max;  // bounce 0: wave cones when every |d_l - d_0| is below this
 };
 
 // Closest hit over a brute-force face list whose permuted table lives at `tab`
@@ -253,17 +262,30 @@ __device__ __forceinline__ rt::Hit query_list(const float4* tab, const rt::Shear
 // every output bit is unchanged.  The face boxes are padded by 1e-5 * (1 + scene scale) and rounded
 // outward, the same invariant the BVH's boxes rest on (rt_bvh.h: an accepted hit lies inside its
 // face's padded box), and the compare keeps the BVH slab's slack.
+// Slot nf holds the receiver ball's box (when nf < 64): its bit tells whether any lane of the wave
+// can reach the receiver, so most waves skip rx_maybe.  Groups of 32 or 16 lanes per bundle measured
+// slower (113.6 / 116.1 against 110.3 us, r5ai): tighter bundles, but more face rounds.
+__device__ __forceinline__ float4 pad_lo(float x, float y, float z, float p) {
+  return make_float4(nextafterf(x - p, -INFINITY), nextafterf(y - p, -INFINITY), nextafterf(z - p, -INFINITY), 0.0f);
+}
+__device__ __forceinline__ float4 pad_hi(float x, float y, float z, float p) {
+  return make_float4(nextafterf(x + p, INFINITY), nextafterf(y + p, INFINITY), nextafterf(z + p, INFINITY), 0.0f);
+}
 __device__ __forceinline__ void stage_boxes(const TraceArgs& a, float4* box) {
+  const float p = a.env_pad;
   for (int f = threadIdx.x; f < a.env_nf; f += blockDim.x) {
     const float4 q0 = a.env_perm[f * 18 + 12], q1 = a.env_perm[f * 18 + 13];  // case 4: x, y, z
     const float c2 = a.env_perm[f * 18 + 14].x;
-    const float p = a.env_pad;
-    box[2 * f] = make_float4(nextafterf(fminf(fminf(q0.x, q0.w), q1.z) - p, -INFINITY),
-                             nextafterf(fminf(fminf(q0.y, q1.x), q1.w) - p, -INFINITY),
-                             nextafterf(fminf(fminf(q0.z, q1.y), c2) - p, -INFINITY), 0.0f);
-    box[2 * f + 1] = make_float4(nextafterf(fmaxf(fmaxf(q0.x, q0.w), q1.z) + p, INFINITY),
-                                 nextafterf(fmaxf(fmaxf(q0.y, q1.x), q1.w) + p, INFINITY),
-                                 nextafterf(fmaxf(fmaxf(q0.z, q1.y), c2) + p, INFINITY), 0.0f);
+    box[2 * f] = pad_lo(fminf(fminf(q0.x, q0.w), q1.z), fminf(fminf(q0.y, q1.x), q1.w), fminf(fminf(q0.z, q1.y), c2), p);
+    box[2 * f + 1] =
+        pad_hi(fmaxf(fmaxf(q0.x, q0.w), q1.z), fmaxf(fmaxf(q0.y, q1.x), q1.w), fmaxf(fmaxf(q0.z, q1.y), c2), p);
+  }
+  if (threadIdx.x == 0 && a.env_nf < 64) {  // the receiver ball (no receiver: an empty box, never reached)
+    const float r = a.rx_nf > 0 ? sqrtf(a.rx_r2) : 0.0f;
+    box[2 * a.env_nf] = a.rx_nf > 0 ? pad_lo(a.rx_c[0] - r, a.rx_c[1] - r, a.rx_c[2] - r, p)
+                                    : make_float4(INFINITY, INFINITY, INFINITY, 0.0f);
+    box[2 * a.env_nf + 1] = a.rx_nf > 0 ? pad_hi(a.rx_c[0] + r, a.rx_c[1] + r, a.rx_c[2] + r, p)
+                                        : make_float4(-INFINITY, -INFINITY, -INFINITY, 0.0f);
   }
 }
 
@@ -271,6 +293,16 @@ template <int CTRL>
 __device__ __forceinline__ float dpp_f(float x) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
 }
+// minimum over the 64 lanes (every lane active): DPP within rows of 16, then two lane swaps
+__device__ __forceinline__ float wave_min(float x) {
+  x = fminf(x, dpp_f<0xB1>(x));   // quad_perm [1,0,3,2]
+  x = fminf(x, dpp_f<0x4E>(x));   // quad_perm [2,3,0,1]
+  x = fminf(x, dpp_f<0x141>(x));  // row_half_mirror
+  x = fminf(x, dpp_f<0x140>(x));  // row_mirror
+  x = fminf(x, __shfl_xor(x, 16, 64));
+  return fminf(x, __shfl_xor(x, 32, 64));
+}
+
 __device__ __forceinline__ void bundle_axis(float fl, float fh, float ol, float oh, float dl, float dh, float& tlo,
                                             float& thi) {
   if (dl > 0.0f) {
@@ -284,54 +316,23 @@ __device__ __forceinline__ void bundle_axis(float fl, float fh, float ol, float 
   }
 }
 
-#ifndef RT_BOX_GROUP
-#define RT_BOX_GROUP 64
-#endif
-// minimum over each group of G lanes (every lane active): DPP within rows of 16, then lane swaps
-template <int G>
-__device__ __forceinline__ float group_min(float x) {
-  x = fminf(x, dpp_f<0xB1>(x));   // quad_perm [1,0,3,2]
-  x = fminf(x, dpp_f<0x4E>(x));   // quad_perm [2,3,0,1]
-  x = fminf(x, dpp_f<0x141>(x));  // row_half_mirror
-  x = fminf(x, dpp_f<0x140>(x));  // row_mirror
-  if constexpr (G >= 32) x = fminf(x, __shfl_xor(x, 16, 64));
-  if constexpr (G >= 64) x = fminf(x, __shfl_xor(x, 32, 64));
-  return x;
-}
-
 // every lane of the wave must call it; lanes with alive == false do not constrain the bundle.
-// Bundles of G lanes (G = 16, 32, 64): lane j of a group tests faces j, j + G, ... for its group
-template <int G>
+// Bit f < nf: face f is a candidate; bit nf (nf < 64): the receiver ball can be reached.
 __device__ __forceinline__ uint64_t wave_boxes(const float4* box, int nf, bool alive, float3 o, float3 d) {
-  const float inf = INFINITY;
-  const float olx = group_min<G>(alive ? o.x : inf), ohx = -group_min<G>(alive ? -o.x : inf);
-  const float oly = group_min<G>(alive ? o.y : inf), ohy = -group_min<G>(alive ? -o.y : inf);
-  const float olz = group_min<G>(alive ? o.z : inf), ohz = -group_min<G>(alive ? -o.z : inf);
-  const float dlx = group_min<G>(alive ? d.x : inf), dhx = -group_min<G>(alive ? -d.x : inf);
-  const float dly = group_min<G>(alive ? d.y : inf), dhy = -group_min<G>(alive ? -d.y : inf);
-  const float dlz = group_min<G>(alive ? d.z : inf), dhz = -group_min<G>(alive ? -d.z : inf);
   const int lane = threadIdx.x & 63;
-  uint64_t cand = 0;
-  for (int r = 0; r * G < nf; ++r) {
-    const int f = (lane & (G - 1)) + r * G;
-    bool in = false;
-    if (f < nf) {
-      const float4 bl = box[2 * f], bh = box[2 * f + 1];
-      float tlo = 0.0f, thi = INFINITY;
-      bundle_axis(bl.x, bh.x, olx, ohx, dlx, dhx, tlo, thi);
-      bundle_axis(bl.y, bh.y, oly, ohy, dly, dhy, tlo, thi);
-      bundle_axis(bl.z, bh.z, olz, ohz, dlz, dhz, tlo, thi);
-      in = tlo <= fmaf(thi, 1.00002f, 1e-6f);
-    }
-    const uint64_t bal = __ballot(in);
-    if constexpr (G == 64) {
-      cand = bal;
-    } else {
-      const uint64_t mine = (bal >> (lane & ~(G - 1))) & ((1ull << G) - 1);
-      cand |= mine << (r * G);
-    }
-  }
-  return cand;
+  const bool mine = lane <= nf && lane < 64;
+  const int f = mine ? lane : 0;
+  const float4 bl = box[2 * f], bh = box[2 * f + 1];
+  float tlo = 0.0f, thi = INFINITY;
+  const float inf = INFINITY;
+  // axis by axis, so only one axis' four bounds are live at a time
+  bundle_axis(bl.x, bh.x, wave_min(alive ? o.x : inf), -wave_min(alive ? -o.x : inf), wave_min(alive ? d.x : inf),
+              -wave_min(alive ? -d.x : inf), tlo, thi);
+  bundle_axis(bl.y, bh.y, wave_min(alive ? o.y : inf), -wave_min(alive ? -o.y : inf), wave_min(alive ? d.y : inf),
+              -wave_min(alive ? -d.y : inf), tlo, thi);
+  bundle_axis(bl.z, bh.z, wave_min(alive ? o.z : inf), -wave_min(alive ? -o.z : inf), wave_min(alive ? d.z : inf),
+              -wave_min(alive ? -d.z : inf), tlo, thi);
+  return __ballot(mine && tlo <= fmaf(thi, 1.00002f, 1e-6f));
 }
 
 __device__ __forceinline__ rt::Hit query_cone(const float4* tab, const float4* cone, int nf, const rt::Shear& s,
@@ -480,15 +481,23 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
     // bounce 0 on a direction-sorted burst: the wave's cone candidates at once (wave_cones), when
     // every lane has a ray and the directions lie within 0.05 of lane 0's
     uint64_t wave_cand = 0;
-    bool use_wave = false;
+    bool use_wave = false, rx_wave0 = true;
     if (use_cone && a.order) {  // block-uniform
       const float3 d0 = make_float3(__shfl(dir0.x, 0, 64), __shfl(dir0.y, 0, 64), __shfl(dir0.z, 0, 64));
       const float ex = dir0.x - d0.x, ey = dir0.y - d0.y, ez = dir0.z - d0.z;
       float rho = valid ? sqrtf(fmaf(ex, ex, fmaf(ey, ey, ez * ez))) : INFINITY;
 #pragma unroll
       for (int o = 32; o >= 1; o >>= 1) rho = fmaxf(rho, __shfl_xor(rho, o, 64));
-      use_wave = rho < 0.05f;  // wave-uniform (an invalid lane makes it +inf)
+      use_wave = rho < a.cone_rho_max;  // wave-uniform (an invalid lane makes it +inf)
       if (use_wave) wave_cand = wave_cones(cone, a.env_nf, dir0, d0, fmaf(rho, 1.001f, 1e-6f));
+      // the receiver ball at bounce 0: a lane can reach it only if angle(d, u) <= alpha, and
+      // angle(d, d0) <= 2 asin(rho / 2) < beta, so the wave skips rx_maybe when d0 . u < cos(alpha + beta),
+      // bounded below by cos(alpha) (1 - beta^2 / 2) - sin(alpha) beta
+      if (use_wave && !a.rx_all0) {
+        const float beta = fmaf(rho * rho * rho, 1.0f / 12.0f, fmaf(rho, 1.001f, 1e-3f));  // > 2 asin(rho / 2)
+        const float thr = fmaf(a.rx_cos, fmaf(-0.5f * beta, beta, 1.0f), -a.rx_sin * beta) - 1e-5f;
+        rx_wave0 = !(fmaf(d0.x, a.rx_u[0], fmaf(d0.y, a.rx_u[1], d0.z * a.rx_u[2])) < thr);
+      }
     }
     // every lane runs the bounce loop (an invalid lane as a dead ray, storing nothing), so the wave-wide
     // steps (wave_boxes) see the whole wave
@@ -506,7 +515,16 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
     for (int b = 0; b < B; ++b) {
       int kind = 0, face = -1;
       uint64_t box_cand = 0;
-      if (use_box && b > 0) box_cand = wave_boxes<RT_BOX_GROUP>(box, a.env_nf, alive, pos, dir);
+      bool rx_wave = true;  // can any lane of the wave reach the receiver ball (wave-uniform)
+      if (use_box && b > 0) {
+        box_cand = wave_boxes(box, a.env_nf, alive, pos, dir);
+        if (a.env_nf < 64) {
+          rx_wave = (box_cand >> a.env_nf) & 1;
+          box_cand &= (1ull << a.env_nf) - 1;
+        }
+      } else if (b == 0) {
+        rx_wave = rx_wave0;
+      }
       if (alive) {
         const rt::Shear s = rt::make_shear(pos, dir);
         const rt::Hit he = (b == 0 && use_cone) ? query_cone(lds_tab, cone, a.env_nf, s, dir, wave_cand, use_wave)
@@ -515,7 +533,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
         const bool env_hit = he.face >= 0;
         rt::Hit hr;
         rt::hit_init(hr);
-        if (a.rx_nf > 0 && rx_maybe(a, pos, dir, env_hit ? he.t : RT_MAX_T))
+        if (rx_wave && a.rx_nf > 0 && rx_maybe(a, pos, dir, env_hit ? he.t : RT_MAX_T))
           hr = query_faces(a.rx_perm, a.rx_nf, s);
         const bool rx_hit = hr.face >= 0;
         if (rx_hit && (!env_hit || he.t > hr.t)) {  // kernel.py:85
@@ -548,7 +566,12 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
         }
       }
       if (valid && a.hit_kind) a.hit_kind[row * B + b] = kind;
+#if RT_DIAG_CAND  // diagnostics (tools/k2_cand_stats.py): the wave's candidate count, rx_wave, alive
+      if (valid && a.hit_face)
+        a.hit_face[row * B + b] = __popcll(b == 0 ? wave_cand : box_cand) | (rx_wave ? 256 : 0) | (alive ? 512 : 0);
+#else
       if (valid && a.hit_face) a.hit_face[row * B + b] = face;
+#endif
     }
     if (!valid) continue;  // block-uniform loop: the last chunk's spare lanes store nothing
     if (a.traced) store_row_fixed<P, false>(a.traced + row * (P * 3), path);
@@ -867,11 +890,12 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
   if (a.fused) a.fz = *fused;
   if (fused_done) *fused_done = a.fused;
   // brute force: the face table, then the bounce-0 cone normals (3 float4 per face, <= 64 faces)
-  // then the bounce >= 1 face boxes (2 float4 per face, same meshes)
-  const size_t lds = bvh ? 0 : (size_t)env->nf * (env->nf <= kConeMaxFaces ? 23 : 18) * sizeof(float4);
+  // then the bounce >= 1 face boxes (2 float4 per face, same meshes) and the receiver ball's box
+  const size_t lds = bvh ? 0 : (size_t)(env->nf <= kConeMaxFaces ? env->nf * 23 + 2 : env->nf * 18) * sizeof(float4);
   {
-    float amax = 0.0f;
+    float amax = 0.0f;  // the environment's and the receiver's coordinates
     for (int k = 0; k < 3; ++k) amax = std::max(amax, std::max(std::fabs(env->lo[k]), std::fabs(env->hi[k])));
+    for (int k = 0; rx && k < 3; ++k) amax = std::max(amax, std::max(std::fabs(rx->lo[k]), std::fabs(rx->hi[k])));
     a.env_pad = 1e-5f * (1.0f + amax);
   }
   static const bool box_cull = [] {  // RFRT_K2_BOX=0: every face at bounces >= 1 (A/B checks)
@@ -879,6 +903,25 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
     return !(e && e[0] == '0');
   }();
   a.box_cull = box_cull;
+  // bounce-0 wave cones up to a spread of 0.3: 0.05 left half of K2's waves (banded order: a wave spans
+  // a long strip of directions) on the per-lane cone loop; 0.3 takes nearly all, K2 rt_trace -7 us (r5aq)
+  a.cone_rho_max = 0.3f;
+
+  a.rx_all0 = true;
+  if (rx) {  // the receiver ball seen from the TX (bounce 0 of the sorted brute-force kernels)
+    const double dx = (double)rx->center[0] - tx[0], dy = (double)rx->center[1] - tx[1],
+                 dz = (double)rx->center[2] - tx[2];
+    const double dist = std::sqrt(dx * dx + dy * dy + dz * dz), r = (double)rx->radius * 1.001 + 1e-4;
+    if (dist > 2.0 * r) {
+      a.rx_all0 = false;
+      a.rx_u[0] = (float)(dx / dist);
+      a.rx_u[1] = (float)(dy / dist);
+      a.rx_u[2] = (float)(dz / dist);
+      const double sa = r / dist;
+      a.rx_sin = (float)(sa * 1.001);
+      a.rx_cos = (float)(std::sqrt(1.0 - sa * sa) * (1.0 - 1e-6));
+    }
+  }
   int dev_cu = 256;
   const int64_t want = (n + 255) / 256;
   const int64_t cap = (int64_t)dev_cu * 16;

@@ -185,6 +185,25 @@ def test_trace_k2_full_size(room):
     np.testing.assert_array_equal(rc[fin], tr[fin])
 
 
+@pytest.mark.parametrize("tx,rx,rad,B,off", [
+    ((10, 0, 5), (6, 1, 5), 1.0, 3, 0),          # a large receiver near the TX: many bounce-0 waves reach it
+    ((10, 0, 5), (10.3, 0.2, 5.1), 0.5, 3, 7),   # TX inside the (padded) receiver ball
+    ((-3, 4, 2), (12, -6, 8), 0.8, 5, 123_457),  # receiver near a corner, reached after reflections
+    ((0, 5, 7), (10, 0.5, 5), 0.3, 8, 99),
+])
+def test_trace_sorted_bursts(room, tx, rx, rad, B, off):
+    """Direction-sorted brute-force bursts (n >= 2^16): bounce-0 wave cones, the bounce >= 1 bundle
+    boxes and the receiver's wave tests -- every received row and a 1/20 subsample, bit-exact."""
+    n = 100_000
+    rxm = sphere(rx, rad, 1)
+    g = _gpu_trace(room, rxm, tx, B, off, n)
+    assert g["mask"].sum() > 0
+    E, R = orc.Mesh(room.vertices, room.faces), orc.Mesh(rxm.vertices, rxm.faces)
+    rows = np.union1d(np.arange(0, n, 20), np.nonzero(g["mask"])[0])
+    o = orc.trace_ids(E, R, tx, B, rows + off)
+    _assert_trace_equal(g, o, rows)
+
+
 def test_artifact_scene_html_gpu(empty):
     """The reference artifact's 119 received rays (tests/golden/scene_html.npz) on the GPU."""
     g = np.load(os.path.join(HERE, "golden", "scene_html.npz"))
