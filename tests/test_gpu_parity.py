@@ -204,6 +204,34 @@ def test_trace_sorted_bursts(room, tx, rx, rad, B, off):
     _assert_trace_equal(g, o, rows)
 
 
+def _cluttered_room(room, extra, seed):
+    """room.stl plus `extra` small random triangles inside it (face counts around the 64-face
+    limit of the bounce-0 cones and the bounce >= 1 bundle boxes, whose slot nf < 64 holds the receiver)."""
+    from rf_ray_tracing_warp_amd.mesh import TriMesh
+    rng = np.random.default_rng(seed)
+    v = np.asarray(room.vertices, np.float64)
+    f = np.asarray(room.faces, np.int64)
+    c = rng.uniform((-12, -12, 1), (12, 12, 12), (extra, 1, 3))
+    tri = c + rng.uniform(-1.5, 1.5, (extra, 3, 3))
+    v2 = np.concatenate([v, tri.reshape(-1, 3)])
+    f2 = np.concatenate([f, len(v) + np.arange(3 * extra).reshape(extra, 3)])
+    return TriMesh(v2, f2)
+
+
+@pytest.mark.parametrize("extra", [19, 20, 21])  # 63, 64, 65 faces
+def test_trace_sorted_bursts_face_limits(room, extra):
+    env = _cluttered_room(room, extra, seed=extra)
+    assert len(env.faces) == 44 + extra
+    n, B, tx, rx, off = 80_000, 3, (10, 0, 5), (4, 2, 5), 11
+    rxm = sphere(rx, 0.7, 1)
+    g = _gpu_trace(env, rxm, tx, B, off, n)
+    assert g["mask"].sum() > 0
+    E, R = orc.Mesh(env.vertices, env.faces), orc.Mesh(rxm.vertices, rxm.faces)
+    rows = np.union1d(np.arange(0, n, 16), np.nonzero(g["mask"])[0])
+    o = orc.trace_ids(E, R, tx, B, rows + off)
+    _assert_trace_equal(g, o, rows)
+
+
 def test_artifact_scene_html_gpu(empty):
     """The reference artifact's 119 received rays (tests/golden/scene_html.npz) on the GPU."""
     g = np.load(os.path.join(HERE, "golden", "scene_html.npz"))
