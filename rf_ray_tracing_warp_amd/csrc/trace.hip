@@ -49,6 +49,8 @@ struct TraceArgs {
   int32_t* hit_kind;  // (n, B) or null
   int32_t* hit_face;  // (n, B) or null
   const int32_t* order;  // processing order of the rows (null = identity), see launch_trace
+  const int32_t* sched;  // processing order of the 256-row chunks (null = identity), see chunk_schedule
+  uint32_t* cost;        // per-chunk cost to record (null = off): wave time, 10 ns ticks, summed
   bool fused;             // brute-force kernels under rt_trace_cir: list received rows, per-path CIR
   rt::TraceCirFused fz;
   bool sparse_rx;  // received rows / mask words filled beforehand (k_fill_received): store only received rays'
@@ -473,7 +475,9 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
   const float qnan = __builtin_nanf("");
   // block-uniform loop over 256-row chunks (the same rows per thread as a grid-stride loop), so a
   // wave can list its part of a chunk's received rows for rt_trace_cir
-  for (int64_t chunk = blockIdx.x; chunk * 256 < a.n; chunk += gridDim.x) {
+  for (int64_t c0 = blockIdx.x; c0 * 256 < a.n; c0 += gridDim.x) {
+    const int64_t chunk = a.sched ? (int64_t)a.sched[c0] : c0;
+    const uint64_t t_begin = a.cost ? wall_clock64() : 0;
     const int64_t irow = chunk * 256 + threadIdx.x;
     const bool valid = irow < a.n;
     const int64_t row = valid ? (a.order ? (int64_t)a.order[irow] : irow) : 0;
@@ -573,6 +577,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& a) {
       if (valid && a.hit_face) a.hit_face[row * B + b] = face;
 #endif
     }
+    if (a.cost && (threadIdx.x & 63) == 0) atomicAdd(a.cost + chunk, (uint32_t)(wall_clock64() - t_begin));
     if (!valid) continue;  // block-uniform loop: the last chunk's spare lanes store nothing
     if (a.traced) store_row_fixed<P, false>(a.traced + row * (P * 3), path);
     // Direction-sorted launches: launch_trace fills received (NaN) and row_mask (0) in row order first, as the
@@ -860,6 +865,136 @@ void trace_events(hipEvent_t* e0, hipEvent_t* e1);
 // fused (optional, rt_trace_cir): the brute-force kernels list each chunk's received rows as they go
 // and their last block finishes the CIR step; *fused_done tells whether they did (BVH and generic
 // kernels: no, rt_trace_cir then launches k_chunk_counts + k_compact_cir)
+// ------------------------------------------------------------------ chunk schedule (longest first)
+// The chunks of a direction-sorted burst differ several-fold in cost (coherent strips against waves
+// that straddle walls and corners), and the dispatcher starts blocks in chunk order: costly chunks
+// at the end of the order leave the GPU draining a few slow blocks (K2: 132 us with the chunk order
+// reversed against 104 forward, r5aw).  The first launch of a (device, rays, bounces, scene, TX)
+// records each chunk's summed wave time (wall_clock64, one atomic per wave); k_chunk_schedule then
+// orders the chunks by cost, longest first (LPT: 256 linear buckets of the largest cost, a counting
+// sort in one block), and later launches run them in that order.  Any permutation traces the same
+// rows with the same results; the schedule only moves the slow blocks to the front.
+constexpr int kSchedBuckets = 256;
+constexpr int64_t kSchedMaxChunks = 1 << 20;
+__global__ __launch_bounds__(1024) void k_chunk_schedule(const uint32_t* cost, int64_t nch, int32_t* sched) {
+  __shared__ uint32_t s_max;
+  __shared__ int s_off[kSchedBuckets];
+  if (threadIdx.x == 0) s_max = 0;
+  for (int i = threadIdx.x; i < kSchedBuckets; i += blockDim.x) s_off[i] = 0;
+  __syncthreads();
+  uint32_t m = 0;
+  for (int64_t c = threadIdx.x; c < nch; c += blockDim.x) m = max(m, cost[c]);
+  atomicMax(&s_max, m);
+  __syncthreads();
+  const uint64_t top = (uint64_t)s_max + 1;
+  auto bucket = [&](int64_t c) {  // costliest first
+    return kSchedBuckets - 1 - (int)((uint64_t)cost[c] * kSchedBuckets / top);
+  };
+  for (int64_t c = threadIdx.x; c < nch; c += blockDim.x) atomicAdd(&s_off[bucket(c)], 1);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int run = 0;
+    for (int i = 0; i < kSchedBuckets; ++i) {
+      const int k = s_off[i];
+      s_off[i] = run;
+      run += k;
+    }
+  }
+  __syncthreads();
+  for (int64_t c = threadIdx.x; c < nch; c += blockDim.x) sched[atomicAdd(&s_off[bucket(c)], 1)] = (int32_t)c;
+}
+
+namespace {
+struct SchedEntry {
+  int device = -1, B = 0;
+  int64_t ray_offset = 0, n = 0;
+  const rt_mesh *env = nullptr, *rx = nullptr;
+  float tx[3] = {0, 0, 0};
+  int32_t* sched = nullptr;
+  uint32_t* cost = nullptr;
+  hipEvent_t ready = nullptr;  // recorded after k_chunk_schedule
+  hipStream_t made_on = nullptr;
+  uint64_t used = 0;
+};
+constexpr int kSchedCache = 8;
+SchedEntry g_sched[kSchedCache];
+uint64_t g_sched_clock = 0;
+std::mutex g_sched_mu;
+
+bool chunk_schedule_on() {  // RFRT_K2_LPT=0: chunks in order (A/B checks)
+  static const bool v = [] {
+    const char* e = getenv("RFRT_K2_LPT");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
+// Sets a.sched (schedule ready) or a.cost (this launch records the costs; *profile then names the
+// entry whose schedule finish_chunk_schedule computes after the launch).  Errors leave both null.
+void chunk_schedule(TraceArgs& a, int dev, const rt_mesh* env, const rt_mesh* rx, const float tx[3], int B,
+                    int64_t ray_offset, int64_t n, hipStream_t stream, SchedEntry** profile) {
+  *profile = nullptr;
+  const int64_t nch = (n + 255) / 256;
+  if (!chunk_schedule_on() || nch > kSchedMaxChunks) return;
+  std::lock_guard<std::mutex> lock(g_sched_mu);
+  for (SchedEntry& e : g_sched)
+    if (e.sched && e.device == dev && e.B == B && e.ray_offset == ray_offset && e.n == n && e.env == env &&
+        e.rx == rx && e.tx[0] == tx[0] && e.tx[1] == tx[1] && e.tx[2] == tx[2]) {
+      e.used = ++g_sched_clock;
+      if (e.made_on != stream && hipStreamWaitEvent(stream, e.ready, 0) != hipSuccess) return;
+      a.sched = e.sched;
+      return;
+    }
+  SchedEntry* slot = &g_sched[0];
+  for (SchedEntry& e : g_sched)
+    if (!e.sched) {
+      slot = &e;
+      break;
+    } else if (e.used < slot->used) {
+      slot = &e;
+    }
+  if (slot->sched) {  // evict (hipFree waits for the device)
+    int cur = dev;
+    if (slot->device != dev) (void)hipSetDevice(slot->device);
+    (void)hipFree(slot->sched);
+    (void)hipFree(slot->cost);
+    if (slot->ready) (void)hipEventDestroy(slot->ready);
+    if (slot->device != cur) (void)hipSetDevice(cur);
+    *slot = SchedEntry{};
+  }
+  SchedEntry e;
+  e.device = dev;
+  e.B = B;
+  e.ray_offset = ray_offset;
+  e.n = n;
+  e.env = env;
+  e.rx = rx;
+  for (int k = 0; k < 3; ++k) e.tx[k] = tx[k];
+  hipError_t err = hipMalloc(&e.sched, sizeof(int32_t) * (size_t)nch);
+  if (err == hipSuccess) err = hipMalloc(&e.cost, sizeof(uint32_t) * (size_t)nch);
+  if (err == hipSuccess) err = hipEventCreateWithFlags(&e.ready, hipEventDisableTiming);
+  if (err == hipSuccess) err = hipMemsetAsync(e.cost, 0, sizeof(uint32_t) * (size_t)nch, stream);
+  if (err != hipSuccess) {  // no schedule: chunks in order
+    if (e.sched) (void)hipFree(e.sched);
+    if (e.cost) (void)hipFree(e.cost);
+    if (e.ready) (void)hipEventDestroy(e.ready);
+    return;
+  }
+  e.made_on = stream;
+  e.used = ++g_sched_clock;
+  *slot = e;
+  a.cost = slot->cost;
+  *profile = slot;
+}
+
+int finish_chunk_schedule(SchedEntry* e, int64_t n, hipStream_t stream) {
+  hipLaunchKernelGGL(k_chunk_schedule, dim3(1), dim3(1024), 0, stream, e->cost, (n + 255) / 256, e->sched);
+  hipError_t err = hipGetLastError();
+  if (err == hipSuccess) err = hipEventRecord(e->ready, stream);
+  return err == hipSuccess ? 0 : hip_fail(err, "chunk schedule");
+}
+}  // namespace
+
 int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B, int64_t ray_offset, int64_t n,
                  float* traced, float* received, uint32_t* mask, int32_t* hit_kind, int32_t* hit_face,
                  hipStream_t stream, const TraceCirFused* fused, bool* fused_done) {
@@ -945,10 +1080,15 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
     if (rc) return rc;
   }
   const bool sort = (bvh || B <= 8) && n >= kSortMinRays && n <= INT32_MAX;
+  SchedEntry* sched_profile = nullptr;
   if (sort) {
     trace_mark(0, stream);
     a.order = dir_order_cached(ray_offset, n, stream);
     if (!a.order) return -1;
+    if (B <= 8) {
+      int dev = 0;
+      if (hipGetDevice(&dev) == hipSuccess) chunk_schedule(a, dev, env, rx, tx, B, ray_offset, n, stream, &sched_profile);
+    }
     trace_mark(1, stream);
   }
   const int grid = grid0;
@@ -995,6 +1135,10 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
       break;
   }
 #undef RT_LAUNCH
+  if (sched_profile) {
+    const int rc = finish_chunk_schedule(sched_profile, n, stream);
+    if (rc) return rc;
+  }
   if (a.fused) hipLaunchKernelGGL(k_trace_cir_tail, dim3(1), dim3(512), 0, stream, a.fz, n, received, B + 1);
   RT_HIP(hipGetLastError());
   return 0;

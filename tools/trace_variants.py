@@ -47,6 +47,9 @@ def child(n, B, reps, scene="room"):
         go()
     e1.record(st)
     torch.cuda.synchronize()
+    h2 = hashlib.sha256(tr.cpu().numpy().tobytes() + rc.cpu().numpy().tobytes() + mk.cpu().numpy().tobytes()).hexdigest()
+    if h2 != h:  # later launches (cached order and chunk schedule) must give the first launch's bits
+        h = "repeat-differs-" + h2
     print(json.dumps({"variant": os.environ.get(os.environ.get("VAR_ENV", "RFRT_TRACE_VARIANT"), "0"),
                       "lib": os.path.basename(os.environ.get("RFRT_LIB_PATH", "librfrt.so")),
                       "us": e0.elapsed_time(e1) * 1e3 / reps, "hash": h[:16], "bvh": env.bvh_info()}))
@@ -70,6 +73,7 @@ if __name__ == "__main__":
             env[os.environ.get("VAR_ENV", "RFRT_TRACE_VARIANT")] = v
         scene = os.environ.get("SCENE", "room")
         n, B, reps = ("2097152", "5", "5") if scene == "terrain" else ("1000000", "3", "50")
+        n = os.environ.get("N", n)  # burst size override (tail-effect probes)
         out = subprocess.run([sys.executable, __file__, "child", n, B, reps, scene], env=env, capture_output=True,
                              text=True, timeout=300)
         if out.returncode != 0:
