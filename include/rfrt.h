@@ -66,7 +66,10 @@ int rt_bvh_info(const rt_mesh* mesh, int64_t* info4);
  *   hit_kind (n, B) i32       per bounce 0 miss / 1 env / 2 receiver   (diagnostic, not in reference)
  *   hit_face (n, B) i32       per bounce face id of the chosen hit, -1 on miss (diagnostic)
  * rx may be NULL (no receiver); it is queried by brute force, so at most 65536 faces (RT_EINVAL
- * otherwise, before any launch).  max_bounces > 8 requires `traced` (it holds the path). */
+ * otherwise, before any launch).  max_bounces > 8 requires `traced` (it holds the path).
+ * Bursts of >= 65536 rays run in a cached direction-sorted order and, from the second call with the
+ * same (rays, bounces, meshes, TX) on, a cached longest-first chunk schedule; neither changes a bit
+ * of the outputs (Conventions). */
 int rt_trace(const rt_mesh* env, const float* tx_pos, const rt_mesh* rx, int max_bounces, int64_t ray_offset,
              int64_t n, float* traced, float* received, uint32_t* row_mask, int32_t* hit_kind, int32_t* hit_face,
              void* stream);
