@@ -206,6 +206,10 @@ def test_trace_k2_full_size(room):
     ((10, 0, 5), (10.3, 0.2, 5.1), 0.5, 3, 7),   # TX inside the (padded) receiver ball
     ((-3, 4, 2), (12, -6, 8), 0.8, 5, 123_457),  # receiver near a corner, reached after reflections
     ((0, 5, 7), (10, 0.5, 5), 0.3, 8, 99),
+    ((10, 0, 5), (6, 1, 5), 1.0, 1, 5),           # k_trace_bf<1>: bounce 0 only
+    ((10, 0, 5), (-4, 3, 6), 0.6, 2, 77),
+    ((2, -6, 3), (-8, 8, 9), 0.9, 4, 31_337),
+    ((-12, 12, 13), (9, -9, 2), 0.9, 7, 4_242),
 ])
 def test_trace_sorted_bursts(room, tx, rx, rad, B, off):
     """Direction-sorted brute-force bursts (n >= 2^16): bounce-0 wave cones, the bounce >= 1 bundle
