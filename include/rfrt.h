@@ -145,6 +145,13 @@ int rt_coverage_run(rt_coverage* cov, const float* tx_pos, double tx_power, doub
 int rt_coverage_create_rays(int device, const rt_mesh* env, int max_bounces, int64_t n_rays_total, int64_t ray_offset,
                             int64_t n_rays, const rt_grid* grid, double rx_radius, int rank, int world,
                             rt_coverage** out);
+/* rt_coverage_create_rays with the rays chosen by direction instead of by id: the burst of
+ * n_rays_total rays sorted by the azimuth of each ray's initial direction (kernel.py:51-52), rank r
+ * taking positions [r n / world, (r+1) n / world) of that order -- a wedge of directions around the
+ * transmitter, so that the rank's trajectories, candidates and replays stay in one sector of the
+ * scene.  Any partition of the rays gives the same map bit for bit (exact fixed-point sums). */
+int rt_coverage_create_sectors(int device, const rt_mesh* env, int max_bounces, int64_t n_rays_total,
+                               const rt_grid* grid, double rx_radius, int rank, int world, rt_coverage** out);
 int rt_coverage_trace_records(rt_coverage* cov, const float* tx_pos, double tx_power, double light_speed,
                               double sample_rate, int flags, int64_t n_bins, int64_t* counts, int64_t* stats,
                               void* stream);
@@ -240,6 +247,10 @@ int rt_coverage_last_profile(rt_coverage* cov, double* out, int n);
  * < 0 turns it off (default).  A result that changes with the byte reads memory the run never
  * wrote (tests/test_gpu_poison.py). */
 int rt_debug_poison(int byte);
+/* Debug: lists of first wins longer than n take the device-wide replay-order sort instead of the
+ * 4096-entry windows (default 2^21, i.e. only one GPU's whole map; n < 0 restores it).  Process-wide.
+ * The parity tests set 0 to drive the whole-map sort path on small grids. */
+int rt_debug_replay_window_max(int64_t n);
 int rt_selftest_math(const float* x, int64_t n, float* out, int op, void* stream);
 int rt_ray_dirs(int64_t ray_offset, int64_t n, float* out, void* stream);
 /* Exact fixed point of the coverage sums, on the host: op 0 converts n (w0, w1, w2) uint64 triples

@@ -120,13 +120,18 @@ class Coverage:
         self.rx_radius = float(rx_radius)
         self.n_bins = int(sample_window_s * sample_rate_hz)
         self.shard_index, self.shard_count = int(shard_index), int(shard_count)
-        if shard_mode not in ("cells", "rays"):
-            raise ValueError(f"shard_mode must be 'cells' or 'rays', not {shard_mode!r}")
+        if shard_mode not in ("cells", "rays", "sectors"):
+            raise ValueError(f"shard_mode must be 'cells', 'rays' or 'sectors', not {shard_mode!r}")
         self.shard_mode = shard_mode
         self.env = env_mesh or DeviceMesh(environment_trimesh.vertices, environment_trimesh.faces, self.device)
         self._h = _lib._vp()
         g = grid._c()
-        if shard_mode == "rays":
+        if shard_mode == "sectors":  # ray shards by initial azimuth (rt_coverage_create_sectors)
+            self.ray_offset, self.ray_count = 0, rdist.ray_range(self.shard_index, self.shard_count, self.tx_num_rays)[1]
+            check(lib().rt_coverage_create_sectors(self.device, self.env.handle, self.max_bounces, self.tx_num_rays,
+                                                   ctypes.byref(g), self.rx_radius, self.shard_index, self.shard_count,
+                                                   ctypes.byref(self._h)), "rt_coverage_create_sectors")
+        elif shard_mode == "rays":
             self.ray_offset, self.ray_count = rdist.ray_range(self.shard_index, self.shard_count, self.tx_num_rays)
             check(lib().rt_coverage_create_rays(self.device, self.env.handle, self.max_bounces, self.tx_num_rays,
                                                 self.ray_offset, self.ray_count, ctypes.byref(g), self.rx_radius,
@@ -139,6 +144,7 @@ class Coverage:
                                            ctypes.byref(self._h)), "rt_coverage_create")
         self.power = torch.empty(grid.num_cells, dtype=torch.float64, device=f"cuda:{self.device}")
         self.last_candidates = 0
+        self.last_first_wins = 0
         self._rec = None  # ray mode: (keys, sums) record buffers of trace_records
 
     def trace_records(self, tx_pos, tx_power=1):
@@ -149,7 +155,7 @@ class Coverage:
         views of this plan's buffers, overwritten by its next trace_records call."""
         import torch
 
-        if self.shard_mode != "rays":
+        if self.shard_mode not in ("rays", "sectors"):
             raise _lib.RfrtError("trace_records needs shard_mode='rays'")
         tx = np.ascontiguousarray(np.asarray(tx_pos, dtype=np.float64).astype(np.float32))
         counts = np.zeros(self.shard_count, np.int64)
@@ -187,7 +193,7 @@ class Coverage:
         overwritten by its next call."""
         import torch
 
-        if self.shard_mode != "rays":
+        if self.shard_mode not in ("rays", "sectors"):
             raise _lib.RfrtError("trace_rows needs shard_mode='rays'")
         tx = np.ascontiguousarray(np.asarray(tx_pos, dtype=np.float64).astype(np.float32))
         counts = np.zeros(self.shard_count, np.int64)
@@ -218,7 +224,7 @@ class Coverage:
         counts (run_device, "nccl"), so one host wait serves the send and the receive counts."""
         import torch
 
-        if self.shard_mode != "rays":
+        if self.shard_mode not in ("rays", "sectors"):
             raise _lib.RfrtError("trace_rows_async needs shard_mode='rays'")
         tx = np.ascontiguousarray(np.asarray(tx_pos, dtype=np.float64).astype(np.float32))
         dev = f"cuda:{self.device}"
@@ -305,7 +311,7 @@ class Coverage:
             return self._run_device(tx_pos, tx_power, process_group)
 
     def _run_device(self, tx_pos, tx_power, process_group):
-        if self.shard_mode == "rays":
+        if self.shard_mode in ("rays", "sectors"):
             if self.shard_count > 1 and rdist.device_collectives(process_group):
                 # RCCL: the counts' all-to-all is queued behind the trace stage, and one host wait
                 # (trace_rows_finish) returns the send and the receive counts together
@@ -325,6 +331,7 @@ class Coverage:
                                     self.n_bins, phase_step(self.sample_window_s, self.n_bins), ptr(self.power),
                                     stats.ctypes.data, _lib.stream_handle(self.device)), "rt_coverage_run")
         self.last_candidates = int(stats[0])
+        self.last_first_wins = int(stats[1])
         return self.power
 
     def check(self):

@@ -182,6 +182,7 @@ int rt_mesh_create_ex(int device, const float* vertices, int64_t nv, const int32
   }
   rt_mesh* m = new rt_mesh();
   m->device = device;
+  m->gen = rt::next_mesh_gen();
   m->nf = nf;
   // bounding sphere (double), padded so f32 rounding in the pre-test can never reject a hit
   double cen[3], rmax = 0.0, amax = 0.0;
@@ -228,6 +229,7 @@ int rt_mesh_create_ex(int device, const float* vertices, int64_t nv, const int32
 int rt_mesh_destroy(rt_mesh* m) {
   if (!m) return RT_OK;
   rt::DeviceGuard dg(m->device);
+  rt::forget_mesh_schedules(m->gen);
   if (m->perm) (void)hipFree(m->perm);
   if (m->nrm) (void)hipFree(m->nrm);
   if (m->nodes) (void)hipFree(m->nodes);

@@ -31,6 +31,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <atomic>
 #include <vector>
 
 #include "../../include/rfrt.h"
@@ -455,7 +456,8 @@ __global__ __launch_bounds__(256) void k_traj_lds_split(CovParams p) {
   for (int64_t it = 0; it < nit; ++it) {
     const int64_t ir = it * stride + (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> LG);
     const bool valid = ir < p.n;
-    float3 dir = rt::ray_dir(p.ray_offset + (valid ? ir : 0));
+    const int64_t r = valid ? (p.order ? (int64_t)p.order[ir] : ir) : 0;
+    float3 dir = rt::ray_dir(p.ray_offset + r);
     float3 pos = make_float3(p.tx[0], p.tx[1], p.tx[2]);
     int nseg = 0;
     bool alive = valid;
@@ -1278,6 +1280,10 @@ __global__ __launch_bounds__(256) void k_replay_keys(CovParams p, const ReplayIt
 constexpr int kReplayWinItems = 4;
 constexpr int kReplayWin = 1024 * kReplayWinItems;
 constexpr int64_t kReplayWindowMax = 1 << 21;
+// rt_debug_replay_window_max: the parity tests lower the threshold to 0 so that small whole-map
+// lists take the device-wide sort over k_sel_scatter's pre-written order keys (the path of one
+// GPU's K3 / K5 map), e.g. after a regrowth that leaves the list far shorter than the capacity
+std::atomic<int64_t> g_replay_window_max{kReplayWindowMax};
 template <bool USE_BVH>
 __global__ __launch_bounds__(1024) void k_replay_order(CovParams p, const ReplayItem* items, int64_t nl,
                                                        const unsigned long long* nl_dev, int32_t* order) {
@@ -1891,6 +1897,8 @@ struct rt_coverage {
   int64_t n = 0, ray_offset = 0;
   int64_t n_total = 0;     // rays per cell of the whole burst (amplitude tx_power / n_total)
   bool ray_mode = false;   // ray-sharded: candidates for every cell, records grouped by owner
+  bool sectors = false;    // ray-sharded by initial azimuth (rt_coverage_create_sectors): ray_order holds
+                           // the plan's global ray ids (ray_offset 0) in banded order, set at creation
   rt_grid grid{};
   double r_rx = 0.1;
   int shard = 0, nshard = 1;
@@ -2612,6 +2620,11 @@ int free_cands(rt_coverage* c, hipStream_t s) {
   // read freed memory, an illegal address in the N = 4 rehearsal, profiles/r4zb_rehearse_4.log).
   // Growth is rare (first runs), so wait for the plan's stream here (s: the stream of the call that
   // grows; the plan's work is ordered on it).  A fault of earlier work surfaces as this call's error.
+  // Work the plan queued on ANOTHER stream (Python passes torch's current stream, which may differ
+  // between calls on one plan; rt_coverage_create passes the null stream) is not covered by that
+  // wait: what makes the frees below safe for it is hipFree itself, which synchronises the whole
+  // device before it releases memory (HIP's documented hipFree semantics; the stream-ordered
+  // hipFreeAsync is deliberately not used here).  The same holds for alloc_items.
   RT_HIP(hipStreamSynchronize(s));
   for (void* q : {(void*)c->keys, (void*)c->keys_sorted, (void*)c->okeys, (void*)c->okeys_sorted, (void*)c->ukeys,
                   (void*)c->oamps, (void*)c->oamps_sorted, (void*)c->uamps, (void*)c->tcos, (void*)c->tsin, (void*)c->ev,
@@ -2661,11 +2674,19 @@ bool onesweep_fused();
 // the sort is the same): rocPRIM's driver fills the digit histogram, then before every pass the
 // pass's look-back states and its ordered block id -- 1 + 2 x passes fills of ~5 us each (a K5 rank
 // of 8: 9 of its 17 sort launches).  Here one fill zeroes the histogram and every pass's states and
-// block id together, then the histogram, the scan and one launch per pass.  Keys in kout after an
-// odd pass count, else in the key scratch (returned through *in_out: true = kout holds them).
+// block id together, then the histogram, the scan and one launch per pass.  The sorted keys and
+// values always end in kout / vout (the passes alternate through the scratch so that the last one
+// writes them).  The look-back states of all passes are allocated together (radix x blocks x
+// places, i.e. places x rocPRIM's one-pass size), which is what lets one fill serve every pass.
+// rocprim::detail is not a stable interface: this driver is compiled only against the rocPRIM it
+// was written and checked for (ROCm 7.2's 4.2.0, kRocprimDetailVersion); any other version takes
+// rocprim::radix_sort_pairs with the same Onesweep configuration (same results, more fills).
+constexpr int kRocprimDetailVersion = 400200;
 template <class Cfg, typename K, typename V>
 hipError_t onesweep_pairs(void* temp, size_t& storage, const K* kin, K* kout, const V* vin, V* vout, unsigned n,
                           unsigned end_bit, hipStream_t s) {
+#if ROCPRIM_VERSION == 400200
+  static_assert(ROCPRIM_VERSION == kRocprimDetailVersion, "onesweep_pairs: checked against rocPRIM 4.2.0 only");
   namespace rd = rocprim::detail;
   using config = rd::wrapped_radix_sort_onesweep_config<Cfg, K, V>;
   using bid_t = rd::block_id_wrapper<unsigned int, true>;
@@ -2740,6 +2761,10 @@ hipError_t onesweep_pairs(void* temp, size_t& storage, const K* kin, K* kout, co
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
+#else
+  using Only = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, Cfg, 0>;
+  return rocprim::radix_sort_pairs<Only>(temp, storage, kin, kout, vin, vout, n, 0u, end_bit, s);
+#endif
 }
 
 template <typename V>
@@ -3067,6 +3092,7 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
     prof_mark(c, 1, s);
     p.order = nullptr;
   } else {
+    p.order = c->sectors ? c->ray_order : nullptr;  // sector plans: the listed global ids
     prof_mark(c, 0, s);
     if (c->n <= traj_split_max_rays())  // few rays: G lanes per ray
       hipLaunchKernelGGL(k_traj_lds_split<kTrajLdsSplit>,
@@ -3075,6 +3101,7 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
     else
       hipLaunchKernelGGL(k_traj<false>, dim3(grid_rays), dim3(256), lds, s, p);
     prof_mark(c, 1, s);
+    p.order = nullptr;
   }
   RT_HIP(hipGetLastError());
   if (c->profile) {
@@ -3190,7 +3217,7 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
     // vetoes the window order once a rank's list outgrows kReplayWindowMax; the kernels stride over
     // the device count either way, so a stale length costs time, never correctness.
     replayed = c->ray_mode && c->nshard > 1 &&
-               (c->last_list > 0 ? c->last_list : c->cap) <= kReplayWindowMax;
+               (c->last_list > 0 ? c->last_list : c->cap) <= g_replay_window_max.load();
     if (replayed) {
       int rc = launch_replay(c->cap, (const unsigned long long*)c->counters + 2, true,
                              c->last_list > 0 ? c->last_list + c->last_list / 8 : c->cap);
@@ -3224,7 +3251,7 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
   if (ncand > 0) {
     if (nlist > 0) {
       if (!replayed) {
-        int rc = launch_replay(nlist, nullptr, nlist <= kReplayWindowMax, nlist);
+        int rc = launch_replay(nlist, nullptr, nlist <= g_replay_window_max.load(), nlist);
         if (rc) return rc;
       }
       if (c->profile)
@@ -3477,6 +3504,32 @@ int rt_coverage_create_rays(int device, const rt_mesh* env, int max_bounces, int
       hipHostMalloc((void**)&c->hbounds, sizeof(int64_t) * (world + 2), hipHostMallocDefault) != hipSuccess) {
     rt_coverage_destroy(c);
     return rt::hip_fail(hipErrorOutOfMemory, "rt_coverage_create_rays");
+  }
+  *out = c;
+  return RT_OK;
+}
+
+int rt_coverage_create_sectors(int device, const rt_mesh* env, int max_bounces, int64_t n_rays_total,
+                               const rt_grid* grid, double rx_radius, int rank, int world, rt_coverage** out) {
+  if (!out || world < 1 || rank < 0 || rank >= world || n_rays_total < world || n_rays_total > (1 << 24)) {
+    rt::set_error("rt_coverage_create_sectors: invalid arguments (0 <= rank < world <= n_rays_total <= 2^24)");
+    return RT_EINVAL;
+  }
+  const int64_t lo = rank * n_rays_total / world, hi = (rank + 1) * n_rays_total / world;
+  rt_coverage* c = nullptr;
+  int rc = rt_coverage_create_rays(device, env, max_bounces, n_rays_total, 0, hi - lo, grid, rx_radius, rank, world, &c);
+  if (rc) return rc;
+  rt::DeviceGuard dg(device);
+  c->sectors = true;
+  c->ray_offset = 0;
+  if (hipMalloc(&c->ray_order, sizeof(int32_t) * (size_t)(hi - lo)) != hipSuccess) {
+    rt_coverage_destroy(c);
+    return rt::hip_fail(hipErrorOutOfMemory, "rt_coverage_create_sectors");
+  }
+  rc = rt::sector_ray_ids(n_rays_total, lo, hi, c->ray_order, nullptr);
+  if (rc) {
+    rt_coverage_destroy(c);
+    return rc;
   }
   *out = c;
   return RT_OK;
@@ -3866,6 +3919,11 @@ int rt_coverage_check(rt_coverage* c, int64_t* out, void* stream) {
                              "map is wrong)");
     return RT_EHIP;
   }
+  return RT_OK;
+}
+
+int rt_debug_replay_window_max(int64_t n) {
+  g_replay_window_max.store(n < 0 ? kReplayWindowMax : n);
   return RT_OK;
 }
 

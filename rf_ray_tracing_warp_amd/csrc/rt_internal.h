@@ -17,6 +17,7 @@
 //   bvh nodes (optional, large meshes): see rt_bvh.h
 struct rt_mesh {
   int device = 0;
+  uint64_t gen = 0;  // process-unique id (caches key on it, never on the handle's address)
   int64_t nf = 0;
   float4* perm = nullptr;
   float4* nrm = nullptr;
@@ -73,6 +74,9 @@ const int32_t* dir_order_banded(int64_t ray_offset, int64_t n, hipStream_t strea
 // The same order, computed once per (device, ray_offset, n) and kept by the library (the rays of a
 // burst depend on their ids only); ready on `stream` when it returns.  nullptr on failure.
 const int32_t* dir_order_cached(int64_t ray_offset, int64_t n, hipStream_t stream);
+// Sector shards of a burst of n_total rays: positions [lo, hi) of the burst sorted by the azimuth
+// of the initial direction, written to out[hi - lo] as global ids in the banded order (trace.hip)
+int sector_ray_ids(int64_t n_total, int64_t lo, int64_t hi, int32_t* out, hipStream_t stream);
 // Device view of a mesh's BVH for rt::bvh_query
 inline BvhView bvh_view(const rt_mesh* m) {
   return BvhView{(const float4*)m->nodes, (const int2*)m->leaves, (const float4*)m->lcomp, (int)m->nf,
@@ -83,6 +87,10 @@ inline BvhView bvh_view(const rt_mesh* m) {
 int pack_leaf_refs(rt_mesh* m);
 // After pack_leaf_refs: the 4-wide copy of the tree that rt::bvh4_query traverses (bvh_wide.hip)
 int build_wide(rt_mesh* m);
+// A new process-unique mesh id (rt_mesh_create), and the eviction of rt_trace's cached chunk
+// schedules of a mesh that is being destroyed (trace.hip)
+uint64_t next_mesh_gen();
+void forget_mesh_schedules(uint64_t gen);
 // rt_trace's launch (trace.hip).  fused (rt_trace_cir, optional): the brute-force kernels finish
 // the CIR step in their last block (rt_cir.h); *fused_done tells whether this launch did.
 struct TraceCirFused;

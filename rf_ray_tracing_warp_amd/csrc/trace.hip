@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 
 #include "rt_bvh.h"
@@ -731,6 +732,25 @@ __global__ __launch_bounds__(256) void k_dir_keys_banded(int64_t ray_offset, int
   keys[i] = band << 16 | dir_cell(ray_offset + i);
   rows[i] = (int32_t)i;
 }
+// Sector shards (rt::sector_ray_ids): the azimuth of a ray's initial direction, 16 bits over
+// [-pi, pi), and the banded key of a listed global id.  Only which rank traces a ray and in which
+// order depend on them, never a result.
+__global__ __launch_bounds__(256) void k_azimuth_keys(int64_t n, uint32_t* keys, int32_t* ids) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float3 d = rt::ray_dir(i);
+  const float a = (atan2f(d.y, d.x) + 3.14159265f) * (65536.0f / 6.28318531f);
+  keys[i] = (uint32_t)fminf(fmaxf(a, 0.0f), 65535.0f);
+  ids[i] = (int32_t)i;
+}
+__global__ __launch_bounds__(256) void k_ids_keys_banded(const int32_t* ids, int64_t n, uint32_t* keys) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t gid = ids[i];
+  const float3 d = rt::ray_dir(gid);
+  const uint32_t band = (uint32_t)fminf(fabsf(d.z) * (float)rt::kZBands, (float)(rt::kZBands - 1));
+  keys[i] = band << 16 | dir_cell(gid);
+}
 }  // namespace
 
 // ------------------------------------------------------------------ launch (C++ side of rt_trace)
@@ -785,6 +805,42 @@ const int32_t* dir_order_banded(int64_t ray_offset, int64_t n, hipStream_t strea
     return nullptr;
   }
   return r_out;
+}
+
+// The rays of a sector shard of a burst of n_total rays (global ids 0..n_total-1): the burst sorted
+// by the azimuth of the initial direction (stable, so equal keys stay in id order), positions
+// [lo, hi) of that order, then those ids in the banded order the trajectory kernels want.  Written
+// to out[hi - lo]; synchronises `stream` (once per plan).
+int sector_ray_ids(int64_t n_total, int64_t lo, int64_t hi, int32_t* out, hipStream_t stream) {
+  if (n_total <= 0 || lo < 0 || hi > n_total || lo >= hi || n_total > INT32_MAX) {
+    set_error("sector_ray_ids: invalid range");
+    return RT_EINVAL;
+  }
+  const int64_t m = hi - lo;
+  size_t b1 = 0, b2 = 0;
+  RT_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, b1, (uint32_t*)nullptr, (uint32_t*)nullptr, (int32_t*)nullptr,
+                                            (int32_t*)nullptr, (int)n_total, 0, 16, stream));
+  RT_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, b2, (uint32_t*)nullptr, (uint32_t*)nullptr, (int32_t*)nullptr,
+                                            (int32_t*)nullptr, (int)m, 0, 16 + kZBandBits, stream));
+  const size_t kb = ((size_t)n_total * 4 + 255) / 256 * 256;
+  char* ws = nullptr;
+  RT_HIP(hipMalloc(&ws, 4 * kb + std::max(b1, b2)));
+  uint32_t* k_in = (uint32_t*)ws;
+  uint32_t* k_out = (uint32_t*)(ws + kb);
+  int32_t* i_in = (int32_t*)(ws + 2 * kb);
+  int32_t* i_out = (int32_t*)(ws + 3 * kb);
+  void* tmp = ws + 4 * kb;
+  hipError_t e = hipSuccess;
+  hipLaunchKernelGGL(k_azimuth_keys, dim3((unsigned)((n_total + 255) / 256)), dim3(256), 0, stream, n_total, k_in, i_in);
+  e = hipcub::DeviceRadixSort::SortPairs(tmp, b1, k_in, k_out, i_in, i_out, (int)n_total, 0, 16, stream);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_ids_keys_banded, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, stream, i_out + lo, m, k_in);
+    e = hipcub::DeviceRadixSort::SortPairs(tmp, b2, k_in, k_out, i_out + lo, out, (int)m, 0, 16 + kZBandBits, stream);
+  }
+  if (e == hipSuccess) e = hipGetLastError();
+  if (e == hipSuccess) e = hipStreamSynchronize(stream);
+  (void)hipFree(ws);
+  return e == hipSuccess ? RT_OK : hip_fail(e, "sector_ray_ids");
 }
 
 // The banded order of a burst depends only on (ray_offset, n): every call traces the same rays
@@ -905,16 +961,24 @@ __global__ __launch_bounds__(1024) void k_chunk_schedule(const uint32_t* cost, i
 }
 
 namespace {
+// One cached schedule.  An entry is published (added to the table) when its cost-recording launch
+// is set up, but its `sched` buffer is only meaningful once k_chunk_schedule has run and `ready`
+// has been recorded after it: `valid` says so, and is set under the mutex by finish_chunk_schedule.
+// Lookups that find an entry that is not valid yet (another thread's launch in flight) trace in
+// chunk order; a launch that fails between the two steps drops its entry (SchedClaim).
+// Keys: the meshes' process-unique ids (rt_mesh::gen; a destroyed mesh's entries are evicted by
+// rt_mesh_destroy), never their addresses, which a later mesh may reuse.
 struct SchedEntry {
   int device = -1, B = 0;
   int64_t ray_offset = 0, n = 0;
-  const rt_mesh *env = nullptr, *rx = nullptr;
+  uint64_t env_gen = 0, rx_gen = 0;
   float tx[3] = {0, 0, 0};
   int32_t* sched = nullptr;
   uint32_t* cost = nullptr;
   hipEvent_t ready = nullptr;  // recorded after k_chunk_schedule
   hipStream_t made_on = nullptr;
   uint64_t used = 0;
+  bool valid = false;
 };
 constexpr int kSchedCache = 8;
 SchedEntry g_sched[kSchedCache];
@@ -929,6 +993,18 @@ bool chunk_schedule_on() {  // RFRT_K2_LPT=0: chunks in order (A/B checks)
   return v;
 }
 
+// caller holds g_sched_mu; hipFree waits for the device, so no launch still reads the buffers
+void drop_entry(SchedEntry& e) {
+  int cur = -1;
+  (void)hipGetDevice(&cur);
+  if (e.device >= 0 && e.device != cur) (void)hipSetDevice(e.device);
+  if (e.sched) (void)hipFree(e.sched);
+  if (e.cost) (void)hipFree(e.cost);
+  if (e.ready) (void)hipEventDestroy(e.ready);
+  if (cur >= 0 && e.device != cur) (void)hipSetDevice(cur);
+  e = SchedEntry{};
+}
+
 // Sets a.sched (schedule ready) or a.cost (this launch records the costs; *profile then names the
 // entry whose schedule finish_chunk_schedule computes after the launch).  Errors leave both null.
 void chunk_schedule(TraceArgs& a, int dev, const rt_mesh* env, const rt_mesh* rx, const float tx[3], int B,
@@ -936,10 +1012,12 @@ void chunk_schedule(TraceArgs& a, int dev, const rt_mesh* env, const rt_mesh* rx
   *profile = nullptr;
   const int64_t nch = (n + 255) / 256;
   if (!chunk_schedule_on() || nch > kSchedMaxChunks) return;
+  const uint64_t env_gen = env->gen, rx_gen = rx ? rx->gen : 0;
   std::lock_guard<std::mutex> lock(g_sched_mu);
   for (SchedEntry& e : g_sched)
-    if (e.sched && e.device == dev && e.B == B && e.ray_offset == ray_offset && e.n == n && e.env == env &&
-        e.rx == rx && e.tx[0] == tx[0] && e.tx[1] == tx[1] && e.tx[2] == tx[2]) {
+    if (e.sched && e.device == dev && e.B == B && e.ray_offset == ray_offset && e.n == n && e.env_gen == env_gen &&
+        e.rx_gen == rx_gen && e.tx[0] == tx[0] && e.tx[1] == tx[1] && e.tx[2] == tx[2]) {
+      if (!e.valid) return;  // being computed by another launch: this one runs in chunk order
       e.used = ++g_sched_clock;
       if (e.made_on != stream && hipStreamWaitEvent(stream, e.ready, 0) != hipSuccess) return;
       a.sched = e.sched;
@@ -953,31 +1031,24 @@ void chunk_schedule(TraceArgs& a, int dev, const rt_mesh* env, const rt_mesh* rx
     } else if (e.used < slot->used) {
       slot = &e;
     }
-  if (slot->sched) {  // evict (hipFree waits for the device)
-    int cur = dev;
-    if (slot->device != dev) (void)hipSetDevice(slot->device);
-    (void)hipFree(slot->sched);
-    (void)hipFree(slot->cost);
-    if (slot->ready) (void)hipEventDestroy(slot->ready);
-    if (slot->device != cur) (void)hipSetDevice(cur);
-    *slot = SchedEntry{};
+  if (slot->sched) {
+    if (!slot->valid) return;  // every entry in flight (8 threads at once): no schedule this time
+    drop_entry(*slot);
   }
   SchedEntry e;
   e.device = dev;
   e.B = B;
   e.ray_offset = ray_offset;
   e.n = n;
-  e.env = env;
-  e.rx = rx;
+  e.env_gen = env_gen;
+  e.rx_gen = rx_gen;
   for (int k = 0; k < 3; ++k) e.tx[k] = tx[k];
   hipError_t err = hipMalloc(&e.sched, sizeof(int32_t) * (size_t)nch);
   if (err == hipSuccess) err = hipMalloc(&e.cost, sizeof(uint32_t) * (size_t)nch);
   if (err == hipSuccess) err = hipEventCreateWithFlags(&e.ready, hipEventDisableTiming);
   if (err == hipSuccess) err = hipMemsetAsync(e.cost, 0, sizeof(uint32_t) * (size_t)nch, stream);
   if (err != hipSuccess) {  // no schedule: chunks in order
-    if (e.sched) (void)hipFree(e.sched);
-    if (e.cost) (void)hipFree(e.cost);
-    if (e.ready) (void)hipEventDestroy(e.ready);
+    drop_entry(e);
     return;
   }
   e.made_on = stream;
@@ -987,13 +1058,40 @@ void chunk_schedule(TraceArgs& a, int dev, const rt_mesh* env, const rt_mesh* rx
   *profile = slot;
 }
 
-int finish_chunk_schedule(SchedEntry* e, int64_t n, hipStream_t stream) {
-  hipLaunchKernelGGL(k_chunk_schedule, dim3(1), dim3(1024), 0, stream, e->cost, (n + 255) / 256, e->sched);
-  hipError_t err = hipGetLastError();
-  if (err == hipSuccess) err = hipEventRecord(e->ready, stream);
-  return err == hipSuccess ? 0 : hip_fail(err, "chunk schedule");
-}
+// The entry a cost-recording launch claimed: finish() computes its schedule and publishes it as
+// valid; any other way out of launch_trace (an error return between the two) drops it.
+struct SchedClaim {
+  SchedEntry* e = nullptr;
+  int finish(int64_t n, hipStream_t stream) {
+    if (!e) return 0;
+    hipLaunchKernelGGL(k_chunk_schedule, dim3(1), dim3(1024), 0, stream, e->cost, (n + 255) / 256, e->sched);
+    hipError_t err = hipGetLastError();
+    if (err == hipSuccess) err = hipEventRecord(e->ready, stream);
+    std::lock_guard<std::mutex> lock(g_sched_mu);
+    if (err == hipSuccess) e->valid = true;
+    else drop_entry(*e);
+    e = nullptr;
+    return err == hipSuccess ? 0 : hip_fail(err, "chunk schedule");
+  }
+  ~SchedClaim() {
+    if (!e) return;
+    std::lock_guard<std::mutex> lock(g_sched_mu);
+    drop_entry(*e);
+  }
+};
 }  // namespace
+
+uint64_t next_mesh_gen() {
+  static std::atomic<uint64_t> g{0};
+  return ++g;
+}
+
+void forget_mesh_schedules(uint64_t gen) {
+  std::lock_guard<std::mutex> lock(g_sched_mu);
+  for (SchedEntry& e : g_sched)
+    // entries still in flight are left to finish: their ids never match again, LRU evicts them
+    if (e.sched && e.valid && (e.env_gen == gen || e.rx_gen == gen)) drop_entry(e);
+}
 
 int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B, int64_t ray_offset, int64_t n,
                  float* traced, float* received, uint32_t* mask, int32_t* hit_kind, int32_t* hit_face,
@@ -1080,14 +1178,14 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
     if (rc) return rc;
   }
   const bool sort = (bvh || B <= 8) && n >= kSortMinRays && n <= INT32_MAX;
-  SchedEntry* sched_profile = nullptr;
+  SchedClaim sched_claim;
   if (sort) {
     trace_mark(0, stream);
     a.order = dir_order_cached(ray_offset, n, stream);
     if (!a.order) return -1;
     if (B <= 8) {
       int dev = 0;
-      if (hipGetDevice(&dev) == hipSuccess) chunk_schedule(a, dev, env, rx, tx, B, ray_offset, n, stream, &sched_profile);
+      if (hipGetDevice(&dev) == hipSuccess) chunk_schedule(a, dev, env, rx, tx, B, ray_offset, n, stream, &sched_claim.e);
     }
     trace_mark(1, stream);
   }
@@ -1135,8 +1233,8 @@ int launch_trace(const rt_mesh* env, const float tx[3], const rt_mesh* rx, int B
       break;
   }
 #undef RT_LAUNCH
-  if (sched_profile) {
-    const int rc = finish_chunk_schedule(sched_profile, n, stream);
+  {
+    const int rc = sched_claim.finish(n, stream);
     if (rc) return rc;
   }
   if (a.fused) hipLaunchKernelGGL(k_trace_cir_tail, dim3(1), dim3(512), 0, stream, a.fz, n, received, B + 1);

@@ -1,5 +1,6 @@
 """The stated collective cost model of the rank projection (tools/cov_profile.py: collective_model):
-an all-to-all of 32-B rows (a rank's own share stays local) plus an all-gather of the owners' f64
+an all-to-all of the 32-B rows that leave their rank (measured per rank: the records a rank keeps for
+its own cells never cross xGMI) plus an all-gather of the owners' f64
 x columns, over a stated xGMI rate, with a fixed latency per collective (three of them)."""
 import importlib.util
 import os
@@ -22,7 +23,7 @@ def test_collective_model_arithmetic(monkeypatch):
     monkeypatch.setenv("XGMI_GBS", "300")
     monkeypatch.setenv("COLL_US", "25")
     m = _model()([200_000, 180_000], [150_000, 210_000], _Grid(), 8)
-    a2a = 210_000 * 32 * 7 / 8  # the largest sender or receiver, its own eighth local
+    a2a = 210_000 * 32  # the largest remote sender or receiver
     ag = (256 + 7) // 8 * 256 * 8 * 7  # the other owners' columns, f64
     assert m["a2a_bytes_max"] == int(a2a)
     assert m["allgather_bytes_in"] == ag
@@ -32,5 +33,5 @@ def test_collective_model_arithmetic(monkeypatch):
 
 
 def test_collective_model_one_rank_moves_nothing():
-    m = _model()([1000], [1000], _Grid(), 1)
+    m = _model()([0], [0], _Grid(), 1)
     assert m["a2a_bytes_max"] == 0 and m["allgather_bytes_in"] == 0

@@ -143,10 +143,11 @@ def test_coverage_on_bvh_terrain():
     cov.close()
 
 
-def _ray_sharded_rows(env, grid, tx, B, N, S, win=100e-9, env_mesh=None):
+def _ray_sharded_rows(env, grid, tx, B, N, S, win=100e-9, env_mesh=None, mode="rays"):
     """_ray_sharded through the packed path run() takes: trace_rows -> each owner's segments of
-    (key, sum) rows in source-rank order -> power_from_rows."""
-    plans = [Coverage(env, 2.998e8, 100e9, win, B, N, grid, shard_index=r, shard_count=S, shard_mode="rays",
+    (key, sum) rows in source-rank order -> power_from_rows.  mode "sectors": the ranks' rays are
+    wedges of initial azimuth (rt_coverage_create_sectors) instead of ray-id ranges."""
+    plans = [Coverage(env, 2.998e8, 100e9, win, B, N, grid, shard_index=r, shard_count=S, shard_mode=mode,
                       env_mesh=env_mesh) for r in range(S)]
     sent = []
     for p in plans:
@@ -214,6 +215,42 @@ def test_coverage_ray_sharded_equals_whole(room, S):
     np.testing.assert_array_equal(c[o], wc)
     np.testing.assert_array_equal(b[o], wb)
     np.testing.assert_allclose(a[o], wa, rtol=1e-12)
+
+
+@pytest.mark.parametrize("S", [2, 3, 8])
+def test_coverage_sector_sharded_equals_whole(room, S):
+    """Sector shards (each rank traces the rays of one wedge of initial azimuth, rays chosen by
+    direction rather than by id) give the single-GPU map and sparse impulse responses bit for bit:
+    any partition of a cell's rays sums to the same fixed-point integers."""
+    grid, tx, B, N = CoverageGrid(8.0, -2.5, 4.6, 0.37, 0.41, 0.4, 13, 12, 2), (10, 0, 5), 3, 60_000
+    cov = Coverage(room, 2.998e8, 100e9, 100e-9, B, N, grid)
+    whole = cov.run_device(tx).cpu().numpy()
+    wc, wb, wa = cov.impulse_responses()
+    cov.close()
+    total, irs = _ray_sharded_rows(room, grid, tx, B, N, S, mode="sectors")
+    assert (~np.isnan(whole)).sum() >= 20
+    np.testing.assert_array_equal(total, whole)
+    c = np.concatenate([x[0] for x in irs])
+    b = np.concatenate([x[1] for x in irs])
+    a = np.concatenate([x[2] for x in irs])
+    o = np.lexsort((b, c))
+    np.testing.assert_array_equal(c[o], wc)
+    np.testing.assert_array_equal(b[o], wb)
+    assert a[o].tobytes() == wa.tobytes()
+
+
+def test_coverage_sector_sharded_bvh_terrain():
+    from rf_ray_tracing_warp_amd._lib import DeviceMesh
+    from rf_ray_tracing_warp_amd.mesh import synthetic_terrain
+    t = synthetic_terrain(256, 50.0)
+    env = DeviceMesh(t.vertices, t.faces, 0)
+    grid, tx, B, N = CoverageGrid(4.0, -6.0, 2.0, 0.9, 0.8, 1.0, 16, 16, 1), (10.0, 0.0, 4.5), 3, 40_000
+    cov = Coverage(t, 2.998e8, 100e9, 200e-9, B, N, grid, env_mesh=env)
+    whole = cov.run_device(tx).cpu().numpy()
+    cov.close()
+    total, _ = _ray_sharded_rows(t, grid, tx, B, N, 8, win=200e-9, env_mesh=env, mode="sectors")
+    assert (~np.isnan(whole)).sum() >= 10
+    np.testing.assert_array_equal(total, whole)
 
 
 @pytest.mark.parametrize("S", [1, 3, 8])
@@ -558,3 +595,48 @@ def test_exchange_counts_async_over_rccl(room):
         assert host.is_pinned() and host.tolist() == [12345]
     finally:
         dist.destroy_process_group()
+
+
+def test_whole_map_sort_after_regrowth_short_list(room):
+    """The fault class of round 5 (r5y): k_sel_scatter writes the whole-map replay-order keys at the
+    plan's capacity-based workspace layout (rord_key_bytes(cap)), and the replay-order sort must take
+    its key / value pointers from the same layout -- a list far shorter than the capacity, after a
+    regrowth, read keys from the wrong place (an illegal address).  Here every whole-map list takes
+    the device-wide sort over k_sel_scatter's keys (rt_debug_replay_window_max(0); by default only
+    one GPU's K3 / K5 maps do).  Run 1: a dense 3-layer grid around the TX overflows the plan's
+    initial 2^20 candidates and regrows it.  Run 2, same plan: the TX far away, a few thousand first
+    wins against a capacity of millions.  Both maps against the oracle's per-cell loop on sampled
+    cells (coverage bar: identical bins, 1e-5 norm-wise impulse responses, 1e-9 power vs the
+    rounded-once arccos)."""
+    L = lib()
+    grid = CoverageGrid(9.2, -0.8, 4.95, 0.05, 0.05, 0.05, 32, 32, 3)
+    B, N = 3, 100_000
+    E = orc.Mesh(room.vertices, room.faces)
+    cen = grid.centers().reshape(-1, 3)
+    check(L.rt_debug_replay_window_max(0))
+    try:
+        cov = Coverage(room, 2.998e8, 100e9, 100e-9, B, N, grid)
+        for run, tx in enumerate([(10.0, 0.0, 5.0), (-12.0, 9.0, 11.0)]):
+            power = cov.run(tx, 1).reshape(-1)
+            cells, bins, amps = cov.impulse_responses()
+            if run == 0:
+                assert cov.last_candidates > (1 << 20), cov.last_candidates  # the first run regrew the plan
+                cap = cov.last_candidates
+            else:
+                assert 0 < cov.last_first_wins < cap // 20, (cov.last_first_wins, cap)  # nl << cap
+            rng = np.random.default_rng(run)
+            recv = np.unique(cells)
+            picks = np.union1d(rng.choice(recv, min(24, len(recv)), replace=False),
+                               rng.choice(grid.num_cells, 6, replace=False))
+            for c in picks:
+                ref = orc.coverage_cell(E, tx, cen[c], B, N)
+                sel = cells == c
+                rb = np.nonzero(ref["ir"])[0]
+                np.testing.assert_array_equal(bins[sel], rb, err_msg=f"run {run} cell {c}")
+                assert np.isnan(power[c]) == np.isnan(ref["power"]), f"run {run} cell {c}"
+                if len(rb):
+                    assert np.abs(amps[sel] - ref["ir"][rb]).max() <= 1e-5 * np.abs(ref["ir"]).max()
+                    np.testing.assert_allclose(power[c], ref["power_cr"], rtol=1e-9, err_msg=f"run {run} cell {c}")
+        cov.close()
+    finally:
+        check(L.rt_debug_replay_window_max(-1))

@@ -33,8 +33,8 @@ def main():
             grid, tx, win, B = CoverageGrid.square(1024, 50.0, 2.0), (10.0, 0.0, 4.5), 200e-9, 3
         env = DeviceMesh(m.vertices, m.faces, 0)
         for S in shards:
-            if mode == "rays" and S > 1:
-                rays_case(case, m, grid, tx, win, B, env, S, reps)
+            if mode in ("rays", "sectors") and S > 1:
+                rays_case(case, m, grid, tx, win, B, env, S, reps, mode)
                 continue
             per_rank = []
             for r in range(S):  # cell shards: every rank's plan in turn (the slowest defines the map)
@@ -53,11 +53,11 @@ def main():
         env.close()
 
 
-def rays_case(case, m, grid, tx, win, B, env, S, reps):
+def rays_case(case, m, grid, tx, win, B, env, S, reps, mode="rays"):
     import torch
     from rf_ray_tracing_warp_amd.coverage import Coverage
     plans = [Coverage(m, 2.998e8, 100e9, win, B, 1_000_000, grid, 0.1, device=0, shard_index=r, shard_count=S,
-                      env_mesh=env, shard_mode="rays") for r in range(S)]
+                      env_mesh=env, shard_mode=mode) for r in range(S)]
 
     def timed(fn):
         torch.cuda.synchronize()
@@ -102,15 +102,19 @@ def rays_case(case, m, grid, tx, win, B, env, S, reps):
             t_own.append(dt)
         per_rank = [a + b for a, b in zip(t_trace, t_own)]
         if best is None or max(per_rank) < max(best[0]):
-            best = (per_rank, t_trace, t_own, nrec, [sum(x[-1]) for x in sent])
-    per_rank, t_trace, t_own, nrec, nsent = best
-    coll = collective_model(nsent, nrec, grid, S)
-    print(json.dumps({"case": case, "mode": "rays", "shards": S, "ms_per_map_max_rank": max(per_rank) * 1e3,
+            # records that leave their rank (a rank's own share stays local)
+            remote_out = [sum(x[-1]) - x[-1][r] for r, x in enumerate(sent)]
+            remote_in = [sum(x[-1][d] for r, x in enumerate(sent) if r != d) for d in range(S)]
+            best = (per_rank, t_trace, t_own, nrec, [sum(x[-1]) for x in sent], remote_out, remote_in)
+    per_rank, t_trace, t_own, nrec, nsent, rout, rin = best
+    coll = collective_model(rout, rin, grid, S)
+    print(json.dumps({"case": case, "mode": mode, "shards": S, "ms_per_map_max_rank": max(per_rank) * 1e3,
                       "ms_per_map_with_collectives": max(t_trace) * 1e3 + coll["ms_total"] + max(t_own) * 1e3,
                       "collectives_model": coll,
                       "ms_trace_stage": [round(x * 1e3, 3) for x in t_trace],
                       "ms_owner_stage": [round(x * 1e3, 3) for x in t_own],
-                      "records_sent": nsent, "records_received": nrec}), flush=True)
+                      "records_sent": nsent, "records_received": nrec, "records_remote_out": rout,
+                      "records_remote_in": rin}), flush=True)
     for p in plans:
         p.close()
 
@@ -123,12 +127,12 @@ def rays_case(case, m, grid, tx, win, B, env, S, reps):
 # collective (launch + RCCL protocol + the host read of the counts).  The trace stage of every rank
 # ends before the exchange, and the owner stage starts after it, so the map time is
 # max(trace) + collectives + max(owner) + the all-gather.
-def collective_model(nsent, nrec, grid, S):
+def collective_model(remote_out, remote_in, grid, S):
     gbs = float(os.environ.get("XGMI_GBS", "300"))
     lat = float(os.environ.get("COLL_US", "25"))
     row = 32
-    a2a_out = max(n * row * (S - 1) / S for n in nsent)  # a rank's own share stays local
-    a2a_in = max(n * row * (S - 1) / S for n in nrec)
+    a2a_out = max(n * row for n in remote_out)  # the rows that cross xGMI (a rank's own stay local)
+    a2a_in = max(n * row for n in remote_in)
     a2a = max(a2a_out, a2a_in)
     owned = (grid.nx + S - 1) // S * grid.ny * grid.nz * 8
     ag_in = owned * (S - 1)  # every rank receives the other owners' columns
