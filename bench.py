@@ -75,6 +75,11 @@ def parse():
     ap.add_argument("--coverage-runs", type=int, default=3)
     ap.add_argument("--coverage-shard", choices=("rays", "cells"), default="rays",
                     help="N>1 coverage decomposition: ray shards + record all-to-all, or x-column cell shards")
+    ap.add_argument("--no-validate", action="store_true",
+                    help="N>1: skip rank 0's one-GPU reference map (the N-rank map is compared with it bit for bit)")
+    ap.add_argument("--debug-unordered-rows", action="store_true",
+                    help="test hook: ray-sharded coverage (also at N=1), with two received rows of each owner's first "
+                         "segment swapped -- the owner stage must flag it and the bench exit non-zero")
     ap.add_argument("--no-k4", action="store_true", help="skip the terrain (apollo stand-in) legs K4/K5")
     ap.add_argument("--k4-rays", type=int, default=2_097_152, help="rays per GPU (K4: 16.7M over 8 GPUs)")
     ap.add_argument("--k5-grid", type=int, default=1024)
@@ -105,7 +110,15 @@ def host_info():
     aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
     # the box gives one GPU's job a share of the host (OMP_NUM_THREADS, 16 there); use all of it
     share = int(os.environ.get("OMP_NUM_THREADS") or aff or 1)
-    return {"lscpu_model": model, "os_cpu_count": os.cpu_count(), "affinity_cpus": aff, "threads_used": share}
+    quota = None  # the cgroup's CPU bandwidth limit in CPUs (cpu.max "quota period"), if any
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+            quota = None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    return {"lscpu_model": model, "os_cpu_count": os.cpu_count(), "affinity_cpus": aff, "threads_used": share,
+            "cgroup_cpu_quota": quota}
 
 
 def native_oracle():
@@ -153,7 +166,8 @@ def cpu_baseline_k2(args, B, tx, rx, info, build):
     E, R = orc.Mesh(env.vertices, env.faces), orc.Mesh(rxm.vertices, rxm.faces)
     out = {}
     for label, threads, rays in (("all", info["threads_used"], args.cpu_rays),
-                                 ("1thread", 1, max(args.cpu_rays // 16, 50_000))):
+                                 ("1thread", 1, max(args.cpu_rays // 16, 50_000)),
+                                 ("all_cores", info["affinity_cpus"], args.cpu_rays)):
         def run():
             o = orc.trace(E, R, tx, B, 0, rays, want_traced=True, nthreads=threads)
             orc.cir_from_paths(orc.clean_paths(o["received"], o["mask"]), 1, rays, 2.998e8, 100e9, 100e-9)
@@ -197,7 +211,8 @@ def cpu_baseline_k3(args, info):
     ir = np.zeros(10000)
     ir[[3000, 5000, 7000]] = 1e-6
     conv, _ = _median_runs(lambda: orc.signal_power(ir, 100e-9), 5)
-    out = {"all": leg(len(cells), info["threads_used"]), "1thread": leg(args.cpu_cells_1thread, 1)}
+    out = {"all": leg(len(cells), info["threads_used"]), "1thread": leg(args.cpu_cells_1thread, 1),
+           "all_cores": leg(len(cells), info["affinity_cpus"])}
     out["all"]["np_convolve_power_ms_per_cell"] = conv * 1e3
     return out
 
@@ -214,7 +229,7 @@ def cpu_baseline_k1(args, info, build):
     E, R = orc.Mesh(env.vertices, env.faces), orc.Mesh(rxm.vertices, rxm.faces)
     n, B, reps = 10_000, 1, 50
     out = {}
-    for label, threads in (("all", info["threads_used"]), ("1thread", 1)):
+    for label, threads in (("all", info["threads_used"]), ("1thread", 1), ("all_cores", info["affinity_cpus"])):
         def run():
             for _ in range(reps):
                 o = orc.trace(E, R, (1.0, 0.0, 1.0), B, 0, n, want_traced=True, nthreads=threads)
@@ -241,7 +256,8 @@ def cpu_baseline_k4(args, terr, info, build):
     R = orc.Mesh(rxm.vertices, rxm.faces)
     B = 5
     out = {}
-    for label, threads, rays in (("all", info["threads_used"], 1_000_000), ("1thread", 1, 50_000)):
+    for label, threads, rays in (("all", info["threads_used"], 1_000_000), ("1thread", 1, 50_000),
+                                 ("all_cores", info["affinity_cpus"], 1_000_000)):
         def run():
             o = orc.trace(E, R, (10.0, 0.0, 4.5), B, 0, rays, want_traced=True, nthreads=threads)
             orc.cir_from_paths(orc.clean_paths(o["received"], o["mask"]), 1, rays, 2.998e8, 100e9, 200e-9)
@@ -282,7 +298,8 @@ def cpu_baseline_k5(args, terr, info):
                           f"loop body: {N}-ray trace over the terrain stand-in with its icosphere (oracle BVH path) + "
                           f"host CIR + np.convolve power; median of {len(ts)} runs after 1 warm-up "
                           f"({', '.join(f'{t:.2f}' for t in ts)} s)", "host": info}
-    return {"all": leg(len(ids), info["threads_used"]), "1thread": leg(args.cpu_cells_1thread, 1)}
+    return {"all": leg(len(ids), info["threads_used"]), "1thread": leg(args.cpu_cells_1thread, 1),
+            "all_cores": leg(len(ids), info["affinity_cpus"])}
 
 
 # ------------------------------------------------------------------ coverage legs
@@ -318,8 +335,35 @@ def _roofline(kernel, ms, work, B, note, default_size=True):
             "ray_bounces_per_s": work / (ms * 1e-3), "note": note}
 
 
+def _swap_first_rows(cov):
+    """--debug-unordered-rows: break the owner stage's precondition (each received segment strictly
+    ascending by key) by swapping two rows of the first segment that has two."""
+    orig = cov.power_from_rows
+
+    def broken(rows, counts=None):
+        if counts is not None:
+            off = 0
+            for c in counts:
+                if c >= 2:
+                    rows = rows.clone()
+                    rows[[off, off + 1]] = rows[[off + 1, off]]
+                    break
+                off += c
+        return orig(rows, counts)
+    cov.power_from_rows = broken
+
+
+def coverage_mode(args, world):
+    if args.debug_unordered_rows:
+        return "rays"
+    return args.coverage_shard if world > 1 else "cells"
+
+
 def run_coverage(cov, tx, runs, world, dist, local):
-    """Time `runs` maps (profiling off), then one profiled map for the stage breakdown."""
+    """Time `runs` maps (profiling off), then one profiled map for the stage breakdown.  After the
+    timed maps (outside the timed region) the plan's device-side error report is checked
+    (Coverage.check: a look-back wait that gave up or an owner-stage segment out of key order means
+    that map is wrong): RfrtError, and the bench exits non-zero."""
     import torch
 
     from rf_ray_tracing_warp_amd.dist import gather_power_map
@@ -341,6 +385,7 @@ def run_coverage(cov, tx, runs, world, dist, local):
     if world > 1:
         dist.barrier()
     dt = (time.perf_counter() - t0) / runs
+    cov.check()  # raises on a device-flagged error of the timed maps (outside the timed region)
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -350,10 +395,27 @@ def run_coverage(cov, tx, runs, world, dist, local):
     one()
     prof = cov.last_profile()
     cov.profile(False)
+    cov.check()
     return dt, pm, prof
 
 
-def coverage_block(name, cov, grid, dt, pm, prof, B, workload, world, mode, bvh, default_size):
+def one_gpu_reference(make_plan, tx, pm, rank, world):
+    """N>1 validation (outside the timed region): rank 0 computes the same map with a one-GPU plan
+    and compares it with the gathered N-rank map bit for bit (the per-bin sums are exact fixed point,
+    so the decomposition must not move a single bit).  Returns (equal, sha256 of the N-rank map,
+    sha256 of the one-GPU map) on rank 0, None elsewhere or at N=1."""
+    import hashlib
+    if world == 1 or rank != 0:
+        return None
+    ref = make_plan()
+    r = ref.run_device(tx, 1).cpu().numpy()
+    ref.check()
+    ref.close()
+    a, b = hashlib.sha256(pm.tobytes()).hexdigest(), hashlib.sha256(r.tobytes()).hexdigest()
+    return a == b, a, b
+
+
+def coverage_block(name, cov, grid, dt, pm, prof, B, val, workload, world, mode, bvh, default_size):
     t = "true" if bvh else "false"
     traj = _roofline(f"k_traj<{t}>", prof["traj_ms"], prof["traced_ray_bounces"], B,
                      "trajectory pass, D4 bytes over the actually traced ray-bounces (rays x segments)",
@@ -371,6 +433,9 @@ def coverage_block(name, cov, grid, dt, pm, prof, B, workload, world, mode, bvh,
             "stage_ms": {k: prof[k] for k in ("traj_ms", "candidates_ms", "win_ms", "replay_ms", "reduce_power_ms",
                                                 "total_ms")},
             "roofline": traj, "roofline_replay": rep,
+            # N>1: the gathered map against rank 0's one-GPU map, bit for bit (null at N=1)
+            "map_equals_one_gpu": None if val is None else bool(val[0]),
+            "map_sha256": None if val is None else val[1],
             "algorithm": "exact shared-trajectory (csrc/coverage.hip)", "name": name}
 
 
@@ -379,12 +444,17 @@ def coverage_leg(args, env_m, env, local, rank, world, dist):
     from rf_ray_tracing_warp_amd.coverage import Coverage, CoverageGrid
 
     grid = CoverageGrid.square(args.coverage_grid, 15.0, 5.0)
-    mode = args.coverage_shard if world > 1 else "cells"
+    mode = coverage_mode(args, world)
     cov = Coverage(env_m, 2.998e8, 100e9, 100e-9, args.bounces, args.coverage_rays, grid, 0.1, device=local,
                    shard_index=rank, shard_count=world, env_mesh=env, shard_mode=mode)
+    if args.debug_unordered_rows:
+        _swap_first_rows(cov)
     dt, pm, prof = run_coverage(cov, (10.0, 0.0, 5.0), args.coverage_runs, world, dist, local)
     cov.close()
-    return coverage_block("K3", cov, grid, dt, pm, prof, args.bounces,
+    val = None if args.no_validate else one_gpu_reference(
+        lambda: Coverage(env_m, 2.998e8, 100e9, 100e-9, args.bounces, args.coverage_rays, grid, 0.1, device=local,
+                         env_mesh=env), (10.0, 0.0, 5.0), pm, rank, world)
+    return coverage_block("K3", cov, grid, dt, pm, prof, args.bounces, val,
                           f"K3: room.stl, {grid.nx}x{grid.ny} receivers at z=5 (centres -15+(i+1/2)*30/{grid.nx}), "
                           f"tx (10,0,5), {args.coverage_rays} rays per cell, {args.bounces} bounces, 10000 bins, "
                           f"signal power per cell", world, mode, False,
@@ -522,12 +592,17 @@ def terrain_legs(args, local, rank, world, dist):
         rx.close()
     if "k5" in args.legs:
         grid = CoverageGrid.square(args.k5_grid, 50.0, 2.0)
-        mode = args.coverage_shard if world > 1 else "cells"
+        mode = coverage_mode(args, world)
         cov = Coverage(terr, 2.998e8, 100e9, 200e-9, 3, args.k5_rays, grid, 0.1, device=local, shard_index=rank,
                        shard_count=world, env_mesh=env, shard_mode=mode)
+        if args.debug_unordered_rows:
+            _swap_first_rows(cov)
         dt, pm, prof = run_coverage(cov, (10.0, 0.0, 4.5), args.k5_runs, world, dist, local)
         cov.close()
-        k5 = coverage_block("K5", cov, grid, dt, pm, prof, 3,
+        val = None if args.no_validate else one_gpu_reference(
+            lambda: Coverage(terr, 2.998e8, 100e9, 200e-9, 3, args.k5_rays, grid, 0.1, device=local, env_mesh=env),
+            (10.0, 0.0, 4.5), pm, rank, world)
+        k5 = coverage_block("K5", cov, grid, dt, pm, prof, 3, val,
                             f"K5 on the terrain stand-in: {grid.nx}x{grid.ny} receivers at z=2 over +-50 m, "
                             f"tx (10,0,4.5), {args.k5_rays} rays per cell, 3 bounces, 20000 bins", world, mode,
                             True, args.k5_grid == 1024 and args.k5_rays == 1_000_000)
@@ -537,9 +612,11 @@ def terrain_legs(args, local, rank, world, dist):
         if k4 is not None:
             cb = cpu_baseline_k4(args, terr, info, build)
             k4["cpu_baseline"], k4["cpu_baseline_1thread"] = cb["all"], cb["1thread"]
+            k4["cpu_baseline_all_cores"] = cb["all_cores"]
         if k5 is not None:
             cb = cpu_baseline_k5(args, terr, info)
             k5["cpu_baseline"], k5["cpu_baseline_1thread"] = cb["all"], cb["1thread"]
+            k5["cpu_baseline_all_cores"] = cb["all_cores"]
     return k4, k5
 
 
@@ -569,6 +646,7 @@ def summary(out):
             f, k = roof(leg)
             s[name] = {"value": r(leg["value"]), "ms_per_map": r(leg["ms_per_map"]), "roofline_frac": f,
                        "traj_ms": k, "replay_ms": r((leg.get("stage_ms") or {}).get("replay_ms")),
+                       "map_equals_one_gpu": leg.get("map_equals_one_gpu"),
                        "cpu": r((leg.get("cpu_baseline") or {}).get("value")),
                        "cpu_1t": r((leg.get("cpu_baseline_1thread") or {}).get("value"))}
     return s
@@ -702,12 +780,16 @@ def main():
         value = bounces / elapsed
         bytes_per_launch = N * (24 * P + 4)  # traced + received rows + row_mask
         achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
-        traffic = None
+        traffic = traffic_parts = None
         try:
             with open(args.traffic_json) as fh:
                 tj = json.load(fh)
             if tj.get("rays") == N and tj.get("bounces") == B:
+                # both launches of the step's timed span: the coalesced NaN / 0 fill of received and
+                # row_mask (k_fill_received) and the trace kernel
                 traffic = tj.get("hbm_bytes_per_launch")
+                traffic_parts = {"k_fill_received": tj.get("fill_bytes_per_launch"),
+                                 f"k_trace_bf<{B}>": tj.get("trace_kernel_bytes_per_launch"), "source": tj.get("tag")}
         except (OSError, ValueError):
             pass
         # the binding resource of the brute-force LDS kernel is the VALU issue rate: VALU
@@ -745,8 +827,10 @@ def main():
                        "rays_per_gpu": N, "bounces": B, "rays_total": N * world, "settle_steps": settle,
                        "parallelism": f"ray-id shards x{world}, RCCL all-reduce of the CIR"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": f"k_trace_bf<{B}>", "kernel_ms": kern_ms,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_parts": traffic_parts,
+                         "kernel": f"k_fill_received + k_trace_bf<{B}>", "kernel_ms": kern_ms,
+                         "kernel_ms_span": "HIP events carried by the fill's and the trace kernel's dispatch packets "
+                                           "(fill start to trace end)",
                          "launches_timed": int(pst[0]), "launch_sampling": f"every {args.profile_every}",
                          "algorithmic_bytes_per_launch": bytes_per_launch, "ray_bounces": N * B,
                          "active_ray_bounces": active},
@@ -767,16 +851,28 @@ def main():
             out["cpu_baseline"] = cb["all"]
             # Warp's CPU launch is serial: the same restatement on one thread
             out["cpu_baseline_1thread"] = cb["1thread"]
+            # every CPU the process may run on (affinity), beside the box's thread share;
+            # host.cgroup_cpu_quota says how many of them the box's scheduler lets run at once
+            out["cpu_baseline_all_cores"] = cb["all_cores"]
             if cov_out is not None:
                 cb3 = cpu_baseline_k3(args, info)
                 out["coverage"]["cpu_baseline"], out["coverage"]["cpu_baseline_1thread"] = cb3["all"], cb3["1thread"]
+                out["coverage"]["cpu_baseline_all_cores"] = cb3["all_cores"]
             if k1_out is not None:
                 cb1 = cpu_baseline_k1(args, info, build)
                 k1_out["cpu_baseline"], k1_out["cpu_baseline_1thread"] = cb1["all"], cb1["1thread"]
+                k1_out["cpu_baseline_all_cores"] = cb1["all_cores"]
         out["summary"] = summary(out)  # last key: survives a truncated tail of the line
         print(json.dumps(out), flush=True)
+        bad = [k for k in ("coverage", "k5_terrain_coverage") if (out.get(k) or {}).get("map_equals_one_gpu") is False]
+    else:
+        bad = []
     if world > 1:
         dist.destroy_process_group()
+    if bad:
+        print(f"bench: the {world}-rank map of {', '.join(bad)} differs from the one-GPU map", file=sys.stderr,
+              flush=True)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

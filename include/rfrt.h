@@ -134,14 +134,15 @@ int rt_coverage_run(rt_coverage* cov, const float* tx_pos, double tx_power, doub
  * of (cell, bin, sum) records.  Sums are exact: 192-bit unsigned fixed point, unit 2^-136, three
  * uint64 per record (least significant first), rounded once to f64 by the owner, so the map does
  * not depend on the rank count or on the order in which records arrive.
- *   1. rt_coverage_create_rays                         (once)
- *   2. rt_coverage_trace_records -> counts[world]      (records for each destination rank; syncs)
- *   3. rt_coverage_records -> caller device buffers    (grouped by destination, rank 0 first)
- *      (2+3 in one call: rt_coverage_trace_records_to, or _packed for one row per record)
- *   4. all-to-all of the records (the caller's collective: RCCL via torch.distributed)
- *   5. rt_coverage_power_segments on the received records, concatenated in source-rank order
- *      (rt_coverage_power_packed for packed rows; rt_coverage_power_records for any order)
- *   6. sum-reduce of the power maps (other ranks' cells are 0 here). */
+ * A record travels as one 32-B row: (cell << 32 | bin, sum word 0, 1, 2), rows 16-B aligned.
+ *   1. rt_coverage_create_rays (or _create_sectors)      (once)
+ *   2. rt_coverage_trace_rows_async -> rows grouped by destination rank (rank 0 first), send
+ *      counts on the device; rt_coverage_trace_rows_finish -> host counts (one stream wait)
+ *      (rt_coverage_records_packed fetches the rows when the caller's buffer was too small)
+ *   3. all-to-all of the counts and the rows (the caller's collective: RCCL via torch.distributed)
+ *   4. rt_coverage_power_packed on the received rows, segment t from rank t in source order
+ *      (rt_coverage_power_rows for rows in any order, e.g. unsummed amplitudes)
+ *   5. sum-reduce / all-gather of the power maps (other ranks' cells are 0 here). */
 int rt_coverage_create_rays(int device, const rt_mesh* env, int max_bounces, int64_t n_rays_total, int64_t ray_offset,
                             int64_t n_rays, const rt_grid* grid, double rx_radius, int rank, int world,
                             rt_coverage** out);
@@ -152,67 +153,44 @@ int rt_coverage_create_rays(int device, const rt_mesh* env, int max_bounces, int
  * scene.  Any partition of the rays gives the same map bit for bit (exact fixed-point sums). */
 int rt_coverage_create_sectors(int device, const rt_mesh* env, int max_bounces, int64_t n_rays_total,
                                const rt_grid* grid, double rx_radius, int rank, int world, rt_coverage** out);
-int rt_coverage_trace_records(rt_coverage* cov, const float* tx_pos, double tx_power, double light_speed,
-                              double sample_rate, int flags, int64_t n_bins, int64_t* counts, int64_t* stats,
-                              void* stream);
-/* rt_coverage_trace_records that also writes the records (rt_coverage_records' layout) into the
- * caller's device buffers of max_out records before it synchronizes, when they fit: stats[2] = 1
- * then (else 0, and the caller takes them with rt_coverage_records).  stats: 3 int64.
- * The trace calls return RT_EHIP ("a look-back wait timed out") if a cross-tile wait of this
- * call's record reduce, or of the plan's previous owner stage, gave up: the sums would be wrong. */
-int rt_coverage_trace_records_to(rt_coverage* cov, const float* tx_pos, double tx_power, double light_speed,
-                                 double sample_rate, int flags, int64_t n_bins, uint64_t* keys_out, uint64_t* sums_out,
-                                 int64_t max_out, int64_t* counts, int64_t* stats, void* stream);
-/* rt_coverage_trace_records_to with each record as one 32-B row (key, sum word 0, 1, 2) of
- * rows_out (device, 16-B aligned, max_out rows): the layout the all-to-all sends as it is, so the
- * caller packs nothing (rt_coverage_power_packed takes the received rows).  stats: 3 int64. */
-int rt_coverage_trace_records_packed(rt_coverage* cov, const float* tx_pos, double tx_power, double light_speed,
-                                     double sample_rate, int flags, int64_t n_bins, uint64_t* rows_out,
-                                     int64_t max_out, int64_t* counts, int64_t* stats, void* stream);
-/* rt_coverage_trace_records_packed in two halves, so a rank can exchange its send counts on the
- * device (the RCCL all-to-all of the counts, queued on `stream`) before the host waits once for
- * both: _async queues the trace stage and leaves the send counts in counts_dev (device int64
- * [world]) without synchronising; _finish synchronises `stream` and returns the host counts and
- * stats as rt_coverage_trace_records_packed does (stats[2] = 0: rows_out was too small, fetch with
- * rt_coverage_records_packed).  Replaces the blocking count read of the reference-side all-to-all
- * (coverage.py:38-57 has none: its loop is single-process). */
+/* The trace stage in two halves, so a rank can exchange its send counts on the device (the RCCL
+ * all-to-all of the counts, queued on `stream`) before the host waits once for both: _async
+ * queues the trajectories, candidates, exact receiver tests, replay and the exact per-(owner,
+ * cell, bin) sums, writes the rows into rows_out (max_out rows) and the send counts into
+ * counts_dev (device int64 [world]) without synchronising; _finish synchronises `stream` and
+ * returns the host counts and stats[3] = (candidates, first-win records, 1 if rows_out held every
+ * row else 0 -- then fetch them with rt_coverage_records_packed).  Returns RT_EHIP ("a look-back
+ * wait timed out") if a cross-tile wait of this stage's reduce, or of the plan's previous owner
+ * stage, gave up: the sums would be wrong.  Replaces the per-cell loop's trace + CIR
+ * (coverage.py:43, tracer.py:63-117) for this rank's rays. */
 int rt_coverage_trace_rows_async(rt_coverage* cov, const float* tx_pos, double tx_power, double light_speed,
                                  double sample_rate, int flags, int64_t n_bins, uint64_t* rows_out, int64_t max_out,
                                  int64_t* counts_dev, void* stream);
 int rt_coverage_trace_rows_finish(rt_coverage* cov, int64_t* counts, int64_t* stats, void* stream);
-/* keys_out (cell << 32 | bin), sums_out (3 uint64 per record): device, max_out >= sum(counts). */
-int rt_coverage_records(rt_coverage* cov, uint64_t* keys_out, uint64_t* sums_out, int64_t max_out, void* stream);
-/* The last trace's records as rt_coverage_trace_records_packed's 32-B rows (device, 16-B aligned,
- * max_out >= sum(counts)): fetches them when that call's rows_out was too small (stats[2] = 0),
- * instead of tracing again. */
+/* The last trace stage's rows (device, 16-B aligned, max_out >= sum(counts)), when
+ * rt_coverage_trace_rows_async's buffer was too small: fetched from the plan, not traced again. */
 int rt_coverage_records_packed(rt_coverage* cov, uint64_t* rows_out, int64_t max_out, void* stream);
-/* keys (cell << 32 | bin) and sums (3 uint64 per record) received from every rank, in any order. */
-int rt_coverage_power_records(rt_coverage* cov, const uint64_t* keys, const uint64_t* sums, int64_t n, int64_t n_bins,
-                              double alpha, double* power, void* stream);
-/* rt_coverage_power_records for records that arrive as nseg (<= 64) segments of seg_counts[t]
- * records (host array), segment t from rank t, each in rt_coverage_records' order (ascending keys,
- * no repeated key): the segments are merged by rank instead of sorted (one launch).
- * PRECONDITION: every segment strictly ascending -- what rt_coverage_records /
- * _trace_records_packed emit and an all-to-all delivers.  The merge counts violations on the
- * device (the map is then wrong); rt_coverage_check reports them.  Unordered records go through
- * rt_coverage_power_records (which sorts) instead. */
-int rt_coverage_power_segments(rt_coverage* cov, const uint64_t* keys, const uint64_t* sums, const int64_t* seg_counts,
-                               int nseg, int64_t n_bins, double alpha, double* power, void* stream);
-/* rt_coverage_power_segments on received (key, sum) rows of rt_coverage_trace_records_packed's
- * layout, segment t = seg_counts[t] rows from rank t. */
+/* The owner stage (coverage.py:45-52 for this rank's cells): received rows as nseg (<= 64)
+ * segments of seg_counts[t] rows (host array), segment t from rank t, merged by rank.
+ * PRECONDITION: every segment strictly ascending by key -- what rt_coverage_trace_rows_async emits
+ * and an all-to-all delivers.  The merge counts violations on the device (the map is then wrong);
+ * rt_coverage_check reports them.  Unordered rows go through rt_coverage_power_rows (which sorts). */
 int rt_coverage_power_packed(rt_coverage* cov, const uint64_t* rows, const int64_t* seg_counts, int nseg,
                              int64_t n_bins, double alpha, double* power, void* stream);
+/* The owner stage on n rows in any order (keys may repeat: equal keys are summed exactly). */
+int rt_coverage_power_rows(rt_coverage* cov, const uint64_t* rows, int64_t n, int64_t n_bins, double alpha,
+                           double* power, void* stream);
 /* Errors the device detected in this plan's earlier asynchronous stages, reported and cleared
  * (synchronises `stream`): out[0] = look-back waits that gave up (the sums of that call are wrong),
  * out[1] = received rows of a segment not in strictly ascending key order (the owner stage's
  * precondition: that power map is wrong).  RT_EHIP when either is nonzero.  out may be NULL.
  * (The owner stage returns before the device has run; Coverage.run checks after every map.) */
 int rt_coverage_check(rt_coverage* cov, int64_t* out, void* stream);
-/* f64 amplitudes (finite, >= 0, below 2^56) -> the exact fixed-point sums of rt_coverage_records
+/* f64 amplitudes (finite, >= 0, below 2^56) -> the exact fixed-point sums of the coverage rows
  * (truncated below 2^-136), on the device. */
 int rt_coverage_amps_to_sums(const double* amps, int64_t n, uint64_t* sums, void* stream);
 /* Sparse per-cell impulse responses of the last rt_coverage_run (or, ray-sharded, of this rank's cells
- * after rt_coverage_power_records): keys (cell << 32 | bin) ascending, amplitudes. */
+ * after its owner stage): keys (cell << 32 | bin) ascending, amplitudes. */
 int rt_coverage_received(rt_coverage* cov, uint64_t* keys_out, double* amps_out, int64_t max_out, int64_t* n_out,
                          void* stream);
 /* Signal power (same definition) of `rows` dense impulse responses (rows, n_bins) f64 on the device.

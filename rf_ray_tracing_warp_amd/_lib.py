@@ -63,33 +63,21 @@ def lib():
                                   ctypes.c_double, _vp, _vp, _vp]
     L.rt_coverage_create_rays.argtypes = [_int, _vp, _int, _i64, _i64, _i64, _vp, ctypes.c_double, _int, _int,
                                           ctypes.POINTER(_vp)]
-    if hasattr(L, "rt_coverage_create_sectors"):
-        L.rt_coverage_create_sectors.argtypes = [_int, _vp, _int, _i64, _vp, ctypes.c_double, _int, _int, _vp]
-    L.rt_coverage_trace_records.argtypes = [_vp, _vp, ctypes.c_double, ctypes.c_double, ctypes.c_double, _int, _i64,
-                                            _vp, _vp, _vp]
-    L.rt_coverage_records.argtypes = [_vp, _vp, _vp, _i64, _vp]
+    L.rt_coverage_create_sectors.argtypes = [_int, _vp, _int, _i64, _vp, ctypes.c_double, _int, _int, _vp]
     L.rt_coverage_records_packed.argtypes = [_vp, _vp, _i64, _vp]
-    L.rt_coverage_trace_records_to.argtypes = [_vp, _vp, ctypes.c_double, ctypes.c_double, ctypes.c_double, _int,
-                                               _i64, _vp, _vp, _i64, _vp, _vp, _vp]
-    L.rt_coverage_power_records.argtypes = [_vp, _vp, _vp, _i64, _i64, ctypes.c_double, _vp, _vp]
-    L.rt_coverage_power_segments.argtypes = [_vp, _vp, _vp, _vp, _int, _i64, ctypes.c_double, _vp, _vp]
-    L.rt_coverage_trace_records_packed.argtypes = [_vp, _vp, ctypes.c_double, ctypes.c_double, ctypes.c_double,
-                                                   _int, _i64, _vp, _i64, _vp, _vp, _vp]
+    L.rt_coverage_power_rows.argtypes = [_vp, _vp, _i64, _i64, ctypes.c_double, _vp, _vp]
     L.rt_coverage_power_packed.argtypes = [_vp, _vp, _vp, _int, _i64, ctypes.c_double, _vp, _vp]
     L.rt_coverage_amps_to_sums.argtypes = [_vp, _i64, _vp, _vp]
     L.rt_coverage_received.argtypes = [_vp, _vp, _vp, _i64, ctypes.POINTER(_i64), _vp]
     L.rt_power_dense.argtypes = [_vp, _i64, _i64, ctypes.c_double, _vp, _i64, _vp, _vp]
     L.rt_coverage_profile.argtypes = [_vp, _int]
-    # round-5 entry points; an A/B library of an older tree (tools/_var, RFRT_LIB_PATH) lacks them
-    if hasattr(L, "rt_coverage_check"):
-        L.rt_coverage_check.argtypes = [_vp, _vp, _vp]
-        L.rt_coverage_trace_rows_async.argtypes = [_vp, _vp, ctypes.c_double, ctypes.c_double, ctypes.c_double,
-                                                   _int, _i64, _vp, _i64, _vp, _vp]
-        L.rt_coverage_trace_rows_finish.argtypes = [_vp, _vp, _vp, _vp]
+    L.rt_coverage_check.argtypes = [_vp, _vp, _vp]
+    L.rt_coverage_trace_rows_async.argtypes = [_vp, _vp, ctypes.c_double, ctypes.c_double, ctypes.c_double, _int,
+                                               _i64, _vp, _i64, _vp, _vp]
+    L.rt_coverage_trace_rows_finish.argtypes = [_vp, _vp, _vp, _vp]
     L.rt_coverage_last_profile.argtypes = [_vp, _vp, _int]
     L.rt_debug_poison.argtypes = [_int]
-    if hasattr(L, "rt_debug_replay_window_max"):
-        L.rt_debug_replay_window_max.argtypes = [_i64]
+    L.rt_debug_replay_window_max.argtypes = [_i64]
     L.rt_profile.argtypes = [_int]
     L.rt_trace_last_profile.argtypes = [_vp, _int]
     L.rt_trace_profile_stats.argtypes = [_vp, _int]
@@ -99,9 +87,9 @@ def lib():
     L.rt_selftest_fx.argtypes = [_vp, _vp, _i64, _int]
     for name in ("rt_mesh_create", "rt_mesh_create_ex", "rt_mesh_destroy", "rt_mesh_info", "rt_bvh_info", "rt_trace", "rt_compact", "rt_cir", "rt_trace_cir",
                  "rt_coverage_create", "rt_coverage_destroy", "rt_coverage_run", "rt_coverage_received",
-                 "rt_coverage_create_rays", "rt_coverage_create_sectors", "rt_coverage_trace_records", "rt_coverage_trace_records_to", "rt_coverage_records",
+                 "rt_coverage_create_rays", "rt_coverage_create_sectors",
                  "rt_coverage_records_packed",
-                 "rt_coverage_power_records", "rt_coverage_power_segments", "rt_coverage_trace_records_packed",
+                 "rt_coverage_power_rows",
                  "rt_coverage_power_packed", "rt_coverage_amps_to_sums", "rt_coverage_profile", "rt_coverage_check",
                  "rt_coverage_trace_rows_async", "rt_coverage_trace_rows_finish",
                  "rt_coverage_last_profile", "rt_debug_poison", "rt_debug_replay_window_max",

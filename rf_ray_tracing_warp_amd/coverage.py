@@ -104,7 +104,8 @@ class Coverage:
         """shard_index / shard_count: this rank of the job.  shard_mode "cells": this rank traces all
         tx_num_rays rays for the cells of its x columns (ix % shard_count == shard_index); "rays":
         it traces its contiguous share of the rays (dist.ray_range) for every cell and exchanges
-        records with the other ranks in run() (dist.exchange_records)."""
+        records with the other ranks in run() (dist.exchange_rows); "sectors": as "rays", with the
+        rank's rays a wedge of initial azimuth (rt_coverage_create_sectors) instead of an id range."""
         import torch
 
         if not torch.cuda.is_available():
@@ -145,77 +146,16 @@ class Coverage:
         self.power = torch.empty(grid.num_cells, dtype=torch.float64, device=f"cuda:{self.device}")
         self.last_candidates = 0
         self.last_first_wins = 0
-        self._rec = None  # ray mode: (keys, sums) record buffers of trace_records
-
-    def trace_records(self, tx_pos, tx_power=1):
-        """Ray mode, stage 1: this rank's rays for every cell.  Returns (keys, sums, counts): device
-        int64 keys (cell << 32 | bin) and the amplitudes summed per (cell, bin) over this rank's rays
-        as exact fixed point ((n, 3) int64: 192-bit unsigned, unit 2^-136, least significant word
-        first; include/rfrt.h), grouped by owner rank, counts[d] records for rank d.  The tensors are
-        views of this plan's buffers, overwritten by its next trace_records call."""
-        import torch
-
-        if self.shard_mode not in ("rays", "sectors"):
-            raise _lib.RfrtError("trace_records needs shard_mode='rays'")
-        tx = np.ascontiguousarray(np.asarray(tx_pos, dtype=np.float64).astype(np.float32))
-        counts = np.zeros(self.shard_count, np.int64)
-        stats = np.zeros(3, np.int64)
-        # grow-only record buffers, handed to the trace so that it fills them before it synchronizes
-        # (a fresh allocation per map measured ~0.25 ms of host time per rank; a second call after
-        # the synchronize, one launch and the ctypes round trip); the slices stay valid until the
-        # next call
-        if self._rec is None:
-            dev = f"cuda:{self.device}"
-            m = max(self.ray_count * 2, 1 << 16)
-            self._rec = (torch.empty(m, dtype=torch.int64, device=dev), torch.empty((m, 3), dtype=torch.int64, device=dev))
-        keys, sums = self._rec
-        check(lib().rt_coverage_trace_records_to(self._h, tx.ctypes.data, float(tx_power), float(self.light_speed_mps),
-                                                 float(self.sample_rate_hz),
-                                                 cir_flags(self.light_speed_mps, self.sample_rate_hz), self.n_bins,
-                                                 ptr(keys), ptr(sums), keys.numel(), counts.ctypes.data,
-                                                 stats.ctypes.data, _lib.stream_handle(self.device)),
-              "rt_coverage_trace_records_to")
-        self.last_candidates = int(stats[0])
-        n = int(counts.sum())
-        if not stats[2]:  # more records than the buffers hold: grow them and fetch the records
-            dev = f"cuda:{self.device}"
-            m = n + n // 4 + 1024
-            self._rec = (torch.empty(m, dtype=torch.int64, device=dev), torch.empty((m, 3), dtype=torch.int64, device=dev))
-            keys, sums = self._rec
-            check(lib().rt_coverage_records(self._h, ptr(keys), ptr(sums), n, _lib.stream_handle(self.device)),
-                  "rt_coverage_records")
-        return keys[:n], sums[:n], [int(c) for c in counts]
 
     def trace_rows(self, tx_pos, tx_power=1):
-        """trace_records with every record as one (n, 4) int64 row (key, sum words 0..2): the
-        layout exchange_rows sends as it is and power_from_rows takes (no packing copies on either
-        side of the all-to-all).  Returns (rows, counts); rows is a view of this plan's buffer,
-        overwritten by its next call."""
-        import torch
-
-        if self.shard_mode not in ("rays", "sectors"):
-            raise _lib.RfrtError("trace_rows needs shard_mode='rays'")
-        tx = np.ascontiguousarray(np.asarray(tx_pos, dtype=np.float64).astype(np.float32))
-        counts = np.zeros(self.shard_count, np.int64)
-        stats = np.zeros(3, np.int64)
-        dev = f"cuda:{self.device}"
-        if getattr(self, "_rows", None) is None:
-            # grow-only; a first guess of 2 records per ray (K3 ranks send ~1.6, K5 ~3.7): an
-            # overflow fetches the records from the plan (rt_coverage_records_packed), no re-trace
-            self._rows = torch.empty((max(self.ray_count * 2, 1 << 16), 4), dtype=torch.int64, device=dev)
-        rows = self._rows
-        check(lib().rt_coverage_trace_records_packed(
-            self._h, tx.ctypes.data, float(tx_power), float(self.light_speed_mps), float(self.sample_rate_hz),
-            cir_flags(self.light_speed_mps, self.sample_rate_hz), self.n_bins, ptr(rows), rows.shape[0],
-            counts.ctypes.data, stats.ctypes.data, _lib.stream_handle(self.device)),
-            "rt_coverage_trace_records_packed")
-        n = int(counts.sum())
-        if n and not stats[2]:
-            self._rows = rows = torch.empty((n + n // 4 + 1024, 4), dtype=torch.int64, device=dev)
-            check(lib().rt_coverage_records_packed(self._h, ptr(rows), rows.shape[0], _lib.stream_handle(self.device)),
-                  "rt_coverage_records_packed")
-        self.last_candidates = int(stats[0])
-        return rows[:n], [int(c) for c in counts]
+        """Ray mode, stage 1: this rank's rays for every cell, as one (n, 4) int64 row per record
+        (key = cell << 32 | bin, then the amplitudes summed per (cell, bin) over this rank's rays as
+        exact fixed point: 192-bit unsigned, unit 2^-136, least significant word first;
+        include/rfrt.h), grouped by owner rank -- the layout exchange_rows sends as it is and
+        power_from_rows takes.  Returns (rows, counts), counts[d] rows for rank d; rows is a view of
+        this plan's buffer, overwritten by its next call.  trace_rows_async + trace_rows_finish."""
+        self.trace_rows_async(tx_pos, tx_power)
+        return self.trace_rows_finish()
 
     def trace_rows_async(self, tx_pos, tx_power=1):
         """trace_rows without the host wait: queues the trace stage on the current stream and returns
@@ -225,7 +165,7 @@ class Coverage:
         import torch
 
         if self.shard_mode not in ("rays", "sectors"):
-            raise _lib.RfrtError("trace_rows_async needs shard_mode='rays'")
+            raise _lib.RfrtError("trace_rows_async needs shard_mode 'rays' or 'sectors'")
         tx = np.ascontiguousarray(np.asarray(tx_pos, dtype=np.float64).astype(np.float32))
         dev = f"cuda:{self.device}"
         if getattr(self, "_rows", None) is None:
@@ -253,55 +193,45 @@ class Coverage:
             check(lib().rt_coverage_records_packed(self._h, ptr(rows), rows.shape[0], _lib.stream_handle(self.device)),
                   "rt_coverage_records_packed")
         self.last_candidates = int(stats[0])
+        self.last_first_wins = int(stats[1])
         return rows[:n], [int(c) for c in counts]
 
-    def power_from_rows(self, rows, counts):
-        """power_from_records for (n, 4) int64 rows of trace_rows' layout arriving as consecutive
-        segments, counts[t] rows from rank t (exchange_rows' output).  Each segment must be in
-        trace_rows' order (strictly ascending keys): the segments are merged, not sorted.  The merge
-        counts keys out of order, and check() (run() calls it) raises on them: that map is wrong; use
-        power_from_records without counts for unordered records."""
+    def power_from_rows(self, rows, counts=None):
+        """Ray mode, last stage: the power of this rank's cells from (n, 4) int64 rows of
+        trace_rows' layout; the (num_cells,) float64 device map, 0 elsewhere.  counts: the rows
+        arrive as consecutive segments, counts[t] from rank t (exchange_rows' output), each in
+        trace_rows' order (strictly ascending keys): the segments are merged, not sorted
+        (rt_coverage_power_packed).  The merge counts keys out of order, and check() (run() calls it)
+        raises on them: that map is wrong.  Without counts the rows may come in any order, with
+        repeated keys summed exactly (rt_coverage_power_rows: sorted)."""
         import torch
         n = int(rows.shape[0]) if rows.dim() == 2 else 0
         if n and (tuple(rows.shape) != (n, 4) or not rows.is_contiguous() or rows.dtype != torch.int64):
             raise ValueError(f"rows must be a contiguous (n, 4) int64 tensor, got {tuple(rows.shape)} {rows.dtype}")
+        alpha = phase_step(self.sample_window_s, self.n_bins)
+        s = _lib.stream_handle(self.device)
+        if counts is None:
+            check(lib().rt_coverage_power_rows(self._h, ptr(rows) if n else None, n, self.n_bins, alpha,
+                                               ptr(self.power), s), "rt_coverage_power_rows")
+            return self.power
         c = np.ascontiguousarray(np.asarray(counts, dtype=np.int64))
         if int(c.sum()) != n or (c < 0).any():
             raise ValueError(f"segment counts {c.tolist()} do not add up to the {n} rows")
         check(lib().rt_coverage_power_packed(self._h, ptr(rows) if n else None, c.ctypes.data, len(c), self.n_bins,
-                                             phase_step(self.sample_window_s, self.n_bins), ptr(self.power),
-                                             _lib.stream_handle(self.device)), "rt_coverage_power_packed")
-        return self.power
-
-    def power_from_records(self, keys, sums, counts=None):
-        """Ray mode, last stage: the power of this rank's cells from the records every rank sent it
-        (keys and (n, 3) fixed-point sums); the (num_cells,) float64 device map, 0 elsewhere.
-        counts: the number of records from each source rank, when they arrive as consecutive
-        segments in trace_records' order (strictly ascending keys per segment, as exchange_records
-        delivers them; not checked -- another order gives a wrong map): the segments are merged by
-        rank (rt_coverage_power_segments).  Without counts the records may come in any order and are
-        sorted (rt_coverage_power_records)."""
-        n = int(keys.numel())
-        if n and tuple(sums.shape) != (n, 3):
-            raise ValueError(f"sums must be (n, 3) int64 fixed point, got {tuple(sums.shape)}")
-        alpha = phase_step(self.sample_window_s, self.n_bins)
-        s = _lib.stream_handle(self.device)
-        if counts is not None:
-            c = np.ascontiguousarray(np.asarray(counts, dtype=np.int64))
-            if int(c.sum()) != n or (c < 0).any():
-                raise ValueError(f"segment counts {c.tolist()} do not add up to the {n} records")
-            check(lib().rt_coverage_power_segments(self._h, ptr(keys) if n else None, ptr(sums) if n else None,
-                                                   c.ctypes.data, len(c), self.n_bins, alpha, ptr(self.power), s),
-                  "rt_coverage_power_segments")
-            return self.power
-        check(lib().rt_coverage_power_records(self._h, ptr(keys) if n else None, ptr(sums) if n else None, n,
-                                              self.n_bins, alpha, ptr(self.power), s), "rt_coverage_power_records")
+                                             alpha, ptr(self.power), s), "rt_coverage_power_packed")
         return self.power
 
     def power_from_amplitudes(self, keys, amps):
-        """power_from_records for float64 amplitudes (e.g. per-cell impulse responses computed
-        elsewhere): converted exactly to the fixed-point sums on the device first."""
-        return self.power_from_records(keys, amps_to_sums(amps))
+        """power_from_rows for (cell << 32 | bin) int64 keys with float64 amplitudes, in any order
+        (e.g. per-cell impulse responses computed elsewhere): packed into rows with their exact
+        fixed-point sums on the device first."""
+        import torch
+        n = int(keys.numel())
+        rows = torch.empty((n, 4), dtype=torch.int64, device=keys.device)
+        if n:
+            rows[:, 0] = keys.reshape(-1).to(torch.int64)
+            rows[:, 1:] = amps_to_sums(amps.reshape(-1))
+        return self.power_from_rows(rows)
 
     def run_device(self, tx_pos, tx_power=1, process_group=None):
         """Launch; returns the (num_cells,) float64 device tensor (0 for cells of other shards).

@@ -1350,17 +1350,17 @@ struct WideKey {
 
 // wide (cell << 32 | bin) keys received from other ranks -> compact [cell | bin] for the sort
 // ... and the record indices the sort carries as its payload (one launch for both)
-__global__ __launch_bounds__(256) void k_compact_keys(const uint64_t* in, int64_t n, int bin_bits, uint64_t* out,
-                                                      int64_t* idx) {
+__global__ __launch_bounds__(256) void k_compact_keys(const uint64_t* in, int64_t stride, int64_t n, int bin_bits,
+                                                      uint64_t* out, int64_t* idx) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint64_t k = in[i];
+    const uint64_t k = in[i * stride];
     out[i] = k == ~0ull ? ~0ull : ((k >> 32) << bin_bits | (k & 0xFFFFFFFFull));
     idx[i] = i;
   }
 }
 
 // The owner stage's records arrive as nseg segments (one per source rank), each sorted by its wide
-// key (rt_coverage_records' order).  Their stable merge by (key, segment) needs no sort: the merged
+// key (the order rt_coverage_trace_rows_async writes).  Their stable merge by (key, segment) needs no sort: the merged
 // position of element i of segment s is its index in s plus, over every other segment, the number
 // of elements with a smaller key (a larger-or-equal one for the segments before s) -- nseg - 1
 // binary searches over L2-resident keys.  One launch instead of a record sort (rocPRIM's merge sort,
@@ -1941,7 +1941,7 @@ struct rt_coverage {
   void* rord = nullptr;        // replay-order sort workspace (16-bit keys + int32 rows, x2, + hipCUB)
   size_t rord_bytes = 0;
   int64_t* bounds = nullptr;   // ray mode: [world + 1] starts of each owner's run in the reduced records
-  int64_t n_out = 0;           // ray mode: valid reduced records of the last rt_coverage_trace_records
+  int64_t n_out = 0;           // ray mode: valid reduced records of the last trace stage
   int64_t pend_ncand = 0, pend_nlist = 0, pend_max_out = -1;  // trace stage awaiting its host half
   // rt_coverage_profile: stage events of the last run and its work counts (device, [0] traced
   // ray-bounces = sum of the trajectories' segments, [1] replayed ray-bounces)
@@ -2409,10 +2409,8 @@ struct SendRuns {
   double* uamps;
   int64_t* nuniq;
   int64_t* bounds;
-  uint64_t* out;     // packed: 32-B rows; else keys (owner stripped), sums in sums_out
-  Fx192* sums_out;
-  int packed;
-  int64_t cap;       // rows the caller's buffers hold
+  uint64_t* out;     // 32-B (key without the owner field, sum words 0..2) rows
+  int64_t cap;       // rows the caller's buffer holds
 };
 __global__ __launch_bounds__(256) void k_send_runs(SendRuns a) {
   __shared__ uint32_t s_tile;
@@ -2586,15 +2584,10 @@ __global__ __launch_bounds__(256) void k_send_runs(SendRuns a) {
     a.usums[u] = acc;
     a.uamps[u] = fx_to_double(acc);
     if (a.out && k[j] != ~0ull && u < a.cap) {
-      if (a.packed) {
-        typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-        u64x2* row = reinterpret_cast<u64x2*>(a.out + 4 * u);  // 32-B rows: two 16-B stores
-        row[0] = u64x2{wkey & mask, acc.w0};
-        row[1] = u64x2{acc.w1, acc.w2};
-      } else {
-        a.out[u] = wkey & mask;
-        a.sums_out[u] = acc;
-      }
+      typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+      u64x2* row = reinterpret_cast<u64x2*>(a.out + 4 * u);  // 32-B rows: two 16-B stores
+      row[0] = u64x2{wkey & mask, acc.w0};
+      row[1] = u64x2{acc.w1, acc.w2};
     }
     if (i + 1 == a.n) {  // the owners after the last record's start at the end
       const int hi = k[j] == ~0ull ? a.world : (int)(wkey >> a.own_shift);
@@ -2939,7 +2932,7 @@ int own_shift(const rt_coverage* c) { return 32 + bits_for((uint64_t)cov_ncell(c
 // caller's capacity (the host sees the count and grows the buffer when it was too small)
 __global__ __launch_bounds__(256) void k_bounds_strip(const uint64_t* ukeys, const Fx192* usums, const int64_t* nuniq,
                                                       int world, int64_t cap, int shift, int64_t* bounds,
-                                                      uint64_t* out, Fx192* sums_out, int packed) {
+                                                      uint64_t* out) {
   const int64_t nu = *nuniq;
   const uint64_t mask = (1ull << shift) - 1;
   for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u <= nu; u += (int64_t)gridDim.x * blockDim.x) {
@@ -2949,27 +2942,11 @@ __global__ __launch_bounds__(256) void k_bounds_strip(const uint64_t* ukeys, con
     for (int64_t o = lo + 1; o <= hi; ++o) bounds[o] = u;  // owners lo+1 .. hi start at u
     if (out && k != ~0ull && u < cap) {
       const Fx192 v = usums[u];
-      if (packed) {
-        typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-        u64x2* row = reinterpret_cast<u64x2*>(out + 4 * u);  // 32-B rows: two 16-B stores
-        row[0] = u64x2{k & mask, v.w0};
-        row[1] = u64x2{v.w1, v.w2};
-      } else {
-        out[u] = k & mask;
-        sums_out[u] = v;
-      }
+      typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+      u64x2* row = reinterpret_cast<u64x2*>(out + 4 * u);  // 32-B rows: two 16-B stores
+      row[0] = u64x2{k & mask, v.w0};
+      row[1] = u64x2{v.w1, v.w2};
     }
-  }
-}
-
-// the reduced records of a ray-sharded plan into the caller's send buffers: keys without the owner
-// field, and the exact sums (one launch for both)
-__global__ __launch_bounds__(256) void k_strip_owner(const uint64_t* ukeys, const Fx192* usums, int64_t n, int shift,
-                                                     uint64_t* out, Fx192* sums_out) {
-  const uint64_t mask = (1ull << shift) - 1;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    out[i] = ukeys[i] & mask;
-    sums_out[i] = usums[i];
   }
 }
 
@@ -3302,8 +3279,9 @@ int cov_reduce(rt_coverage* c, const uint64_t* keys, const double* amps, int64_t
 }
 
 // owner stage: received (compact key, Fx192 sum) records -> sorted by key (index payload), summed
-int cov_reduce_sums(rt_coverage* c, const uint64_t* keys, const Fx192* sums, int64_t n, int sort_bits, WideKey wk,
-                    hipStream_t s) {
+// keys: compact keys of the records; words: record j's exact sum at words[j * stride .. + 2]
+int cov_reduce_sums(rt_coverage* c, const uint64_t* keys, const uint64_t* words, int64_t stride, int64_t n,
+                    int sort_bits, WideKey wk, hipStream_t s) {
   int rc = grow_for(c, n, s);
   if (rc) return rc;
   int64_t* idx = reinterpret_cast<int64_t*>(c->oamps);  // filled by k_compact_keys
@@ -3311,7 +3289,7 @@ int cov_reduce_sums(rt_coverage* c, const uint64_t* keys, const Fx192* sums, int
   size_t tb = c->tmp_bytes;
   RT_HIP(sort_records(c->tmp, tb, keys, c->okeys_sorted, (const int64_t*)idx, idx_sorted, n,
                       sort_bits < 64 ? sort_bits : 64, s));
-  return run_sums(c, SumVal{(const uint64_t*)sums, idx_sorted}, n, wk, s);
+  return run_sums(c, SumVal{words, idx_sorted, stride}, n, wk, s);
 }
 
 // Closed-form signal power of this plan's cells from the reduced records in c->ukeys / c->uamps
@@ -3451,7 +3429,7 @@ int rt_coverage_destroy(rt_coverage* c) {
 int rt_coverage_run(rt_coverage* c, const float* tx_pos, double tx_power, double light_speed, double sample_rate,
                     int flags, int64_t n_bins, double alpha, double* power, int64_t* stats, void* stream) {
   if (!c || !tx_pos || !power || n_bins < 1 || n_bins >= ((int64_t)1 << 32) || c->ray_mode) {
-    rt::set_error(c && c->ray_mode ? "rt_coverage_run: a ray-sharded plan runs through rt_coverage_trace_records"
+    rt::set_error(c && c->ray_mode ? "rt_coverage_run: a ray-sharded plan runs through rt_coverage_trace_rows_async"
                                    : "rt_coverage_run: invalid arguments");
     return RT_EINVAL;
   }
@@ -3535,61 +3513,18 @@ int rt_coverage_create_sectors(int device, const rt_mesh* env, int max_bounces, 
   return RT_OK;
 }
 
-int rt_coverage_trace_records_to(rt_coverage* c, const float* tx_pos, double tx_power, double light_speed,
-                                 double sample_rate, int flags, int64_t n_bins, uint64_t* keys_out, uint64_t* sums_out,
-                                 int64_t max_out, int64_t* counts, int64_t* stats, void* stream);
-
-int rt_coverage_trace_records(rt_coverage* c, const float* tx_pos, double tx_power, double light_speed,
-                              double sample_rate, int flags, int64_t n_bins, int64_t* counts, int64_t* stats,
-                              void* stream) {
-  int64_t st3[3] = {0, 0, 0};
-  const int rc = rt_coverage_trace_records_to(c, tx_pos, tx_power, light_speed, sample_rate, flags, n_bins, nullptr,
-                                              nullptr, 0, counts, st3, stream);
-  if (!rc && stats) {
-    stats[0] = st3[0];
-    stats[1] = st3[1];
-  }
-  return rc;
-}
-
 namespace {
-static int trace_records_impl(rt_coverage* c, const float* tx_pos, double tx_power, double light_speed, double sample_rate,
-                       int flags, int64_t n_bins, uint64_t* keys_out, uint64_t* sums_out, bool packed,
-                       int64_t max_out, int64_t* counts, int64_t* stats, void* stream, int64_t* counts_dev = nullptr);
-static int trace_rows_finish(rt_coverage* c, int64_t* counts, int64_t* stats, hipStream_t s);
-}
-
-int rt_coverage_trace_records_to(rt_coverage* c, const float* tx_pos, double tx_power, double light_speed,
-                                 double sample_rate, int flags, int64_t n_bins, uint64_t* keys_out, uint64_t* sums_out,
-                                 int64_t max_out, int64_t* counts, int64_t* stats, void* stream) {
-  if ((keys_out || sums_out) && (!keys_out || !sums_out || max_out < 0)) {
-    rt::set_error("rt_coverage_trace_records: invalid arguments (keys_out and sums_out go together)");
+// The trace stage of a ray-sharded plan: this rank's first-win records, summed exactly per
+// (owner, cell, bin) and written as 32-B rows (key without the owner field, three sum words) into
+// rows_out, grouped by owner (rank 0 first), when they fit (max_out rows); the send counts go to
+// counts_dev on the device.  No host wait: trace_rows_finish does it.
+int trace_rows_impl(rt_coverage* c, const float* tx_pos, double tx_power, double light_speed, double sample_rate,
+                    int flags, int64_t n_bins, uint64_t* rows_out, int64_t max_out, int64_t* counts_dev,
+                    hipStream_t s) {
+  if (!c || !c->ray_mode || !tx_pos || !counts_dev || n_bins < 1 || n_bins >= ((int64_t)1 << 32)) {
+    rt::set_error("rt_coverage_trace_rows_async: invalid arguments (needs a ray-sharded plan)");
     return RT_EINVAL;
   }
-  return trace_records_impl(c, tx_pos, tx_power, light_speed, sample_rate, flags, n_bins, keys_out, sums_out, false,
-                            max_out, counts, stats, stream);
-}
-
-int rt_coverage_trace_records_packed(rt_coverage* c, const float* tx_pos, double tx_power, double light_speed,
-                                     double sample_rate, int flags, int64_t n_bins, uint64_t* rows_out,
-                                     int64_t max_out, int64_t* counts, int64_t* stats, void* stream) {
-  if (!rows_out || max_out < 0 || (reinterpret_cast<uintptr_t>(rows_out) & 15)) {
-    rt::set_error("rt_coverage_trace_records_packed: invalid arguments (16-B aligned rows_out, max_out >= 0)");
-    return RT_EINVAL;
-  }
-  return trace_records_impl(c, tx_pos, tx_power, light_speed, sample_rate, flags, n_bins, rows_out, nullptr, true,
-                            max_out, counts, stats, stream);
-}
-
-namespace {
-static int trace_records_impl(rt_coverage* c, const float* tx_pos, double tx_power, double light_speed, double sample_rate,
-                       int flags, int64_t n_bins, uint64_t* keys_out, uint64_t* sums_out, bool packed,
-                       int64_t max_out, int64_t* counts, int64_t* stats, void* stream, int64_t* counts_dev) {
-  if (!c || !c->ray_mode || !tx_pos || (!counts && !counts_dev) || n_bins < 1 || n_bins >= ((int64_t)1 << 32)) {
-    rt::set_error("rt_coverage_trace_records: invalid arguments (needs a plan from rt_coverage_create_rays)");
-    return RT_EINVAL;
-  }
-  hipStream_t s = (hipStream_t)stream;
   rt::DeviceGuard dg(c->device);
   RT_HIP(dg.err);
   const int world = c->nshard;
@@ -3602,37 +3537,33 @@ static int trace_records_impl(rt_coverage* c, const float* tx_pos, double tx_pow
   prof_mark(c, 6, s);
   if (nlist > 0) {
     const KeyBits kb = key_bits(c, n_bins);
-    // the send buffers are filled before the host synchronizes (no launch after it)
-    {
-      if ((rc = grow_for(c, nlist, s))) return rc;
-      size_t tb = c->tmp_bytes;
-      const int sb = record_sort_bits(c, kb, n_bins);
-      RT_HIP(sort_records(c->tmp, tb, c->okeys, c->okeys_sorted, c->oamps, c->oamps_sorted, nlist, sb < 64 ? sb : 64, s));
-      SendRuns a{};
-      a.keys = c->okeys_sorted;
-      a.amps = c->oamps_sorted;
-      a.n = nlist;
-      a.states = c->own_states;
-      const int64_t ntiles = (nlist + kSendTile - 1) / kSendTile;
-      a.agg_tail = c->send_tails;
-      a.inc_tail = a.agg_tail + 5 * (c->cap / kOwnTile + 2);
-      a.ticket = c->own_aux;
-      a.errors = reinterpret_cast<unsigned*>(c->own_aux + 1);
-      a.tag = (c->own_tag++ % 0xFFFFFEull + 1ull) << 40;
-      a.wk = wide_key(c, kb);
-      a.world = world;
-      a.own_shift = own_shift(c);
-      a.ukeys = c->ukeys;
-      a.usums = plan_sums(c);
-      a.uamps = c->uamps;
-      a.nuniq = c->nuniq;
-      a.bounds = c->bounds;
-      a.out = keys_out;
-      a.sums_out = (Fx192*)sums_out;
-      a.packed = packed ? 1 : 0;
-      a.cap = keys_out ? max_out : 0;
-      hipLaunchKernelGGL(k_send_runs, dim3((unsigned)ntiles), dim3(256), 0, s, a);
-    }
+    // the send rows are written before the host synchronizes (no launch after it)
+    if ((rc = grow_for(c, nlist, s))) return rc;
+    size_t tb = c->tmp_bytes;
+    const int sb = record_sort_bits(c, kb, n_bins);
+    RT_HIP(sort_records(c->tmp, tb, c->okeys, c->okeys_sorted, c->oamps, c->oamps_sorted, nlist, sb < 64 ? sb : 64, s));
+    SendRuns a{};
+    a.keys = c->okeys_sorted;
+    a.amps = c->oamps_sorted;
+    a.n = nlist;
+    a.states = c->own_states;
+    const int64_t ntiles = (nlist + kSendTile - 1) / kSendTile;
+    a.agg_tail = c->send_tails;
+    a.inc_tail = a.agg_tail + 5 * (c->cap / kOwnTile + 2);
+    a.ticket = c->own_aux;
+    a.errors = reinterpret_cast<unsigned*>(c->own_aux + 1);
+    a.tag = (c->own_tag++ % 0xFFFFFEull + 1ull) << 40;
+    a.wk = wide_key(c, kb);
+    a.world = world;
+    a.own_shift = own_shift(c);
+    a.ukeys = c->ukeys;
+    a.usums = plan_sums(c);
+    a.uamps = c->uamps;
+    a.nuniq = c->nuniq;
+    a.bounds = c->bounds;
+    a.out = rows_out;
+    a.cap = max_out;
+    hipLaunchKernelGGL(k_send_runs, dim3((unsigned)ntiles), dim3(256), 0, s, a);
     RT_HIP(hipGetLastError());
     prof_mark(c, 7, s);
     // both into pinned memory (a pageable copy stages through the host: ~20 us of gap per rank),
@@ -3640,36 +3571,29 @@ static int trace_records_impl(rt_coverage* c, const float* tx_pos, double tx_pow
     // an earlier owner stage): their sums would be wrong, so the run fails instead
     RT_HIP(hipMemcpyAsync(c->hbounds, c->bounds, sizeof(int64_t) * (world + 1), hipMemcpyDeviceToHost, s));
     RT_HIP(hipMemcpyAsync(c->hbounds + world + 1, c->own_aux + 1, 8, hipMemcpyDeviceToHost, s));
+    hipLaunchKernelGGL(k_bounds_to_counts, dim3(1), dim3(64), 0, s, c->bounds, world, counts_dev);
   } else {
     for (int o = 0; o <= world + 1; ++o) c->hbounds[o] = 0;  // nothing sent (no copy in flight)
+    RT_HIP(hipMemsetAsync(counts_dev, 0, sizeof(int64_t) * world, s));
   }
+  RT_HIP(hipGetLastError());
   c->pend_ncand = ncand;
   c->pend_nlist = nlist;
-  c->pend_max_out = keys_out ? max_out : -1;
-  if (counts_dev) {  // deferred: the send counts on the device now, the host reads them at the finish
-    if (nlist > 0)
-      hipLaunchKernelGGL(k_bounds_to_counts, dim3(1), dim3(64), 0, s, c->bounds, world, counts_dev);
-    else
-      RT_HIP(hipMemsetAsync(counts_dev, 0, sizeof(int64_t) * world, s));
-    RT_HIP(hipGetLastError());
-    return RT_OK;
-  }
-  const int rcf = trace_rows_finish(c, counts, stats, s);
-  c->pend_max_out = -1;
-  return rcf;
+  c->pend_max_out = max_out;
+  return RT_OK;
 }
 
 // The host half of a trace stage: waits for the stream, then the bounds and the look-back error
-// word copied to pinned memory by trace_records_impl give the send counts.
-static int trace_rows_finish(rt_coverage* c, int64_t* counts, int64_t* stats, hipStream_t s) {
+// word copied to pinned memory by trace_rows_impl give the send counts.
+int trace_rows_finish(rt_coverage* c, int64_t* counts, int64_t* stats, hipStream_t s) {
   const int world = c->nshard;
   RT_HIP(hipStreamSynchronize(s));
   if (const int64_t w = c->hbounds[world + 1]) {
     c->hbounds[world + 1] = 0;
     RT_HIP(hipMemset(c->own_aux + 1, 0, 8));
-    rt::set_error((w & 0xFFFFFFFFll) ? "rt_coverage_trace_records: a look-back wait timed out (results discarded)"
-                                     : "rt_coverage_trace_records: the previous owner stage received a segment out "
-                                       "of key order (its power map was wrong)");
+    rt::set_error((w & 0xFFFFFFFFll) ? "rt_coverage_trace_rows_finish: a look-back wait timed out (results discarded)"
+                                     : "rt_coverage_trace_rows_finish: the previous owner stage received a segment "
+                                       "out of key order (its power map was wrong)");
     return RT_EHIP;
   }
   for (int o = 0; o < world; ++o) counts[o] = c->hbounds[o + 1] - c->hbounds[o];
@@ -3677,7 +3601,7 @@ static int trace_rows_finish(rt_coverage* c, int64_t* counts, int64_t* stats, hi
   if (stats) {
     stats[0] = c->pend_ncand;
     stats[1] = c->pend_nlist;
-    stats[2] = c->pend_max_out >= 0 && c->n_out <= c->pend_max_out ? 1 : 0;  // the records are in the caller's buffer
+    stats[2] = c->n_out <= c->pend_max_out ? 1 : 0;  // the rows are in the caller's buffer
   }
   return RT_OK;
 }
@@ -3690,8 +3614,8 @@ int rt_coverage_trace_rows_async(rt_coverage* c, const float* tx_pos, double tx_
     rt::set_error("rt_coverage_trace_rows_async: invalid arguments (16-B aligned rows_out, max_out >= 0, counts_dev)");
     return RT_EINVAL;
   }
-  return trace_records_impl(c, tx_pos, tx_power, light_speed, sample_rate, flags, n_bins, rows_out, nullptr, true,
-                            max_out, nullptr, nullptr, stream, counts_dev);
+  return trace_rows_impl(c, tx_pos, tx_power, light_speed, sample_rate, flags, n_bins, rows_out, max_out, counts_dev,
+                         (hipStream_t)stream);
 }
 
 int rt_coverage_trace_rows_finish(rt_coverage* c, int64_t* counts, int64_t* stats, void* stream) {
@@ -3706,21 +3630,6 @@ int rt_coverage_trace_rows_finish(rt_coverage* c, int64_t* counts, int64_t* stat
   return rc;
 }
 
-int rt_coverage_records(rt_coverage* c, uint64_t* keys_out, uint64_t* sums_out, int64_t max_out, void* stream) {
-  if (!c || !c->ray_mode || (c->n_out > 0 && (!keys_out || !sums_out)) || max_out < c->n_out) {
-    rt::set_error("rt_coverage_records: invalid arguments (max_out must hold the sum of the counts)");
-    return RT_EINVAL;
-  }
-  if (c->n_out == 0) return RT_OK;
-  hipStream_t s = (hipStream_t)stream;
-  rt::DeviceGuard dg(c->device);
-  RT_HIP(dg.err);
-  hipLaunchKernelGGL(k_strip_owner, dim3((unsigned)std::min<int64_t>((c->n_out + 255) / 256, 4096)), dim3(256), 0, s,
-                     c->ukeys, plan_sums(c), c->n_out, own_shift(c), keys_out, (Fx192*)sums_out);
-  RT_HIP(hipGetLastError());
-  return RT_OK;
-}
-
 int rt_coverage_records_packed(rt_coverage* c, uint64_t* rows_out, int64_t max_out, void* stream) {
   if (!c || !c->ray_mode || (c->n_out > 0 && !rows_out) || max_out < c->n_out ||
       (reinterpret_cast<uintptr_t>(rows_out) & 15)) {
@@ -3732,10 +3641,9 @@ int rt_coverage_records_packed(rt_coverage* c, uint64_t* rows_out, int64_t max_o
   rt::DeviceGuard dg(c->device);
   RT_HIP(dg.err);
   // the reduced records are still in the plan (ukeys / sums, valid ones first): the same rows
-  // k_bounds_strip writes (its bounds are rewritten with the same values)
+  // k_send_runs writes (its bounds are rewritten with the same values)
   hipLaunchKernelGGL(k_bounds_strip, dim3((unsigned)std::min<int64_t>((c->n_out + 256) / 256, 4096)), dim3(256), 0, s,
-                     c->ukeys, plan_sums(c), c->nuniq, c->nshard, max_out, own_shift(c), c->bounds, rows_out,
-                     (Fx192*)nullptr, 1);
+                     c->ukeys, plan_sums(c), c->nuniq, c->nshard, max_out, own_shift(c), c->bounds, rows_out);
   RT_HIP(hipGetLastError());
   return RT_OK;
 }
@@ -3752,11 +3660,11 @@ int rt_coverage_amps_to_sums(const double* amps, int64_t n, uint64_t* sums, void
   return RT_OK;
 }
 
-int rt_coverage_power_records(rt_coverage* c, const uint64_t* keys, const uint64_t* sums, int64_t n, int64_t n_bins,
-                              double alpha, double* power, void* stream) {
-  if (!c || !c->ray_mode || n < 0 || (n > 0 && (!keys || !sums)) || !power || n_bins < 1 ||
-      n_bins >= ((int64_t)1 << 32) || n > ((int64_t)1 << 31) - 1) {
-    rt::set_error("rt_coverage_power_records: invalid arguments");
+int rt_coverage_power_rows(rt_coverage* c, const uint64_t* rows, int64_t n, int64_t n_bins, double alpha, double* power,
+                           void* stream) {
+  if (!c || !c->ray_mode || n < 0 || (n > 0 && !rows) || !power || n_bins < 1 || n_bins >= ((int64_t)1 << 32) ||
+      n > ((int64_t)1 << 31) - 1) {
+    rt::set_error("rt_coverage_power_rows: invalid arguments");
     return RT_EINVAL;
   }
   hipStream_t s = (hipStream_t)stream;
@@ -3774,13 +3682,12 @@ int rt_coverage_power_records(rt_coverage* c, const uint64_t* keys, const uint64
     kb.ray = 0;
     kb.own = 0;
     kb.cell = std::max(1, bits_for((uint64_t)(cov_ncell(c) - 1)));  // received keys carry global cells
-    hipLaunchKernelGGL(k_compact_keys, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 8192)), dim3(256), 0, s, keys,
-                       n, kb.bin, c->keys_sorted, reinterpret_cast<int64_t*>(c->oamps));
+    hipLaunchKernelGGL(k_compact_keys, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 8192)), dim3(256), 0, s, rows,
+                       (int64_t)4, n, kb.bin, c->keys_sorted, reinterpret_cast<int64_t*>(c->oamps));
     RT_HIP(hipGetLastError());
     // received keys are valid ones (a ~0 key, never sent, would need the extra bit to sort last)
     const bool safe = ((1ll << kb.bin) - 1 >= n_bins) || ((1ll << kb.cell) - 1 >= cov_ncell(c));
-    rc = cov_reduce_sums(c, c->keys_sorted, (const Fx192*)sums, n, kb.total() + (safe ? 0 : 1), wide_key(c, kb, false),
-                         s);
+    rc = cov_reduce_sums(c, c->keys_sorted, rows + 1, 4, n, kb.total() + (safe ? 0 : 1), wide_key(c, kb, false), s);
   } else {
     RT_HIP(hipMemsetAsync(c->nuniq, 0, 8, s));
   }
@@ -3789,42 +3696,30 @@ int rt_coverage_power_records(rt_coverage* c, const uint64_t* keys, const uint64
   return rc;
 }
 
-namespace {
-static int power_segments_impl(rt_coverage* c, const uint64_t* keys, const uint64_t* sums, int64_t stride,
-                        const int64_t* seg_counts, int nseg, int64_t n_bins, double alpha, double* power, void* stream);
-}
-
-int rt_coverage_power_segments(rt_coverage* c, const uint64_t* keys, const uint64_t* sums, const int64_t* seg_counts,
-                               int nseg, int64_t n_bins, double alpha, double* power, void* stream) {
-  return power_segments_impl(c, keys, sums, 1, seg_counts, nseg, n_bins, alpha, power, stream);
-}
-
+// The owner stage on received rows (key, sum words 0..2) arriving as nseg segments, segment t =
+// seg_counts[t] rows from rank t, each strictly ascending by key: merged by rank, not sorted.
 int rt_coverage_power_packed(rt_coverage* c, const uint64_t* rows, const int64_t* seg_counts, int nseg, int64_t n_bins,
                              double alpha, double* power, void* stream) {
-  return power_segments_impl(c, rows, rows ? rows + 1 : nullptr, 4, seg_counts, nseg, n_bins, alpha, power, stream);
-}
-
-namespace {
-// stride 1: keys[n] and Fx192 sums[n]; stride 4: (key, sum) rows, keys = rows, sums = rows + 1
-static int power_segments_impl(rt_coverage* c, const uint64_t* keys, const uint64_t* sums, int64_t stride,
-                        const int64_t* seg_counts, int nseg, int64_t n_bins, double alpha, double* power, void* stream) {
   if (!c || !c->ray_mode || nseg < 1 || nseg > kMaxSegs || !seg_counts || !power || n_bins < 1 ||
       n_bins >= ((int64_t)1 << 32)) {
-    rt::set_error("rt_coverage_power_segments: invalid arguments (1 <= nseg <= 64)");
+    rt::set_error("rt_coverage_power_packed: invalid arguments (1 <= nseg <= 64)");
     return RT_EINVAL;
   }
+  constexpr int64_t stride = 4;  // (key, sum) rows: keys = rows, sums = rows + 1
+  const uint64_t* keys = rows;
+  const uint64_t* sums = rows ? rows + 1 : nullptr;
   SegOffsets so{};
   so.nseg = nseg;
   for (int t = 0; t < nseg; ++t) {
     if (seg_counts[t] < 0) {
-      rt::set_error("rt_coverage_power_segments: negative segment count");
+      rt::set_error("rt_coverage_power_packed: negative segment count");
       return RT_EINVAL;
     }
     so.off[t + 1] = so.off[t] + seg_counts[t];
   }
   const int64_t n = so.off[nseg];
-  if ((n > 0 && (!keys || !sums)) || n > ((int64_t)1 << 31) - 1) {
-    rt::set_error("rt_coverage_power_segments: invalid arguments");
+  if ((n > 0 && !rows) || n > ((int64_t)1 << 31) - 1) {
+    rt::set_error("rt_coverage_power_packed: invalid arguments");
     return RT_EINVAL;
   }
   hipStream_t s = (hipStream_t)stream;
@@ -3858,7 +3753,7 @@ static int power_segments_impl(rt_coverage* c, const uint64_t* keys, const uint6
     if (nseg <= 8) {
       OwnerRuns a{};
       a.keys = c->okeys_sorted;
-      a.val = SumVal{sums, idx_sorted, stride == 1 ? 3 : stride};
+      a.val = SumVal{sums, idx_sorted, stride};
       a.n = n;
       a.states = c->own_states;
       a.ticket = c->own_aux;
@@ -3884,7 +3779,7 @@ static int power_segments_impl(rt_coverage* c, const uint64_t* keys, const uint6
     } else {
       WideKey wk{};
       wk.identity = true;
-      rc = run_sums(c, SumVal{sums, idx_sorted, stride == 1 ? 3 : stride}, n, wk, s);
+      rc = run_sums(c, SumVal{sums, idx_sorted, stride}, n, wk, s);
     }
   } else {
     RT_HIP(hipMemsetAsync(c->nuniq, 0, 8, s));
@@ -3893,7 +3788,6 @@ static int power_segments_impl(rt_coverage* c, const uint64_t* keys, const uint6
   if (!rc) prof_mark(c, 7, s);
   return rc;
 }
-}  // namespace
 
 int rt_coverage_check(rt_coverage* c, int64_t* out, void* stream) {
   if (!c) {
@@ -3974,7 +3868,7 @@ int rt_coverage_last_profile(rt_coverage* c, double* out, int n) {
 int rt_coverage_received(rt_coverage* c, uint64_t* keys_out, double* amps_out, int64_t max_out, int64_t* n_out,
                          void* stream) {
   // the per-cell sparse impulse responses of the last run (rt_coverage_run, or this rank's cells
-  // after rt_coverage_power_records): (cell << 32 | bin, amplitude), ascending
+  // after its owner stage): (cell << 32 | bin, amplitude), ascending
   if (!c || !n_out) {
     rt::set_error("rt_coverage_received: invalid arguments");
     return RT_EINVAL;

@@ -8,11 +8,12 @@ Decompositions:
   rank (x-column cyclic: a strip of constant ix is wholly one rank's, so the candidate passes
   shrink with the rank count); every other rank leaves 0 in its power map and the maps are
   sum-reduced: ``reduce_sum`` again (NaN of an owner survives).
-* coverage rays -- rank r traces its share of every cell's rays (``ray_range``), sums its
-  first-win records per (cell, bin) and sends each record to the owner of its cell (the x-column
-  rule above): ``exchange_records``, one sparse all-to-all.  Owners sum what they receive (exact
-  fixed point, so the order is irrelevant), compute their cells' power, and the maps are
-  sum-reduced.
+* coverage rays -- rank r traces its share of every cell's rays (``ray_range``, or a wedge of
+  initial azimuth for "sectors" plans), sums its first-win records per (cell, bin) and sends each
+  record, one 32-B (key, exact sum) row, to the owner of its cell (the x-column rule above):
+  ``exchange_rows``, one sparse all-to-all.  Owners sum what they receive (exact fixed point, so
+  the order is irrelevant), compute their cells' power, and the maps are gathered
+  (``gather_power_map``).
 """
 from __future__ import annotations
 
@@ -182,37 +183,3 @@ def exchange_rows(rows, send_counts, group=None, recv_counts=None):
     out = torch.empty((sum(recv_counts), w), dtype=torch.int64, device=wire)
     dist.all_to_all_single(out, rows[:n].reshape(n, w).to(wire), recv_counts, send_counts, group=group)
     return out.to(home), recv_counts
-
-
-def exchange_records(keys, vals, send_counts, group=None, return_counts=False):
-    """Sparse all-to-all of coverage records: this rank's (key, value) pairs, grouped by
-    destination rank with send_counts[d] for rank d, go to their owners.  vals is (n,) float64
-    or (n, k) int64 (the exact fixed-point sums of Coverage.trace_records).  Returns the received
-    (keys int64, vals of the same dtype and width), concatenated in source-rank order.  Keys and
-    values travel as one (n, 1 + k) int64 buffer: one collective for the counts, one for the
-    records.  (gloo, used by the CPU tests, moves device tensors through host memory; "nccl" =
-    RCCL sends them device to device over xGMI.)  return_counts: also return the number of records
-    received from each rank (the segments Coverage.power_from_records merges)."""
-    import torch
-    import torch.distributed as dist
-    home = keys.device
-    wire = torch.device("cpu") if (home.type != "cpu" and dist.get_backend(group) == "gloo") else home
-    send_counts = [int(c) for c in send_counts]
-    n = sum(send_counts)
-    sc = torch.tensor(send_counts, dtype=torch.int64, device=wire)
-    rc = torch.empty_like(sc)
-    dist.all_to_all_single(rc, sc, group=group)
-    recv_counts = [int(c) for c in rc.tolist()]
-    v = vals[:n]
-    is_f64 = v.dim() == 1 and v.dtype == torch.float64
-    # explicit widths: reshape(0, -1) is ambiguous and raises when this rank sends nothing
-    vw = 1 if (is_f64 or v.dim() == 1) else int(v.shape[1])
-    v64 = v.contiguous().view(torch.int64).reshape(n, 1) if is_f64 else v.contiguous().reshape(n, vw).to(torch.int64)
-    width = 1 + vw
-    packed = torch.cat([keys[:n].view(torch.int64).reshape(n, 1), v64], dim=1).to(wire)
-    out = torch.empty((sum(recv_counts), width), dtype=torch.int64, device=wire)
-    dist.all_to_all_single(out, packed, recv_counts, send_counts, group=group)
-    out = out.to(home)
-    rv = out[:, 1:].contiguous()
-    res = (out[:, 0].contiguous(), (rv.view(torch.float64).reshape(-1) if is_f64 else rv))
-    return res + (recv_counts,) if return_counts else res

@@ -106,35 +106,30 @@ def _a2a_worker(rank, world, port, out):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    # rank r sends (r + d + 1) records to rank d: key = r*1000 + d*100 + i, amp = key / 7
+    # rank r sends (r + d + 1) rows to rank d: key = r*1000 + d*100 + i, sum words (key, 3 key, -key)
     counts = [rank + d + 1 for d in range(world)]
     keys = torch.tensor([rank * 1000 + d * 100 + i for d in range(world) for i in range(counts[d])], dtype=torch.int64)
-    amps = keys.to(torch.float64) / 7.0
-    k, a = rdist.exchange_records(keys, amps, counts)
-    # the fixed-point form of Coverage.trace_records: (n, 3) int64 sums travel with their keys
-    sums = torch.stack([keys, keys * 3, -keys], dim=1)
-    k3, s3 = rdist.exchange_records(keys, sums, counts)
-    assert k3.tolist() == k.tolist() and s3.shape == (len(k), 3)
-    assert s3[:, 0].tolist() == k.tolist() and (s3[:, 1] == 3 * s3[:, 0]).all() and (s3[:, 2] == -s3[:, 0]).all()
-    r4, rc = rdist.exchange_rows(torch.cat([keys.reshape(-1, 1), sums], dim=1), counts)
-    assert r4[:, 0].tolist() == k.tolist() and r4[:, 1:].tolist() == s3.tolist()
-    assert rc == [r + rank + 1 for r in range(world)]
-    out.put((rank, k.tolist(), a.tolist()))
+    rows = torch.stack([keys, keys, keys * 3, -keys], dim=1)  # Coverage.trace_rows' (n, 4) int64 layout
+    r4, rc = rdist.exchange_rows(rows, counts)
+    assert r4.shape == (sum(rc), 4) and rc == [r + rank + 1 for r in range(world)]
+    assert (r4[:, 1] == r4[:, 0]).all() and (r4[:, 2] == 3 * r4[:, 0]).all() and (r4[:, 3] == -r4[:, 0]).all()
+    out.put((rank, r4[:, 0].tolist(), rc))
     dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world", [2, 3])
-def test_exchange_records_routes_in_source_rank_order(world):
-    """dist.exchange_records (ray-sharded coverage): every owner receives its records from rank 0,
-    then rank 1, ... -- the ray order the per-(cell, bin) sums rely on -- with amplitudes bit-exact."""
+def test_exchange_rows_routes_in_source_rank_order(world):
+    """dist.exchange_rows (ray-sharded coverage): every owner receives its rows from rank 0, then
+    rank 1, ... -- one ascending segment per source, the owner stage's merge precondition -- with
+    every word intact, and the per-source counts."""
     q = mp.get_context("spawn").SimpleQueue()
     pc = mp.spawn(_a2a_worker, args=(world, _port(), q), nprocs=world, join=False)
-    got = dict((r, (k, a)) for r, k, a in (q.get() for _ in range(world)))
+    got = dict((r, (k, c)) for r, k, c in (q.get() for _ in range(world)))
     pc.join()
     for d in range(world):
         want = [r * 1000 + d * 100 + i for r in range(world) for i in range(r + d + 1)]
         assert got[d][0] == want
-        assert got[d][1] == [float(np.float64(x) / 7.0) for x in want]
+        assert got[d][1] == [r + d + 1 for r in range(world)]
 
 
 def test_ray_range_partitions_the_burst():
@@ -184,32 +179,23 @@ def _a2a_empty_worker(rank, world, port, out):
     counts = [0] * world if rank == 0 else [2] * world
     n = sum(counts)
     keys = torch.tensor([rank * 100 + d * 10 + i for d in range(world) for i in range(counts[d])], dtype=torch.int64)
-    sums = torch.stack([keys, keys + 1, keys + 2], dim=1) if n else torch.empty((0, 3), dtype=torch.int64)
-    amps = keys.to(torch.float64) / 3.0
-    k, s = rdist.exchange_records(keys, sums, counts)
-    k1, a1 = rdist.exchange_records(keys, amps, counts)
-    # the packed rows of Coverage.trace_rows: (n, 4) int64, sent as they are
-    rows = torch.cat([keys.reshape(-1, 1), sums], dim=1) if n else torch.empty((0, 4), dtype=torch.int64)
+    rows = torch.stack([keys, keys + 1, keys + 2, keys + 3], dim=1) if n else torch.empty((0, 4), dtype=torch.int64)
     r4, rc = rdist.exchange_rows(rows, counts)
-    assert r4.shape == (len(k), 4) and r4[:, 0].tolist() == k.tolist() and r4[:, 1:].tolist() == s.tolist()
     assert rc == [0] + [2] * (world - 1)
-    out.put((rank, k.tolist(), s.tolist(), k1.tolist(), a1.tolist()))
+    out.put((rank, r4.tolist()))
     dist.destroy_process_group()
 
 
-def test_exchange_records_with_an_empty_sender():
-    """a rank whose send counts are all zero must not break the record all-to-all."""
+def test_exchange_rows_with_an_empty_sender():
+    """a rank whose send counts are all zero must not break the row all-to-all."""
     world = 3
     q = mp.get_context("spawn").Queue()
     pc = mp.spawn(_a2a_empty_worker, args=(world, _port(), q), nprocs=world, join=False)
-    got = dict((r, rest) for r, *rest in (q.get(timeout=120) for _ in range(world)))
+    got = dict(q.get(timeout=120) for _ in range(world))
     pc.join()
     for d in range(world):
-        k, s, k1, a1 = got[d]
         want = [r * 100 + d * 10 + i for r in range(1, world) for i in range(2)]
-        assert k == want and k1 == want
-        assert s == [[x, x + 1, x + 2] for x in want]
-        assert a1 == [float(np.float64(x) / 3.0) for x in want]
+        assert got[d] == [[x, x + 1, x + 2, x + 3] for x in want]
 
 
 def _gather_map_worker(rank, world, port, out):

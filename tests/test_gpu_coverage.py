@@ -143,10 +143,13 @@ def test_coverage_on_bvh_terrain():
     cov.close()
 
 
-def _ray_sharded_rows(env, grid, tx, B, N, S, win=100e-9, env_mesh=None, mode="rays"):
-    """_ray_sharded through the packed path run() takes: trace_rows -> each owner's segments of
-    (key, sum) rows in source-rank order -> power_from_rows.  mode "sectors": the ranks' rays are
-    wedges of initial azimuth (rt_coverage_create_sectors) instead of ray-id ranges."""
+def _ray_sharded(env, grid, tx, B, N, S, win=100e-9, env_mesh=None, segments=True, mode="rays"):
+    """S ray-sharded plans in one process, through the path run() takes: trace_rows -> each
+    owner's (key, sum) rows in source-rank order (what the all-to-all delivers) -> power_from_rows,
+    and the owners' maps summed (what the power-map gather does across S GPUs).  segments: the
+    owners merge the per-source segments (rt_coverage_power_packed), else they sort the rows
+    (rt_coverage_power_rows).  mode "sectors": the ranks' rays are wedges of initial azimuth
+    (rt_coverage_create_sectors) instead of ray-id ranges."""
     plans = [Coverage(env, 2.998e8, 100e9, win, B, N, grid, shard_index=r, shard_count=S, shard_mode=mode,
                       env_mesh=env_mesh) for r in range(S)]
     sent = []
@@ -161,7 +164,7 @@ def _ray_sharded_rows(env, grid, tx, B, N, S, win=100e-9, env_mesh=None, mode="r
             off = sum(counts[:d])
             parts.append(rows[off:off + counts[d]])
             segs.append(counts[d])
-        total += p.power_from_rows(torch.cat(parts), segs)
+        total += p.power_from_rows(torch.cat(parts), segs if segments else None)
         p.check()
         irs.append(p.impulse_responses())
     for p in plans:
@@ -169,28 +172,7 @@ def _ray_sharded_rows(env, grid, tx, B, N, S, win=100e-9, env_mesh=None, mode="r
     return total.cpu().numpy(), irs
 
 
-def _ray_sharded(env, grid, tx, B, N, S, win=100e-9, env_mesh=None, segments=False):
-    """S ray-mode plans in one process: each traces its share of the rays for every cell, the
-    records are routed to their owners as the all-to-all would (source-rank order), every owner
-    computes its cells, and the maps are summed (what run() does across S GPUs).  segments: the
-    owners merge the per-source segments (rt_coverage_power_segments) instead of sorting."""
-    plans = [Coverage(env, 2.998e8, 100e9, win, B, N, grid, shard_index=r, shard_count=S, shard_mode="rays",
-                      env_mesh=env_mesh) for r in range(S)]
-    sent = [p.trace_records(tx, 1) for p in plans]
-    total = torch.zeros(grid.num_cells, dtype=torch.float64, device="cuda")
-    irs = []
-    for d, p in enumerate(plans):
-        ks, as_, segs = [], [], []
-        for keys, amps, counts in sent:  # source ranks in order
-            off = sum(counts[:d])
-            ks.append(keys[off:off + counts[d]])
-            as_.append(amps[off:off + counts[d]])
-            segs.append(counts[d])
-        total += p.power_from_records(torch.cat(ks), torch.cat(as_), segs if segments else None)
-        irs.append(p.impulse_responses())
-    for p in plans:
-        p.close()
-    return total.cpu().numpy(), irs
+_ray_sharded_rows = _ray_sharded
 
 
 @pytest.mark.parametrize("S", [1, 2, 3, 8])
@@ -256,9 +238,10 @@ def test_coverage_sector_sharded_bvh_terrain():
 @pytest.mark.parametrize("S", [1, 3, 8])
 def test_power_segments_equal_sorted_records(room, S):
     """The owner stage's segment merge (each source rank's records arrive sorted, merged by rank:
-    rt_coverage_power_segments) gives exactly the sorted path's maps and impulse responses."""
+    rt_coverage_power_packed) gives exactly the sorted path's (rt_coverage_power_rows) maps and
+    impulse responses."""
     grid, tx, B, N = CoverageGrid(8.0, -2.5, 4.6, 0.37, 0.41, 0.4, 13, 12, 2), (10, 0, 5), 3, 60_000
-    t_sort, irs_sort = _ray_sharded(room, grid, tx, B, N, S)
+    t_sort, irs_sort = _ray_sharded(room, grid, tx, B, N, S, segments=False)
     t_merge, irs_merge = _ray_sharded(room, grid, tx, B, N, S, segments=True)
     assert t_sort.tobytes() == t_merge.tobytes()
     assert np.isfinite(t_sort).sum() >= 20
@@ -267,31 +250,14 @@ def test_power_segments_equal_sorted_records(room, S):
             assert x.tobytes() == y.tobytes()
 
 
-@pytest.mark.parametrize("S", [1, 3, 8])
-def test_packed_rows_equal_records(room, S):
-    """trace_rows / power_from_rows (one 32-B row per record, sent as it is) give exactly the
-    maps and impulse responses of the separate key and sum buffers."""
-    grid, tx, B, N = CoverageGrid(8.0, -2.5, 4.6, 0.37, 0.41, 0.4, 13, 12, 2), (10, 0, 5), 3, 60_000
-    t_rec, irs_rec = _ray_sharded(room, grid, tx, B, N, S, segments=True)
-    t_rows, irs_rows = _ray_sharded_rows(room, grid, tx, B, N, S)
-    assert t_rec.tobytes() == t_rows.tobytes()
-    assert np.isfinite(t_rec).sum() >= 20
-    for a, b in zip(irs_rec, irs_rows):
-        for x, y in zip(a, b):
-            assert x.tobytes() == y.tobytes()
-
-
-def test_trace_rows_match_records_and_grow(room):
-    """trace_rows holds the same (key, sum) records as trace_records, row by row; a buffer too small
-    for them is grown and the trace repeated, with the same rows."""
+def test_trace_rows_grow(room):
+    """A row buffer too small for a trace stage's rows is grown and the rows fetched from the plan
+    (rt_coverage_records_packed, no second trace): the same rows, in the same order."""
     grid, tx, B, N = CoverageGrid(8.0, -2.5, 4.6, 0.37, 0.41, 0.4, 13, 12, 2), (10, 0, 5), 3, 60_000
     p = Coverage(room, 2.998e8, 100e9, 100e-9, B, N, grid, shard_index=2, shard_count=3, shard_mode="rays")
-    k, sm, c = p.trace_records(tx, 1)
-    k, sm = k.cpu().numpy(), sm.cpu().numpy()
-    rows, c2 = p.trace_rows(tx, 1)
+    rows, c = p.trace_rows(tx, 1)
     r = rows.cpu().numpy()
-    assert c == c2 and sum(c) > 100
-    assert r[:, 0].tobytes() == k.tobytes() and np.ascontiguousarray(r[:, 1:]).tobytes() == sm.tobytes()
+    assert sum(c) > 100
     p._rows = torch.empty((1, 4), dtype=torch.int64, device="cuda")
     rows3, c3 = p.trace_rows(tx, 1)
     assert c3 == c and p._rows.shape[0] > 1
@@ -325,11 +291,11 @@ def test_coverage_ray_sharded_bvh_terrain():
     np.testing.assert_array_equal(total, whole)
 
 
-def test_power_from_records_every_sweep_path(room):
+def test_power_from_rows_every_sweep_path(room):
     """The closed-form power of k_power_small (<= 16 bins), k_power's LDS event sweep (17..192) and
     its range-split sweep (> 192; no full-size map cell has that many) against np.convolve, fed
-    through rt_coverage_power_records (fixed-point sums from rt_coverage_amps_to_sums) with synthetic
-    per-cell impulse responses."""
+    through rt_coverage_power_rows (rows of fixed-point sums from rt_coverage_amps_to_sums) with
+    synthetic per-cell impulse responses."""
     rng = np.random.default_rng(8)
     sizes = [0, 1, 2, 5, 16, 17, 64, 191, 192, 193, 400, 2500, 9999]
     grid = CoverageGrid(0.0, 0.0, 5.0, 1.0, 1.0, 1.0, len(sizes), 1, 1)
@@ -383,28 +349,10 @@ def test_fixed_point_bin_sums_are_exact(room):
         assert x == float(exact[(int(cc), int(bb))] * unit), (cc, bb)
 
 
-def test_trace_records_into_small_buffers_falls_back(room):
-    """Coverage.trace_records hands its grow-only buffers to rt_coverage_trace_records_to, which fills
-    them before it synchronizes; when they are too small it says so and the records come from
-    rt_coverage_records into larger ones -- the same records either way."""
-    grid, tx, B, N = CoverageGrid(8.0, -2.5, 4.6, 0.37, 0.41, 0.4, 13, 12, 2), (10, 0, 5), 3, 60_000
-    p = Coverage(room, 2.998e8, 100e9, 100e-9, B, N, grid, shard_index=1, shard_count=3, shard_mode="rays")
-    k1, s1, c1 = p.trace_records(tx, 1)
-    k1, s1 = k1.clone(), s1.clone()
-    assert sum(c1) > 100
-    p._rec = (torch.empty(1, dtype=torch.int64, device="cuda"), torch.empty((1, 3), dtype=torch.int64, device="cuda"))
-    k2, s2, c2 = p.trace_records(tx, 1)
-    assert c1 == c2 and p._rec[0].numel() > 1
-    assert k1.cpu().numpy().tobytes() == k2.cpu().numpy().tobytes()
-    assert s1.cpu().numpy().tobytes() == s2.cpu().numpy().tobytes()
-    p.close()
-
-
 def test_trace_rows_into_small_buffer_fetches_packed(room):
-    """Coverage.trace_rows with a too-small row buffer: rt_coverage_trace_records_packed reports it,
+    """Coverage.trace_rows with a too-small row buffer: rt_coverage_trace_rows_finish reports it,
     and the rows come from rt_coverage_records_packed (no second trace) -- the same rows, in the
-    same order, as with a buffer that was large enough; and the same rows as trace_records' keys
-    and sums."""
+    same order, as with a buffer that was large enough."""
     grid, tx, B, N = CoverageGrid(8.0, -2.5, 4.6, 0.37, 0.41, 0.4, 13, 12, 2), (10, 0, 5), 3, 60_000
     p = Coverage(room, 2.998e8, 100e9, 100e-9, B, N, grid, shard_index=0, shard_count=2, shard_mode="rays")
     r1, c1 = p.trace_rows(tx, 1)
@@ -414,17 +362,13 @@ def test_trace_rows_into_small_buffer_fetches_packed(room):
     r2, c2 = p.trace_rows(tx, 1)
     assert c1 == c2 and p._rows.shape[0] >= sum(c1)
     assert r1.cpu().numpy().tobytes() == r2.cpu().numpy().tobytes()
-    k, s, c3 = p.trace_records(tx, 1)
-    assert c3 == c1
-    assert np.array_equal(r1[:, 0].cpu().numpy(), k.cpu().numpy())
-    assert np.array_equal(r1[:, 1:].cpu().numpy(), s.cpu().numpy())
     p.close()
 
 
 def _owner_segments_case(room, nseg, sizes, seed):
-    """rt_coverage_power_segments on `sizes[c]` random bins per cell c of an nx x 1 x 1 grid, each
+    """rt_coverage_power_packed on `sizes[c]` random bins per cell c of an nx x 1 x 1 grid, each
     (cell, bin)'s fixed-point amplitude split over up to 3 of nseg source segments (each segment in
-    key order), against the sorted path (rt_coverage_power_records) on the same records: maps and
+    key order), against the sorted path (rt_coverage_power_rows) on the same rows: maps and
     impulse responses bit for bit."""
     rng = np.random.default_rng(seed)
     grid = CoverageGrid(0.0, 0.0, 5.0, 1.0, 1.0, 1.0, len(sizes), 1, 1)
@@ -459,9 +403,10 @@ def _owner_segments_case(room, nseg, sizes, seed):
         s_all += [r[1] for r in rows]
     kt = torch.from_numpy(np.array(k_all, np.uint64).view(np.int64)).cuda()
     st = torch.from_numpy(np.array(s_all, np.uint64).reshape(-1, 3).view(np.int64)).cuda()
-    got = cov.power_from_records(kt, st, counts).cpu().numpy().copy()
+    rows = torch.cat([kt.reshape(-1, 1), st], dim=1).contiguous()
+    got = cov.power_from_rows(rows, counts).cpu().numpy().copy()
     gi = cov.impulse_responses()
-    ref = cov.power_from_records(kt, st).cpu().numpy().copy()
+    ref = cov.power_from_rows(rows).cpu().numpy().copy()
     ri = cov.impulse_responses()
     cov.close()
     assert got.tobytes() == ref.tobytes()
@@ -640,3 +585,18 @@ def test_whole_map_sort_after_regrowth_short_list(room):
         cov.close()
     finally:
         check(L.rt_debug_replay_window_max(-1))
+
+
+def test_bench_exits_nonzero_on_an_unordered_segment():
+    """bench.py validates its own coverage maps: after the timed maps it asks the plan for the
+    device-side error report (Coverage.check), so a received segment out of key order (the owner
+    stage's precondition, broken on purpose by --debug-unordered-rows: two rows of a segment
+    swapped) ends the run with a non-zero status instead of a rate for a wrong map."""
+    import subprocess
+    import sys
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--legs", "k2,k3", "--steps", "2", "--warmup", "1",
+           "--settle-steps", "0", "--no-cpu-baseline", "--coverage-grid", "32", "--coverage-rays", "50000",
+           "--coverage-runs", "1", "--rays", "100000", "--debug-unordered-rows"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=REPO)
+    assert r.returncode != 0, r.stdout[-2000:]
+    assert "out of key order" in r.stderr, r.stderr[-2000:]

@@ -145,11 +145,13 @@ def _nccl_worker(q, port):
     paths, ir = t.compute_cir_distributed((10.0, 0.0, 5.0), 1, (6.0, 2.0, 5.0), 0.1)
     grid = CoverageGrid(8.0, -2.5, 4.6, 0.37, 0.41, 0.4, 13, 12, 2)
     cov = Coverage(_scene(), 2.998e8, 100e9, 100e-9, B, 60_000, grid, device=0, shard_mode="rays")
-    keys, amps, counts = cov.trace_records((10.0, 0.0, 5.0), 1)
-    k2, a2 = rdist.exchange_records(keys, amps, counts)  # RCCL all-to-all (world 1)
-    p = cov.power_from_records(k2, a2)
+    rows, counts = cov.trace_rows((10.0, 0.0, 5.0), 1)
+    rows = rows.clone()
+    r2, c2 = rdist.exchange_rows(rows, counts)  # RCCL all-to-all (world 1)
+    p = cov.power_from_rows(r2, c2)
+    cov.check()
     dist.all_reduce(p)
-    q.put(([pp.tolist() for pp in paths], ir, p.cpu().numpy(), bool(torch.equal(k2, keys))))
+    q.put(([pp.tolist() for pp in paths], ir, p.cpu().numpy(), bool(torch.equal(r2, rows))))
     dist.destroy_process_group()
 
 

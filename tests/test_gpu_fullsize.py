@@ -192,18 +192,9 @@ def test_k3_ray_sharded_equals_whole_at_full_size(W):
     whole.close()
     plans = [Coverage(room, 2.998e8, 100e9, win, B, N, grid, 0.1, device=0, shard_index=r, shard_count=W,
                       shard_mode="rays") for r in range(W)]
-    sent = []
+    got, _ = _ray_sharded_map(plans, tx, grid.num_cells)
     for p in plans:
-        k, a, counts = p.trace_records(tx, 1)
-        offs = np.concatenate([[0], np.cumsum(counts)])
-        sent.append([(k[offs[d]:offs[d + 1]].clone(), a[offs[d]:offs[d + 1]].clone()) for d in range(W)])
-    total = torch.zeros(grid.num_cells, dtype=torch.float64, device="cuda:0")
-    for d, p in enumerate(plans):
-        keys = torch.cat([sent[r][d][0] for r in range(W)])
-        sums = torch.cat([sent[r][d][1] for r in range(W)])
-        total += p.power_from_records(keys, sums)
         p.close()
-    got = total.cpu().numpy()
     np.testing.assert_array_equal(got, ref)  # NaN where the whole map has NaN, every other bit equal
 
 
@@ -247,21 +238,21 @@ def test_dense_compute_cir_is_deterministic_and_in_ray_order():
 
 def _ray_sharded_map(plans, tx, num_cells):
     """All W rank plans of a ray-sharded map on this GPU, the all-to-all done in process: rank r's
-    records for owner d are concatenated in source-rank order, as dist.exchange_records delivers them."""
+    rows for owner d are concatenated in source-rank order, as dist.exchange_rows delivers them."""
     W = len(plans)
     sent = []
     for p in plans:
-        k, a, counts = p.trace_records(tx, 1)
+        rows, counts = p.trace_rows(tx, 1)
         offs = np.concatenate([[0], np.cumsum(counts)])
-        sent.append([(k[offs[d]:offs[d + 1]].clone(), a[offs[d]:offs[d + 1]].clone()) for d in range(W)])
+        sent.append([rows[offs[d]:offs[d + 1]].clone() for d in range(W)])
     total = torch.zeros(num_cells, dtype=torch.float64, device="cuda:0")
     nrec = []
     for d, p in enumerate(plans):
-        keys = torch.cat([sent[r][d][0] for r in range(W)])
-        sums = torch.cat([sent[r][d][1] for r in range(W)])
-        nrec.append(int(keys.numel()))
-        # per-source segments merged by rank, as Coverage.run_device does after exchange_records
-        total += p.power_from_records(keys, sums, [int(sent[r][d][0].numel()) for r in range(W)])
+        rows = torch.cat([sent[r][d] for r in range(W)])
+        nrec.append(int(rows.shape[0]))
+        # per-source segments merged by rank, as Coverage.run_device does after exchange_rows
+        total += p.power_from_rows(rows, [int(sent[r][d].shape[0]) for r in range(W)])
+        p.check()
     return total.cpu().numpy(), nrec
 
 

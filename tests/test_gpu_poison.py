@@ -98,13 +98,13 @@ def test_poisoned_buffers_do_not_change_ray_sharded_coverage():
                           shard_count=W, shard_mode="rays") for r in range(W)]
         sent = []
         for pl in plans:
-            k, a, counts = pl.trace_records(tx, 1)
+            rows, counts = pl.trace_rows(tx, 1)
             o = np.concatenate([[0], np.cumsum(counts)])
-            sent.append([(k[o[d]:o[d + 1]].clone(), a[o[d]:o[d + 1]].clone()) for d in range(W)])
+            sent.append([rows[o[d]:o[d + 1]].clone() for d in range(W)])
         tot = torch.zeros(grid.num_cells, dtype=torch.float64, device="cuda:0")
         for d, pl in enumerate(plans):
-            tot += pl.power_from_records(torch.cat([sent[r][d][0] for r in range(W)]),
-                                         torch.cat([sent[r][d][1] for r in range(W)]))
+            tot += pl.power_from_rows(torch.cat([sent[r][d] for r in range(W)]), [len(sent[r][d]) for r in range(W)])
+            pl.check()
             pl.close()
         return tot.cpu().numpy()
 
@@ -130,8 +130,8 @@ def test_poisoned_overflowing_first_run_of_a_rank_plan():
     def records():
         pl = Coverage(room, 2.998e8, 100e9, win, 3, 1_000_000, grid, 0.1, device=0, shard_index=r, shard_count=W,
                       shard_mode="rays")
-        k, a, counts = pl.trace_records(tx, 1)
-        out = (k.cpu().numpy().copy(), a.cpu().numpy().copy(), list(counts), pl.last_candidates)
+        rows, counts = pl.trace_rows(tx, 1)
+        out = (rows[:, 0].cpu().numpy().copy(), rows[:, 1:].cpu().numpy().copy(), list(counts), pl.last_candidates)
         pl.close()
         return out
 

@@ -69,36 +69,23 @@ def rays_case(case, m, grid, tx, win, B, env, S, reps, mode="rays"):
     best = None
     for _ in range(reps + 1):  # first pass warms up
         sent, t_trace = [], []
-        rows_path = not os.environ.get("RECORDS") and not os.environ.get("OWNER_SORT")
         for p in plans:
-            # run()'s path: packed (key, sum) rows (RECORDS=1: separate key and sum buffers)
-            out, dt = timed(lambda: p.trace_rows(tx, 1) if rows_path else p.trace_records(tx, 1))
+            # run()'s path: packed (key, sum) rows
+            out, dt = timed(lambda: p.trace_rows(tx, 1))
             sent.append(out)
             t_trace.append(dt)
         t_own, nrec = [], []
         for d, p in enumerate(plans):
-            if rows_path:
-                parts, segs = [], []
-                for rows, counts in sent:
-                    off = sum(counts[:d])
-                    parts.append(rows[off:off + counts[d]])
-                    segs.append(counts[d])
-                r = torch.cat(parts)
-                nrec.append(int(r.shape[0]))
-                # the received rows as exchange_rows delivers them: one sorted segment per source
-                _, dt = timed(lambda: p.power_from_rows(r, segs))
-                t_own.append(dt)
-                continue
-            ks, as_, segs = [], [], []
-            for keys, amps, counts in sent:
+            parts, segs = [], []
+            for rows, counts in sent:
                 off = sum(counts[:d])
-                ks.append(keys[off:off + counts[d]])
-                as_.append(amps[off:off + counts[d]])
+                parts.append(rows[off:off + counts[d]])
                 segs.append(counts[d])
-            k, a = torch.cat(ks), torch.cat(as_)
-            nrec.append(int(k.numel()))
-            # the received records as exchange_records delivers them: one sorted segment per source
-            _, dt = timed(lambda: p.power_from_records(k, a, None if os.environ.get("OWNER_SORT") else segs))
+            r = torch.cat(parts)
+            nrec.append(int(r.shape[0]))
+            # the received rows as exchange_rows delivers them: one sorted segment per source
+            # (OWNER_SORT=1: sorted instead, rt_coverage_power_rows)
+            _, dt = timed(lambda: p.power_from_rows(r, None if os.environ.get("OWNER_SORT") else segs))
             t_own.append(dt)
         per_rank = [a + b for a, b in zip(t_trace, t_own)]
         if best is None or max(per_rank) < max(best[0]):

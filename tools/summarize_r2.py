@@ -45,13 +45,21 @@ def short(name):
 
 
 def counters(base):
-    """{short kernel: {counter: mean per dispatch}} over every pass directory."""
+    """{short kernel: {counter: mean per dispatch}} over every pass directory.  k_fill_received
+    serves both the K2 and the K4 step (different sizes): each of its dispatches is attributed to
+    the trace kernel dispatched right after it on the same pass ("k_fill_received@k2" before
+    k_trace_bf<3>, "@k4" before k_trace_bvh<5>), so each leg's traffic adds its own fill."""
     acc = defaultdict(lambda: defaultdict(dict))  # kernel -> counter -> dispatch -> value
     for f in glob.glob(os.path.join(base, "p*", "**", "*counter_collection.csv"), recursive=True):
-        for r in csv.DictReader(open(f)):
+        rows = list(csv.DictReader(open(f)))
+        names = {int(r["Dispatch_Id"]): short(r["Kernel_Name"]) for r in rows}
+        for r in rows:
             k = short(r["Kernel_Name"])
             if k is None:
                 continue
+            if k == "k_fill_received":
+                nxt = names.get(int(r["Dispatch_Id"]) + 1)
+                k = {"k_trace_bf<3>": "k_fill_received@k2", "k_trace_bvh<5>": "k_fill_received@k4"}.get(nxt, k)
             d = acc[k][r["Counter_Name"]]
             key = (f, r["Dispatch_Id"])
             d[key] = d.get(key, 0.0) + float(r["Counter_Value"])
@@ -97,17 +105,28 @@ def main(tag, note=""):
             for k, v in out["kernels"].items() if "hbm_bytes_per_launch" in v}
     # a K4 step is the coalesced NaN / 0 fill of received and row_mask, then the trace kernel (which
     # stores only the received rows): the leg's traffic is both launches' bytes
-    if "k_trace_bvh<5>" in legs and "k_fill_received" in legs:
-        t, f = legs["k_trace_bvh<5>"], legs["k_fill_received"]
-        t["hbm_bytes_per_launch"] += f["hbm_bytes_per_launch"]
-        t["note"] = (t["note"] + "; " if t["note"] else "") + "k_trace_bvh<5> + k_fill_received"
+    for trace, fill in (("k_trace_bvh<5>", "k_fill_received@k4"), ("k_trace_bf<3>", "k_fill_received@k2")):
+        if trace in legs and fill in legs:
+            t, f = legs[trace], legs[fill]
+            t["trace_kernel_bytes_per_launch"] = t["hbm_bytes_per_launch"]
+            t["fill_bytes_per_launch"] = f["hbm_bytes_per_launch"]
+            t["hbm_bytes_per_launch"] += f["hbm_bytes_per_launch"]
+            t["note"] = (t["note"] + "; " if t["note"] else "") + f"{trace} + its {fill}"
     json.dump(legs, open(os.path.join(ROOT, "profiles", "traffic_legs.json"), "w"), indent=1)
     k2 = out["kernels"].get("k_trace_bf<3>", {})
     if "hbm_bytes_per_launch" in k2:
         c = k2["counters"]
-        json.dump({"kernel": "k_trace_bf<3, false>", "rays": 1_000_000, "bounces": 3,
+        fill = out["kernels"].get("k_fill_received@k2", {})
+        fb = fill.get("hbm_bytes_per_launch")
+        # the K2 step's span (bench roofline: HIP events from the fill's start to the trace kernel's
+        # end) covers both launches, so its traffic is both launches' bytes
+        json.dump({"kernel": "k_fill_received + k_trace_bf<3, false>", "rays": 1_000_000, "bounces": 3,
                    "how": out["how"], "fetch_size_kb_per_launch": c["FETCH_SIZE"],
-                   "write_size_kb_per_launch": c["WRITE_SIZE"], "hbm_bytes_per_launch": k2["hbm_bytes_per_launch"],
+                   "write_size_kb_per_launch": c["WRITE_SIZE"],
+                   "trace_kernel_bytes_per_launch": k2["hbm_bytes_per_launch"],
+                   "fill_bytes_per_launch": fb,
+                   "fill_counters": fill.get("counters"),
+                   "hbm_bytes_per_launch": k2["hbm_bytes_per_launch"] + (fb or 0.0),
                    "algorithmic_bytes_per_launch": 1_000_000 * (24 * 4 + 4), "tag": tag},
                   open(os.path.join(ROOT, "profiles", "traffic_k2.json"), "w"), indent=1)
         if "SQ_INSTS_VALU" in c:
