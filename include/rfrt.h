@@ -56,6 +56,13 @@ int rt_mesh_info(const rt_mesh* mesh, int64_t* nf, float* bounds6, float* sphere
  * counterpart: Warp's wp.Mesh BVH (tracer.py:24) is internal. */
 int rt_bvh_info(const rt_mesh* mesh, int64_t* info4);
 
+/* rt_trace keeps, per process, up to 8 direction-sorted ray orders (per device, ray_offset and n:
+ * 4 bytes per ray) and up to 8 chunk schedules (per device, burst, meshes and TX; a mesh's are
+ * dropped by rt_mesh_destroy).  This frees all of them (the next rt_trace recomputes what it needs;
+ * no result depends on them).  Synchronises the devices it frees memory on.  No reference
+ * counterpart (Warp keeps no such state). */
+int rt_release_caches(void);
+
 /* Replaces wp.launch(kernel.trace_paths_kernel, dim=(n,1,1), inputs=[env.id, tx_pos, rx.id,
  * max_bounces, traced_paths, received_paths, row_mask]) -- tracer.py:75-79, kernel.py:38-98.
  * Traces global ray ids [ray_offset, ray_offset+n) (ray id = Warp tid; sharding keeps ids global).

@@ -77,6 +77,7 @@ def lib():
     L.rt_coverage_trace_rows_finish.argtypes = [_vp, _vp, _vp, _vp]
     L.rt_coverage_last_profile.argtypes = [_vp, _vp, _int]
     L.rt_debug_poison.argtypes = [_int]
+    L.rt_release_caches.argtypes = []
     L.rt_debug_replay_window_max.argtypes = [_i64]
     L.rt_profile.argtypes = [_int]
     L.rt_trace_last_profile.argtypes = [_vp, _int]
@@ -92,7 +93,7 @@ def lib():
                  "rt_coverage_power_rows",
                  "rt_coverage_power_packed", "rt_coverage_amps_to_sums", "rt_coverage_profile", "rt_coverage_check",
                  "rt_coverage_trace_rows_async", "rt_coverage_trace_rows_finish",
-                 "rt_coverage_last_profile", "rt_debug_poison", "rt_debug_replay_window_max",
+                 "rt_coverage_last_profile", "rt_debug_poison", "rt_debug_replay_window_max", "rt_release_caches",
                  "rt_profile", "rt_trace_last_profile", "rt_trace_profile_stats",
                  "rt_power_dense", "rt_selftest_math", "rt_ray_dirs", "rt_query", "rt_selftest_fx"):
         if hasattr(L, name):

@@ -226,6 +226,11 @@ int rt_mesh_create_ex(int device, const float* vertices, int64_t nv, const int32
   return RT_OK;
 }
 
+int rt_release_caches(void) {
+  rt::release_trace_caches();
+  return RT_OK;
+}
+
 int rt_mesh_destroy(rt_mesh* m) {
   if (!m) return RT_OK;
   rt::DeviceGuard dg(m->device);

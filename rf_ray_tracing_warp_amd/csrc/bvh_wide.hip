@@ -2,7 +2,10 @@
 // nodes for rt::Walk4 (rt_bvh.h).  Host pass over the device tree: every wide node takes the
 // children of one binary node and keeps opening its largest inner child (surface area) until it
 // has four, or until opening more would let the walk's stack bound exceed RT_BVH_STACK; nodes are
-// numbered breadth first, so the top levels are contiguous from node 0.
+// numbered breadth first, so the top levels are contiguous from node 0.  (A depth-first preorder
+// numbering was bit-identical and no faster -- K4 rt_trace 721-724 us either way, K5 map 3.31 vs
+// 3.27 ms, profiles/r6d_*_bvh_dfs_layout_ab.jsonl: a node is exactly one 128-B line, so renumbering
+// changes which lines neighbour each other, not how many distinct lines a wave touches.)
 // The child boxes and leaf references are copied bit for bit from the binary nodes, so culling
 // is exactly as conservative as the binary traversal's.
 #include <math.h>

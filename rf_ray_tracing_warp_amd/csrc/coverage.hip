@@ -2661,7 +2661,6 @@ using OnesweepCfg =
                                         rocprim::block_radix_rank_algorithm::match>;
 using OnesweepOnly = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, OnesweepCfg, 0>;
 constexpr int64_t kOnesweepMinItems = 300000;
-bool onesweep_fused();
 
 // rocPRIM's Onesweep with its host loop rewritten (the kernels are rocPRIM's own, rocprim::detail, so
 // the sort is the same): rocPRIM's driver fills the digit histogram, then before every pass the
@@ -2765,7 +2764,7 @@ hipError_t sort_records(void* tmp, size_t& bytes, const uint64_t* kin, uint64_t*
                         int64_t n, int end_bit, hipStream_t s) {
   if (n >= kOnesweepMinItems) {
     // rocPRIM's Onesweep kernels with one fill (onesweep_pairs); one batch: rocPRIM splits at 2^30
-    if (onesweep_fused() && n < ((int64_t)1 << 30)) {
+    if (n < ((int64_t)1 << 30)) {
       if (!tmp) {  // the workspace of either driver (the plan sizes it once for both)
         size_t b1 = 0, b2 = 0;
         hipError_t e =
@@ -2897,13 +2896,6 @@ int64_t traj_split_max_rays() {
     return e ? (int64_t)atoll(e) : (int64_t)262144;
   }();
   return v;
-}
-
-// record sorts through onesweep_pairs (default) or rocPRIM's own Onesweep driver (RFRT_ONESWEEP_FUSED=0,
-// for A/B checks); read at every call
-bool onesweep_fused() {
-  const char* e = getenv("RFRT_ONESWEEP_FUSED");
-  return !(e && e[0] == '0');
 }
 
 // replay on BVH scenes: the environment traversal culled at the receiver's t (default), or not

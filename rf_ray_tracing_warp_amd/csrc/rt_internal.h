@@ -91,6 +91,7 @@ int build_wide(rt_mesh* m);
 // schedules of a mesh that is being destroyed (trace.hip)
 uint64_t next_mesh_gen();
 void forget_mesh_schedules(uint64_t gen);
+void release_trace_caches();
 // rt_trace's launch (trace.hip).  fused (rt_trace_cir, optional): the brute-force kernels finish
 // the CIR step in their last block (rt_cir.h); *fused_done tells whether this launch did.
 struct TraceCirFused;

@@ -1086,6 +1086,27 @@ uint64_t next_mesh_gen() {
   return ++g;
 }
 
+// rt_release_caches: every cached ray order and chunk schedule of every device (entries still in
+// flight on another thread are left to finish).  hipFree waits for the device.
+void release_trace_caches() {
+  {
+    std::lock_guard<std::mutex> lock(g_sched_mu);
+    for (SchedEntry& e : g_sched)
+      if (e.sched && e.valid) drop_entry(e);
+  }
+  std::lock_guard<std::mutex> lock(g_order_mu);
+  int cur = -1;
+  (void)hipGetDevice(&cur);
+  for (OrderEntry& e : g_orders)
+    if (e.order) {
+      if (e.device != cur) (void)hipSetDevice(e.device);
+      (void)hipFree(e.order);
+      if (e.ready) (void)hipEventDestroy(e.ready);
+      e = OrderEntry{};
+    }
+  if (cur >= 0) (void)hipSetDevice(cur);
+}
+
 void forget_mesh_schedules(uint64_t gen) {
   std::lock_guard<std::mutex> lock(g_sched_mu);
   for (SchedEntry& e : g_sched)

@@ -437,3 +437,16 @@ def test_trace_k4_terrain_full_mesh():
     g = _gpu_trace(t, rxm, tx, B, 3_000_000, n, want_traced=True, reps=2)
     o = orc.trace(orc.Mesh(t.vertices, t.faces), orc.Mesh(rxm.vertices, rxm.faces), tx, B, 3_000_000, n)
     _assert_trace_equal(g, o)
+
+
+def test_release_caches_between_traces(room):
+    """rt_release_caches frees the cached ray orders and chunk schedules: the next
+    launch recomputes them and every output bit is the same; destroying a mesh drops its own
+    schedules (keyed by the mesh's process-unique id, not its address)."""
+    rxm = sphere((6, 1, 5), 1.0, 1)
+    a = _gpu_trace(room, rxm, (10, 0, 5), 3, 0, 100_000, reps=2)
+    check(lib().rt_release_caches())
+    b = _gpu_trace(room, rxm, (10, 0, 5), 3, 0, 100_000, reps=2)
+    for k in a:
+        if a[k] is not None:
+            assert a[k].tobytes() == b[k].tobytes(), k
