@@ -73,8 +73,9 @@ def parse():
     ap.add_argument("--coverage-grid", type=int, default=256, help="K3: n x n receiver cells at z=5 on room.stl")
     ap.add_argument("--coverage-rays", type=int, default=1_000_000)
     ap.add_argument("--coverage-runs", type=int, default=3)
-    ap.add_argument("--coverage-shard", choices=("rays", "cells"), default="rays",
-                    help="N>1 coverage decomposition: ray shards + record all-to-all, or x-column cell shards")
+    ap.add_argument("--coverage-shard", choices=("sectors", "rays", "cells"), default="sectors",
+                    help="N>1 coverage decomposition: ray shards by initial azimuth (four interleaved wedges per "
+                         "GPU) or by ray-id range, each with a record all-to-all, or x-column cell shards")
     ap.add_argument("--no-validate", action="store_true",
                     help="N>1: skip rank 0's one-GPU reference map (the N-rank map is compared with it bit for bit)")
     ap.add_argument("--debug-unordered-rows", action="store_true",
@@ -306,9 +307,10 @@ def cpu_baseline_k5(args, terr, info):
 def shard_desc(mode, world):
     if world == 1:
         return "1 GPU"
-    if mode == "rays":
-        return (f"rays sharded x{world} (1/{world} of every cell's rays per GPU), (cell, bin, amplitude) records "
-                f"to the cells' owners (ix % {world}) by one RCCL all-to-all, RCCL sum of the power map")
+    if mode in ("rays", "sectors"):
+        how = "four interleaved wedges of initial azimuth" if mode == "sectors" else "a ray-id range"
+        return (f"rays sharded x{world} (1/{world} of every cell's rays per GPU: {how}), (cell, bin, amplitude) "
+                f"records to the cells' owners (ix % {world}) by one RCCL all-to-all, RCCL gather of the power map")
     return f"cells sharded by x column (ix % {world}), every GPU traces all rays, RCCL sum of the power map"
 
 

@@ -154,10 +154,11 @@ int rt_coverage_create_rays(int device, const rt_mesh* env, int max_bounces, int
                             int64_t n_rays, const rt_grid* grid, double rx_radius, int rank, int world,
                             rt_coverage** out);
 /* rt_coverage_create_rays with the rays chosen by direction instead of by id: the burst of
- * n_rays_total rays sorted by the azimuth of each ray's initial direction (kernel.py:51-52), rank r
- * taking positions [r n / world, (r+1) n / world) of that order -- a wedge of directions around the
- * transmitter, so that the rank's trajectories, candidates and replays stay in one sector of the
- * scene.  Any partition of the rays gives the same map bit for bit (exact fixed-point sums). */
+ * n_rays_total rays sorted by the azimuth of each ray's initial direction (kernel.py:51-52) and cut
+ * into 4 x world equal pieces, rank r taking pieces r, r + world, r + 2 world, r + 3 world -- four
+ * wedges of directions around the transmitter, so that the rank's trajectories, candidates and
+ * replays stay in few sectors of the scene while the ranks stay balanced.  Any partition of the
+ * rays gives the same map bit for bit (exact fixed-point sums). */
 int rt_coverage_create_sectors(int device, const rt_mesh* env, int max_bounces, int64_t n_rays_total,
                                const rt_grid* grid, double rx_radius, int rank, int world, rt_coverage** out);
 /* The trace stage in two halves, so a rank can exchange its send counts on the device (the RCCL

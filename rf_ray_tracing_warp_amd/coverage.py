@@ -4,10 +4,11 @@ coverage.py:38-57 loops over receiver positions, runs ``Tracer.compute_cir`` for
 impulse response into a received signal power (coverage.py:45-52), then dBm.  ``Coverage`` computes
 the same per-cell power for a whole lattice of receivers in one shot (csrc/coverage.hip, exact
 shared-trajectory algorithm).  Across ranks (one process per GPU) the work is split either by rays
-(``shard_mode="rays"``, the default of ``coverage_map``: every rank traces its share of each cell's
+(``shard_mode="rays"``: every rank traces its share of each cell's
 rays, records go to the cells' owners in one sparse all-to-all) or by cells (``"cells"``: every
-rank traces all rays for its x columns); the power map is then sum-reduced over the process group
-(RCCL over xGMI with the "nccl" backend).
+rank traces all rays for its x columns); "sectors" (the default of ``coverage_map``) is "rays" with
+each rank's rays chosen as four interleaved wedges of initial azimuth instead of an id range.  The
+power map is then gathered over the process group (RCCL over xGMI with the "nccl" backend).
 
     grid = CoverageGrid.from_ranges(range(-15, 16, 2), range(-15, 16, 2), range(0, 16, 2))  # coverage.py:38-40
     cov = Coverage(mesh, 2.998e8, 100e9, 100e-9, max_bounces=2, tx_num_rays=1_000_000, grid=grid)
@@ -361,7 +362,7 @@ def _dist_shard():
 
 def coverage_map(environment_trimesh, tx_pos, grid: CoverageGrid, light_speed_mps=2.998e8, sample_rate_hz=100e9,
                  sample_window_s=100e-9, max_bounces=2, tx_num_rays=1_000_000, tx_power=1, rx_radius=0.1,
-                 device=None, shard_mode="rays"):
+                 device=None, shard_mode="sectors"):
     """coverage.py as a function.  Under torch.distributed the work is sharded over the ranks (by
     rays with a record all-to-all, or by x columns of cells) and the power map is all-reduced;
     every rank returns the full map."""

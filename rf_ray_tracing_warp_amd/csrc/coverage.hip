@@ -3479,24 +3479,31 @@ int rt_coverage_create_rays(int device, const rt_mesh* env, int max_bounces, int
   return RT_OK;
 }
 
+constexpr int kSectorSlices = 4;
 int rt_coverage_create_sectors(int device, const rt_mesh* env, int max_bounces, int64_t n_rays_total,
                                const rt_grid* grid, double rx_radius, int rank, int world, rt_coverage** out) {
   if (!out || world < 1 || rank < 0 || rank >= world || n_rays_total < world || n_rays_total > (1 << 24)) {
     rt::set_error("rt_coverage_create_sectors: invalid arguments (0 <= rank < world <= n_rays_total <= 2^24)");
     return RT_EINVAL;
   }
-  const int64_t lo = rank * n_rays_total / world, hi = (rank + 1) * n_rays_total / world;
+  // Four interleaved wedges per rank (pieces r, r + W, r + 2W, r + 3W of the azimuth order): one
+  // wedge per rank left the ranks unbalanced (the transmitter sits off-centre: K3 rank trace stages
+  // 0.575-0.693 ms, K5 0.667-0.820), four balance them and keep the locality (K3 slowest rank with
+  // the modelled collectives 0.875 ms against 0.933 for ray-id ranges and 0.891 for 16 wedges; K5
+  // 1.124 / 1.149 / 1.142 ms; profiles/r6b_*, r6f_*)
+  const int slices = (int64_t)world * kSectorSlices <= n_rays_total ? kSectorSlices : 1;
+  const int64_t m = rt::sector_ray_count(n_rays_total, rank, world, slices);
   rt_coverage* c = nullptr;
-  int rc = rt_coverage_create_rays(device, env, max_bounces, n_rays_total, 0, hi - lo, grid, rx_radius, rank, world, &c);
+  int rc = rt_coverage_create_rays(device, env, max_bounces, n_rays_total, 0, m, grid, rx_radius, rank, world, &c);
   if (rc) return rc;
   rt::DeviceGuard dg(device);
   c->sectors = true;
   c->ray_offset = 0;
-  if (hipMalloc(&c->ray_order, sizeof(int32_t) * (size_t)(hi - lo)) != hipSuccess) {
+  if (hipMalloc(&c->ray_order, sizeof(int32_t) * (size_t)m) != hipSuccess) {
     rt_coverage_destroy(c);
     return rt::hip_fail(hipErrorOutOfMemory, "rt_coverage_create_sectors");
   }
-  rc = rt::sector_ray_ids(n_rays_total, lo, hi, c->ray_order, nullptr);
+  rc = rt::sector_ray_ids(n_rays_total, rank, world, slices, c->ray_order, nullptr);
   if (rc) {
     rt_coverage_destroy(c);
     return rc;

@@ -314,6 +314,13 @@ __device__ __forceinline__ Hit group_hit(Hit h) {
 // next-node prefetch were measured and removed in round 5; last in commit 43de9a4)
 using Walk = Walk4;
 
+// (Wave-packet walks -- all 64 lanes of a wave on one node sequence, node and leaf data read once
+// per wave through the scalar cache, a wave stack in LDS of (node, lanes, smallest entry t) -- were
+// bit-identical on every BVH parity test and 4-5x slower: K4 rt_trace 2974-2988 vs 719-720 us, K5
+// trajectory pass 2.06 vs 0.395 ms (profiles/r6i_*_bvh_packet_ab.jsonl).  A direction-sorted wave's
+// rays reach terrain points metres apart (and reflect apart), so the packet visits the
+// union of 64 walks, and each visit is a chain of dependent scalar loads.  Removed in round 6.)
+
 // RT_COUNT_STEPS (diagnostic builds only, tools/walk_stats.py): per query, the lane's walk steps and
 // its share of the wave's loop iterations (1 / active lanes per iteration, so the shares of a wave
 // add up to its iteration count), summed over 16 slots by block; the max steps of one query.

@@ -74,9 +74,11 @@ const int32_t* dir_order_banded(int64_t ray_offset, int64_t n, hipStream_t strea
 // The same order, computed once per (device, ray_offset, n) and kept by the library (the rays of a
 // burst depend on their ids only); ready on `stream` when it returns.  nullptr on failure.
 const int32_t* dir_order_cached(int64_t ray_offset, int64_t n, hipStream_t stream);
-// Sector shards of a burst of n_total rays: positions [lo, hi) of the burst sorted by the azimuth
-// of the initial direction, written to out[hi - lo] as global ids in the banded order (trace.hip)
-int sector_ray_ids(int64_t n_total, int64_t lo, int64_t hi, int32_t* out, hipStream_t stream);
+// Sector shards of a burst of n_total rays (trace.hip): the burst sorted by the azimuth of the
+// initial direction, cut into world * slices equal pieces, rank taking every world-th piece from
+// piece rank; written to out[sector_ray_count(...)] as global ids in the banded order
+int64_t sector_ray_count(int64_t n_total, int rank, int world, int slices);
+int sector_ray_ids(int64_t n_total, int rank, int world, int slices, int32_t* out, hipStream_t stream);
 // Device view of a mesh's BVH for rt::bvh_query
 inline BvhView bvh_view(const rt_mesh* m) {
   return BvhView{(const float4*)m->nodes, (const int2*)m->leaves, (const float4*)m->lcomp, (int)m->nf,

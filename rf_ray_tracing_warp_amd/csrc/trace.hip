@@ -808,15 +808,26 @@ const int32_t* dir_order_banded(int64_t ray_offset, int64_t n, hipStream_t strea
 }
 
 // The rays of a sector shard of a burst of n_total rays (global ids 0..n_total-1): the burst sorted
-// by the azimuth of the initial direction (stable, so equal keys stay in id order), positions
-// [lo, hi) of that order, then those ids in the banded order the trajectory kernels want.  Written
-// to out[hi - lo]; synchronises `stream` (once per plan).
-int sector_ray_ids(int64_t n_total, int64_t lo, int64_t hi, int32_t* out, hipStream_t stream) {
-  if (n_total <= 0 || lo < 0 || hi > n_total || lo >= hi || n_total > INT32_MAX) {
-    set_error("sector_ray_ids: invalid range");
+// by the azimuth of the initial direction (stable, so equal keys stay in id order) and cut into
+// world * slices equal pieces; rank takes pieces rank, rank + world, rank + 2 world, ... (slices = 1:
+// one wedge of directions), then those ids in the banded order the trajectory kernels want.
+// Written to out[sector_ray_count(...)]; synchronises `stream` (once per plan).
+int64_t sector_ray_count(int64_t n_total, int rank, int world, int slices) {
+  const int64_t P = (int64_t)world * slices;
+  int64_t m = 0;
+  for (int k = 0; k < slices; ++k) {
+    const int64_t p = (int64_t)k * world + rank;
+    m += (p + 1) * n_total / P - p * n_total / P;
+  }
+  return m;
+}
+int sector_ray_ids(int64_t n_total, int rank, int world, int slices, int32_t* out, hipStream_t stream) {
+  if (n_total <= 0 || world < 1 || rank < 0 || rank >= world || slices < 1 || n_total > INT32_MAX ||
+      (int64_t)world * slices > n_total) {
+    set_error("sector_ray_ids: invalid arguments");
     return RT_EINVAL;
   }
-  const int64_t m = hi - lo;
+  const int64_t m = sector_ray_count(n_total, rank, world, slices), P = (int64_t)world * slices;
   size_t b1 = 0, b2 = 0;
   RT_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, b1, (uint32_t*)nullptr, (uint32_t*)nullptr, (int32_t*)nullptr,
                                             (int32_t*)nullptr, (int)n_total, 0, 16, stream));
@@ -824,18 +835,25 @@ int sector_ray_ids(int64_t n_total, int64_t lo, int64_t hi, int32_t* out, hipStr
                                             (int32_t*)nullptr, (int)m, 0, 16 + kZBandBits, stream));
   const size_t kb = ((size_t)n_total * 4 + 255) / 256 * 256;
   char* ws = nullptr;
-  RT_HIP(hipMalloc(&ws, 4 * kb + std::max(b1, b2)));
+  RT_HIP(hipMalloc(&ws, 5 * kb + std::max(b1, b2)));
   uint32_t* k_in = (uint32_t*)ws;
   uint32_t* k_out = (uint32_t*)(ws + kb);
   int32_t* i_in = (int32_t*)(ws + 2 * kb);
   int32_t* i_out = (int32_t*)(ws + 3 * kb);
-  void* tmp = ws + 4 * kb;
+  int32_t* mine = (int32_t*)(ws + 4 * kb);
+  void* tmp = ws + 5 * kb;
   hipError_t e = hipSuccess;
   hipLaunchKernelGGL(k_azimuth_keys, dim3((unsigned)((n_total + 255) / 256)), dim3(256), 0, stream, n_total, k_in, i_in);
   e = hipcub::DeviceRadixSort::SortPairs(tmp, b1, k_in, k_out, i_in, i_out, (int)n_total, 0, 16, stream);
+  int64_t at = 0;
+  for (int k = 0; k < slices && e == hipSuccess; ++k) {
+    const int64_t p = (int64_t)k * world + rank, lo = p * n_total / P, hi = (p + 1) * n_total / P;
+    e = hipMemcpyAsync(mine + at, i_out + lo, sizeof(int32_t) * (size_t)(hi - lo), hipMemcpyDeviceToDevice, stream);
+    at += hi - lo;
+  }
   if (e == hipSuccess) {
-    hipLaunchKernelGGL(k_ids_keys_banded, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, stream, i_out + lo, m, k_in);
-    e = hipcub::DeviceRadixSort::SortPairs(tmp, b2, k_in, k_out, i_out + lo, out, (int)m, 0, 16 + kZBandBits, stream);
+    hipLaunchKernelGGL(k_ids_keys_banded, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, stream, mine, m, k_in);
+    e = hipcub::DeviceRadixSort::SortPairs(tmp, b2, k_in, k_out, mine, out, (int)m, 0, 16 + kZBandBits, stream);
   }
   if (e == hipSuccess) e = hipGetLastError();
   if (e == hipSuccess) e = hipStreamSynchronize(stream);

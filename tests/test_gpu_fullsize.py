@@ -177,8 +177,8 @@ def test_k2_compute_cir_full_size_vs_oracle(win):
     print(f"\nK2: {len(paths)} received paths, {np.count_nonzero(ir)} bins", flush=True)
 
 
-@pytest.mark.parametrize("W", [4, 8])
-def test_k3_ray_sharded_equals_whole_at_full_size(W):
+@pytest.mark.parametrize("W,mode", [(4, "rays"), (8, "rays"), (8, "sectors")])
+def test_k3_ray_sharded_equals_whole_at_full_size(W, mode):
     """The bench's N>1 coverage decomposition at full K3 size, all W rank plans on one GPU with the
     all-to-all done in process: bit-identical to the whole map (per-bin sums are exact fixed point,
     so per-rank partial sums add up to the same integers).  Both W overflow the plans' first
@@ -191,7 +191,7 @@ def test_k3_ray_sharded_equals_whole_at_full_size(W):
     ref = whole.run(tx, 1).reshape(-1)
     whole.close()
     plans = [Coverage(room, 2.998e8, 100e9, win, B, N, grid, 0.1, device=0, shard_index=r, shard_count=W,
-                      shard_mode="rays") for r in range(W)]
+                      shard_mode=mode) for r in range(W)]
     got, _ = _ray_sharded_map(plans, tx, grid.num_cells)
     for p in plans:
         p.close()
@@ -256,7 +256,8 @@ def _ray_sharded_map(plans, tx, num_cells):
     return total.cpu().numpy(), nrec
 
 
-def test_k5_ray_sharded_equals_whole_at_full_size():
+@pytest.mark.parametrize("mode", ["rays", "sectors"])
+def test_k5_ray_sharded_equals_whole_at_full_size(mode):
     """K5's 8-GPU decomposition (BASELINE configs[4]) at full size: the 2.09M-face terrain stand-in,
     1024^2 cells, 1M rays per cell, B=3, 20,000 bins, as 8 shard_mode="rays" plans on one GPU with
     the all-to-all done in process.  Bit-identical to the whole map (exact fixed-point bin sums), and
@@ -270,11 +271,11 @@ def test_k5_ray_sharded_equals_whole_at_full_size():
     ref = whole.run(tx, 1).reshape(-1)
     whole.close()
     plans = [Coverage(terr, 2.998e8, 100e9, win, B, N, grid, 0.1, device=0, shard_index=r, shard_count=W,
-                      shard_mode="rays", env_mesh=env) for r in range(W)]
+                      shard_mode=mode, env_mesh=env) for r in range(W)]
     got, nrec = _ray_sharded_map(plans, tx, grid.num_cells)
     for p in plans:
         p.close()
-    print(f"\nK5 ray-sharded x{W}: records per owner {nrec}", flush=True)
+    print(f"\nK5 {mode}-sharded x{W}: records per owner {nrec}", flush=True)
     assert min(nrec) > 0
     assert int(np.isfinite(ref).sum()) > 100_000
     np.testing.assert_array_equal(got, ref)
