@@ -32,6 +32,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <numeric>
 #include <vector>
 
 #include "../../include/rfrt.h"
@@ -621,15 +622,25 @@ struct ColSpan {
   uint32_t n;    // columns
   uint32_t tag;  // step << 16 | k << 12 | kz
 };
-__global__ __launch_bounds__(256) void k_cols(CovParams p) {
+// Rows are visited in groups of kColGroup consecutive trajectory slots, group g at slot group
+// (g * gstep) % ngroups (gstep coprime to ngroups, ~ngroups / 16): a block's 16 groups sample the
+// whole burst.  The items' order is the append order either way (one atomic per block), so only the
+// load balance changes: in the direction-banded order of a sector shard the long, nearly horizontal
+// segments -- hundreds of columns each -- are the first slots, and consecutive slots put them all
+// into the same few blocks (K3 rank of 8: 82 us, against 22 us with slots in ray-id order).
+constexpr int kColGroup = 16;
+__global__ __launch_bounds__(256) void k_cols(CovParams p, int64_t ngroups, int64_t gstep) {
   __shared__ uint32_t s_pre[256];  // the lanes' exclusive item prefixes in the block
   __shared__ uint32_t s_tot;
+  __shared__ int64_t s_row[256];
   __shared__ ColSpan s_span[kColSpans][256];
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const bool spans_ok = (int64_t)p.B * p.g.nz <= kColSpans && p.g.nz <= 4096 && p.nshard < 65536;
-  for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < p.n; base += stride) {
-    const int64_t r = base + threadIdx.x;
-    const bool active = r < p.n;
+  const int64_t nslots = ngroups * kColGroup;
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < nslots; base += stride) {
+    const int64_t i = base + threadIdx.x;
+    const int64_t r = (i / kColGroup * gstep) % ngroups * kColGroup + i % kColGroup;
+    const bool active = i < nslots && r < p.n;
     unsigned c = 0;
     int nsp = 0;
     const int ns = active ? p.nseg[r] : 0;
@@ -670,6 +681,7 @@ __global__ __launch_bounds__(256) void k_cols(CovParams p) {
       continue;
     }
     s_pre[threadIdx.x] = pre;
+    s_row[threadIdx.x] = r;
     if (threadIdx.x == 255) s_tot = pre + c;
     __syncthreads();
     const uint32_t tot = s_tot;
@@ -687,7 +699,7 @@ __global__ __launch_bounds__(256) void k_cols(CovParams p) {
       const int64_t w = (int64_t)at + q;
       if (w < p.item_cap) {
         const uint64_t k = (sp.tag >> 12) & 15u, kz = sp.tag & 0xFFFu, step = sp.tag >> 16;
-        p.items[w] = ((uint64_t)(base + lo) << 40) | (k << 36) | (kz << 24) | (uint64_t)(sp.ia0 + (int64_t)off * step);
+        p.items[w] = ((uint64_t)s_row[lo] << 40) | (k << 36) | (kz << 24) | (uint64_t)(sp.ia0 + (int64_t)off * step);
       }
     }
     __syncthreads();  // s_pre, s_tot and the spans are rewritten by the next block-row
@@ -2655,7 +2667,9 @@ size_t rord_row_bytes(int64_t n) { return ((size_t)n * 4 + 255) / 256 * 256; }
 // ~0.2M (31 bits) are faster merged (owner stage 0.23 vs 0.29 ms) and K5's ~0.47M (36 bits) by
 // Onesweep (0.46 vs 0.50 ms).  So: Onesweep from 300k items, rocprim's default below.
 // 10-bit digits and 1024-thread blocks (rocprim's gfx950 default is 8 bits per pass;
-// tools/gpu_sortvar.sh: K5 rank of 8 1.58 -> 1.53 ms)
+// tools/gpu_sortvar.sh: K5 rank of 8 1.58 -> 1.53 ms).  Smaller sort tiles for a rank's < 2M
+// records (512 x 8, 256 x 8, 512 x 4 with 10-bit digits, 256 x 8 with 8-bit) fill more CUs and were
+// slower: K3 rank of 8 with collectives 0.856-0.926 vs 0.856-0.867 ms (profiles/r6o_sort_tile_ab.jsonl).
 using OnesweepCfg =
     rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 8>, rocprim::kernel_config<1024, 8>, 10,
                                         rocprim::block_radix_rank_algorithm::match>;
@@ -3089,6 +3103,10 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
   p.cell_bits = kb.cell;
   int64_t ncand = 0, nrec = 0, nlist = 0;
   const unsigned grid_items = 4096;
+  // k_cols' slot-group stride: coprime to the group count, so that a block's 16 groups spread over the burst
+  const int64_t col_groups = std::max<int64_t>(1, (c->n + kColGroup - 1) / kColGroup);
+  int64_t col_step = std::max<int64_t>(1, col_groups / 16);
+  while (std::gcd(col_step, col_groups) != 1) ++col_step;
   // Replay launched before the list length reaches the host (early replay): the kernels read it
   // from the device counter, so the host's counter read-back and its wake-up (~36 us per K3 rank
   // of 8, profiles/r3j_k3.timeline.txt) overlap the replay instead of idling the GPU.  Only for
@@ -3159,7 +3177,7 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
     p.keys = c->keys;
     p.cap = c->cap;
     if (attempt > 0) RT_HIP(hipMemsetAsync(c->counters, 0, 32, s));
-    hipLaunchKernelGGL(k_cols, dim3(grid_rays), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(k_cols, dim3(grid_rays), dim3(256), 0, s, p, col_groups, col_step);
     hipLaunchKernelGGL(k_cells, dim3(grid_items), dim3(256), 0, s, p);
     const unsigned grid_c = (unsigned)std::min<int64_t>((c->cap + 255) / 256, 8192);
     prof_mark(c, 2, s);
