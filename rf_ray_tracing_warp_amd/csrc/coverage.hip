@@ -1644,62 +1644,11 @@ __global__ __launch_bounds__(256) void k_cell_ranges(const uint64_t* ukeys, cons
 }
 
 constexpr int kPowLds = 192;  // terms per wave staged in LDS (3 per lane); larger cells read global memory
-constexpr int kPowSmall = 16;  // cells with at most this many terms: one thread each (k_power_small)
+constexpr int kPowSmall = 16;  // cells with at most this many terms: k_power_small
+constexpr int kPowGroup = 8;   // lanes per such cell when a plan owns few cells (4 and 16 measured no better, r6q)
+constexpr int64_t kPowGroupMaxCells = 131072;  // maps of at most this many cells (the map's, not a shard's)
 // (Copying each thread's terms into its LDS column first measured K3 rank 37 -> 33 us but K5 rank
 // 42 -> 65 us -- 53 KB of LDS, 3 waves per CU; r3f.  Removed in round 5.)
-
-// cells of ours with 0..kPowSmall terms: one thread per cell, serial sweep (most cells of a large
-// map receive a handful of bins; a wave per such cell costs more than its whole sweep)
-// Larger cells are listed (big[], count in *nbig; one atomic per wave) for k_power, which then
-// visits only them (it used to stride over every cell of the map to skip the small ones: 1M cell
-// ranges read per K5 map for a few thousand large cells).
-__global__ __launch_bounds__(64) void k_power_small(TermArrays G, const int32_t* cstart, const int32_t* cend,
-                                                     const int32_t* cepoch, int32_t epoch, rt_grid g, int shard,
-                                                     int nshard, PowerParams P, double* power, int32_t* big,
-                                                     unsigned* nbig) {
-  const int64_t nxo = g.nx > shard ? (g.nx - shard + nshard - 1) / nshard : 0;
-  const int64_t nown = nxo * g.ny * g.nz;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int lane = threadIdx.x & 63;
-  if (nshard > 1) {  // other ranks' cells: 0 (the map is sum-reduced), instead of a fill
-    // 32-bit index arithmetic (cells < 2^32, rt_coverage_create): a 64-bit division by a run-time
-    // divisor is a ~100-instruction sequence, and this loop visits every cell of the map
-    const uint32_t ncell = (uint32_t)(g.nx * g.ny * g.nz), nx = (uint32_t)g.nx, ns = (uint32_t)nshard;
-    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < ncell; c += (uint32_t)stride)
-      if ((c % nx) % ns != (uint32_t)shard) power[c] = 0.0;
-  }
-  for (int64_t base = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); base < nown; base += stride) {
-    const int64_t t = base + lane;
-    bool is_big = false;
-    int64_t c = 0;
-    if (t < nown) {
-      // the owned cell of index t (32-bit: cells < 2^32; a 64-bit division is ~100 instructions)
-      if (nshard == 1) {
-        c = t;
-      } else {
-        const uint32_t tt = (uint32_t)t, nx32 = (uint32_t)nxo, rest = tt / nx32, jx = tt - rest * nx32;
-        c = (int64_t)rest * g.nx + shard + (int64_t)jx * nshard;
-      }
-      const bool has = cepoch[c] == epoch;
-      const int64_t lo = has ? cstart[c] : 0, hi = has ? cend[c] : 0;
-      if (hi - lo <= kPowSmall) {
-        power[c] = power_sparse(lo, hi, P, G);  // NaN when empty
-      } else {
-        is_big = true;
-      }
-    }
-    const uint64_t m = __ballot(is_big);
-    if (m) {
-      unsigned b0 = 0;
-      if (lane == 0) b0 = atomicAdd(nbig, (unsigned)__popcll(m));
-      b0 = __shfl(b0, 0, 64);
-      if (is_big) {
-        const unsigned r = (unsigned)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        big[b0 + r] = (int32_t)c;
-      }
-    }
-  }
-}
 
 // double-double helpers for the compensated prefix sums
 __device__ __forceinline__ void dd_add(double& h, double& l, double bh, double bl) {
@@ -1718,6 +1667,189 @@ __device__ __forceinline__ double interval_sq(double Pv, double Qv, int64_t L, d
   const double ssu = s2 * ca - c2 * sa, csu = c2 * ca + s2 * sa;    // of a (x + nx - 1)
   const double D = sl * csu / sa, E = sl * ssu / sa;
   return Pv * Pv * (0.5 * ((double)L - D)) + Qv * Qv * (0.5 * ((double)L + D)) + 2.0 * Pv * Qv * (0.5 * E);
+}
+
+// Cells of ours with 0..kPowSmall terms, G lanes per cell (kPowGroup for maps of at most
+// kPowGroupMaxCells cells; G = 1 is the serial sweep of power_sparse).  G > 1: the cell's terms are staged in the wave's LDS with compensated
+// (double-double) prefix sums of a cos / a sin, and each lane closes the intervals that start at its
+// events, as k_power does for larger cells -- equal to the serial sweep up to the order of summation.
+// (One thread per cell made the kernel as long as one thread's chain of up to 2 x 16 intervals, each
+// a few dependent loads and two f64 divisions: K3 rank of 8 ~40 us for 8k cells.)
+// Larger cells are listed (big[], count in *nbig; one atomic per wave) for k_power, which then
+// visits only them (it used to stride over every cell of the map to skip the small ones: 1M cell
+// ranges read per K5 map for a few thousand large cells).
+template <int G>
+__global__ __launch_bounds__(64) void k_power_small(TermArrays T, const int32_t* cstart, const int32_t* cend,
+                                                     const int32_t* cepoch, int32_t epoch, rt_grid g, int shard,
+                                                     int nshard, PowerParams P, double* power, int32_t* big,
+                                                     unsigned* nbig) {
+  static_assert(G == 1 || G == 4 || G == 8 || G == 16, "1, 4, 8 or 16 lanes per cell");
+  constexpr int NG = 64 / G, TP = (kPowSmall + G - 1) / G;  // cells per wave, terms per lane
+  __shared__ int32_t s_st[NG][kPowSmall], s_e1[NG][kPowSmall], s_m[NG][kPowSmall];
+  __shared__ double s_pch[NG][kPowSmall + 1], s_pcl[NG][kPowSmall + 1], s_psh[NG][kPowSmall + 1],
+      s_psl[NG][kPowSmall + 1];
+  __shared__ double s_ev[NG][4 * kPowSmall];
+  const int64_t nxo = g.nx > shard ? (g.nx - shard + nshard - 1) / nshard : 0;
+  const int64_t nown = nxo * g.ny * g.nz;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int lane = threadIdx.x & 63, j = lane & (G - 1), gi = lane / G;
+  if (nshard > 1) {  // other ranks' cells: 0 (the map is sum-reduced), instead of a fill
+    // 32-bit index arithmetic (cells < 2^32, rt_coverage_create): a 64-bit division by a run-time
+    // divisor is a ~100-instruction sequence, and this loop visits every cell of the map
+    const uint32_t ncell = (uint32_t)(g.nx * g.ny * g.nz), nx = (uint32_t)g.nx, ns = (uint32_t)nshard;
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < ncell; c += (uint32_t)stride)
+      if ((c % nx) % ns != (uint32_t)shard) power[c] = 0.0;
+  }
+  const int64_t n = P.n_bins, half = P.half;
+  double sn = 0.0, cn = 0.0;  // sin/cos at the sweep end
+  if (G > 1) sincos_turns(P.turns * (double)n, sn, cn);
+  const int64_t gstride = stride / G;
+  const int64_t nit = (nown + gstride - 1) / gstride;  // the same count for every lane (LDS reuse)
+  for (int64_t it = 0; it < nit; ++it) {
+    const int64_t t = it * gstride + (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G);
+    bool is_big = false, small = false;
+    int64_t c = 0, lo = 0, hi = 0;
+    if (t < nown) {
+      // the owned cell of index t (32-bit: cells < 2^32; a 64-bit division is ~100 instructions)
+      if (nshard == 1) {
+        c = t;
+      } else {
+        const uint32_t tt = (uint32_t)t, nx32 = (uint32_t)nxo, rest = tt / nx32, jx = tt - rest * nx32;
+        c = (int64_t)rest * g.nx + shard + (int64_t)jx * nshard;
+      }
+      const bool has = cepoch[c] == epoch;
+      lo = has ? cstart[c] : 0;
+      hi = has ? cend[c] : 0;
+      small = hi - lo <= kPowSmall;
+      is_big = !small;
+    }
+    const uint64_t m = __ballot(is_big && j == 0);
+    if (m) {
+      unsigned b0 = 0;
+      if (lane == 0) b0 = atomicAdd(nbig, (unsigned)__popcll(m));
+      b0 = __shfl(b0, 0, 64);
+      if (is_big && j == 0) {
+        const unsigned r = (unsigned)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        big[b0 + r] = (int32_t)c;
+      }
+    }
+    if constexpr (G == 1) {
+      if (small) power[c] = power_sparse(lo, hi, P, T);  // NaN when empty
+    } else {
+      const int K = small ? (int)(hi - lo) : 0;
+      // stage: TP consecutive terms per lane, local compensated sums, then a scan over the group
+      double lch = 0, lcl = 0, lsh = 0, lsl = 0;
+#pragma unroll
+      for (int q = 0; q < TP; ++q) {
+        const int k = j * TP + q;
+        if (k < K) {
+          const int64_t mk = T.m(lo + k);
+          s_m[gi][k] = (int32_t)mk;
+          s_st[gi][k] = (int32_t)(mk - half > 0 ? mk - half : 0);
+          const int64_t e = mk + (n - 1 - half);
+          s_e1[gi][k] = (int32_t)((e < n - 1 ? e : n - 1) + 1);
+          for (int r = 0; r < 4; ++r) s_ev[gi][4 * k + r] = T.ev[4 * (lo + k) + r];
+          dd_add(lch, lcl, T.tcos[lo + k], 0.0);
+          dd_add(lsh, lsl, T.tsin[lo + k], 0.0);
+        }
+      }
+      double ech = lch, ecl = lcl, esh = lsh, esl = lsl;  // inclusive scan of the lanes' sums
+#pragma unroll
+      for (int o = 1; o < G; o <<= 1) {
+        const double a = __shfl_up(ech, o, G), b = __shfl_up(ecl, o, G);
+        const double a2 = __shfl_up(esh, o, G), b2 = __shfl_up(esl, o, G);
+        if (j >= o) {
+          dd_add(ech, ecl, a, b);
+          dd_add(esh, esl, a2, b2);
+        }
+      }
+      dd_add(ech, ecl, -lch, -lcl);  // exclusive
+      dd_add(esh, esl, -lsh, -lsl);
+#pragma unroll
+      for (int q = 0; q < TP; ++q) {
+        const int k = j * TP + q;
+        if (k < K) {
+          s_pch[gi][k] = ech;
+          s_pcl[gi][k] = ecl;
+          s_psh[gi][k] = esh;
+          s_psl[gi][k] = esl;
+          dd_add(ech, ecl, T.tcos[lo + k], 0.0);
+          dd_add(esh, esl, T.tsin[lo + k], 0.0);
+          if (k == K - 1) {
+            s_pch[gi][K] = ech;
+            s_pcl[gi][K] = ecl;
+            s_psh[gi][K] = esh;
+            s_psl[gi][K] = esl;
+          }
+        }
+      }
+      __syncthreads();  // one wave per block
+      const int32_t* st = s_st[gi];
+      const int32_t* e1 = s_e1[gi];
+      auto upper = [&](const int32_t* a, int32_t x) {  // first index with a[i] > x
+        int l = 0, r = K;
+        while (l < r) {
+          const int mm = (l + r) >> 1;
+          if (a[mm] <= x) l = mm + 1; else r = mm;
+        }
+        return l;
+      };
+      auto lower = [&](const int32_t* a, int32_t x) {  // first index with a[i] >= x
+        int l = 0, r = K;
+        while (l < r) {
+          const int mm = (l + r) >> 1;
+          if (a[mm] < x) l = mm + 1; else r = mm;
+        }
+        return l;
+      };
+      double total = 0.0, tcomp = 0.0;
+      int64_t count = 0;
+      for (int ev = j; ev < 2 * K; ev += G) {
+        const bool is_start = ev < K;
+        const int k = is_start ? ev : ev - K;
+        const int32_t x = is_start ? st[k] : e1[k];
+        if (x >= n) continue;  // the sweep ends at n
+        // one lane per distinct event position: starts first, an end only where no start is
+        if (k > 0 && (is_start ? st[k - 1] : e1[k - 1]) == x) continue;
+        if (!is_start && upper(st, x) != lower(st, x)) continue;
+        const int is = upper(st, x), ie = upper(e1, x);
+        if (ie >= is) continue;  // nothing active
+        const int nstart = is - lower(st, x);
+        const bool alone = (is - ie == 1) && nstart == 1 && ((int64_t)s_m[gi][is - 1] - half == (int64_t)x);
+        int64_t nx = n;
+        double snx = sn, cnx = cn;
+        if (is < K && st[is] < nx) {
+          nx = st[is];
+          snx = s_ev[gi][4 * is];
+          cnx = s_ev[gi][4 * is + 1];
+        }
+        if (e1[ie] < nx) {
+          nx = e1[ie];
+          snx = s_ev[gi][4 * ie + 2];
+          cnx = s_ev[gi][4 * ie + 3];
+        }
+        const double sx = is_start ? s_ev[gi][4 * k] : s_ev[gi][4 * k + 2];
+        const double cx = is_start ? s_ev[gi][4 * k + 1] : s_ev[gi][4 * k + 3];
+        double Ph = s_pch[gi][is], Pl = s_pcl[gi][is], Qh = s_psh[gi][is], Ql = s_psl[gi][is];
+        dd_add(Ph, Pl, -s_pch[gi][ie], -s_pcl[gi][ie]);
+        dd_add(Qh, Ql, -s_psh[gi][ie], -s_psl[gi][ie]);
+        two_sum(total, tcomp, interval_sq(Ph + Pl, Qh + Ql, nx - x, sx, cx, snx, cnx, P));
+        count += nx - x - (alone ? 1 : 0);
+      }
+#pragma unroll
+      for (int o = G / 2; o >= 1; o >>= 1) {
+        const double t2 = __shfl_down(total, o, G), c2 = __shfl_down(tcomp, o, G);
+        const int64_t n2 = __shfl_down(count, o, G);
+        if (j < o) {
+          two_sum(total, tcomp, t2);
+          tcomp += c2;
+          count += n2;
+        }
+      }
+      if (small && j == 0) power[c] = count > 0 ? (total + tcomp) / (double)count : __builtin_nan("");
+      __syncthreads();  // the LDS slots are reused by the next cells
+    }
+  }
 }
 
 // One wave per cell of ours (x columns ix % nshard == shard; the caller zero-fills the rest, the
@@ -3322,7 +3454,7 @@ int cov_power(rt_coverage* c, int64_t nrec, int64_t n_bins, double alpha, double
   const PowerParams P = power_params(n_bins, alpha);
   // one wave per owned cell, 4 per block
   const unsigned grid_cells = (unsigned)std::min<int64_t>((ncell / c->nshard + 4) / 4, 4096);
-  // one thread per small cell, 64 per block: each thread's sweep is a chain of dependent loads,
+  // one thread (kPowGroup lanes on small maps) per small cell, 64 per block: each sweep is a chain,
   // so a sharded map's few thousand cells must still spread over every CU
   const unsigned grid_small = (unsigned)std::min<int64_t>((ncell / c->nshard + 64) / 64, 16384);
   const TermArrays terms{c->ukeys, c->tcos, c->tsin, c->ev};
@@ -3339,8 +3471,19 @@ int cov_power(rt_coverage* c, int64_t nrec, int64_t n_bins, double alpha, double
                        c->cepoch, epoch, nbig);
   }
   const int32_t epoch = c->range_epoch;
-  hipLaunchKernelGGL(k_power_small, dim3(grid_small), dim3(64), 0, s, terms, c->cstart, c->cend, c->cepoch, epoch,
-                     c->grid, c->shard, c->nshard, P, power, big, nbig);
+  // Small maps: kPowGroup lanes per cell -- a rank of a sharded map owns few cells, and the chain of
+  // one thread's serial sweep set its time (K3 rank of 8, 8k cells: 40 -> 19 us; the whole K3 map,
+  // 65k cells, 55 -> 61 us).  Large maps: one thread per cell, the grouped form's staging and
+  // searches cost more than they overlap (K5 map, 1M cells: 146 vs 231 us; K5 rank 48 vs 44 us,
+  // r6r).  The choice depends on the map, never on the shard, so that every cell's power is summed
+  // in the same order whoever owns it (a sharded map equals the whole map bit for bit).
+  if (ncell <= kPowGroupMaxCells)
+    hipLaunchKernelGGL(k_power_small<kPowGroup>, dim3(std::min<int64_t>((int64_t)grid_small * kPowGroup, 65536)),
+                       dim3(64), 0, s, terms, c->cstart, c->cend, c->cepoch, epoch, c->grid, c->shard, c->nshard, P,
+                       power, big, nbig);
+  else
+    hipLaunchKernelGGL(k_power_small<1>, dim3(grid_small), dim3(64), 0, s, terms, c->cstart, c->cend, c->cepoch,
+                       epoch, c->grid, c->shard, c->nshard, P, power, big, nbig);
   if (nrec > 0)
     hipLaunchKernelGGL(k_power, dim3(grid_cells), dim3(256), 0, s, terms, c->cstart, c->cend, big, nbig, P, power);
   RT_HIP(hipGetLastError());
