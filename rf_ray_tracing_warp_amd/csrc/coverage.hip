@@ -1467,6 +1467,7 @@ struct PowerParams {
   double alpha;   // phase per sample: (2*pi*2.4e9) * (window/(n-1))
   double turns;   // alpha / (2*pi)
   double sin_a, cos_a;
+  double sin_n, cos_n;  // of alpha * n_bins (the sweep end; host, like sin_a / cos_a)
 };
 
 __device__ __forceinline__ void two_sum(double& s, double& c, double x) {  // Neumaier running sum
@@ -1502,8 +1503,8 @@ __device__ void power_range(int64_t lo, int64_t hi, const PowerParams& P, const 
   };
   int64_t is = lo, ie = lo;  // active terms = [ie, is)
   int64_t x = xb;
-  double sx, cx;  // sin, cos of alpha * x
-  sincos_turns(P.turns * (double)xb, sx, cx);
+  double sx = 0.0, cx = 1.0;  // sin, cos of alpha * x (sincos of 0 is exactly that: no call for xb = 0)
+  if (xb != 0) sincos_turns(P.turns * (double)xb, sx, cx);
   if (xb > 0) {  // first term starting after xb, first term ending at or after xb
     int64_t a = lo, b = hi;
     while (a < b) {
@@ -1555,7 +1556,12 @@ __device__ void power_range(int64_t lo, int64_t hi, const PowerParams& P, const 
     }
     if (src == 1) T.start(is, snx, cnx);
     else if (src == 2) T.stop(ie, snx, cnx);
-    else sincos_turns(P.turns * (double)nx, snx, cnx);
+    else if (nx == n) {  // the sweep end: one value for every cell, from the host
+      snx = P.sin_n;
+      cnx = P.cos_n;
+    } else {
+      sincos_turns(P.turns * (double)nx, snx, cnx);
+    }
     if (ie < is) {
       const double Pv = Ps + Pc, Qv = Qs + Qc;
       const int64_t L = nx - x;
@@ -1701,8 +1707,7 @@ __global__ __launch_bounds__(64) void k_power_small(TermArrays T, const int32_t*
       if ((c % nx) % ns != (uint32_t)shard) power[c] = 0.0;
   }
   const int64_t n = P.n_bins, half = P.half;
-  double sn = 0.0, cn = 0.0;  // sin/cos at the sweep end
-  if (G > 1) sincos_turns(P.turns * (double)n, sn, cn);
+  const double sn = P.sin_n, cn = P.cos_n;  // sin/cos at the sweep end
   const int64_t gstride = stride / G;
   const int64_t nit = (nown + gstride - 1) / gstride;  // the same count for every lane (LDS reuse)
   for (int64_t it = 0; it < nit; ++it) {
@@ -1869,8 +1874,7 @@ __global__ __launch_bounds__(256) void k_power(TermArrays G, const int32_t* csta
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t n = P.n_bins, half = P.half;
   const int64_t nown = *nbig;
-  double sn, cn;  // sin/cos at the sweep end
-  sincos_turns(P.turns * (double)n, sn, cn);
+  const double sn = P.sin_n, cn = P.cos_n;  // sin/cos at the sweep end
   for (int64_t t = (int64_t)blockIdx.x * 4 + w; t < nown; t += (int64_t)gridDim.x * 4) {
     const int64_t c = big[t];
     const int64_t lo = cstart[c], hi = cend[c], K = hi - lo;
@@ -3444,6 +3448,11 @@ PowerParams power_params(int64_t n_bins, double alpha) {
   P.turns = alpha / 6.283185307179586;
   P.sin_a = sin(alpha);
   P.cos_a = cos(alpha);
+  {  // as sincos_turns: the phase reduced to [-1/2, 1/2] turn first
+    const double t = P.turns * (double)n_bins, f = t - std::rint(t);
+    P.sin_n = sin(6.283185307179586 * f);
+    P.cos_n = cos(6.283185307179586 * f);
+  }
   return P;
 }
 // ranges_done: the terms, cell ranges (epoch c->range_epoch) and nbig reset were already written
@@ -4079,13 +4088,7 @@ int rt_power_dense(const double* impulse_responses, int64_t rows, int64_t n_bins
     return RT_EINVAL;
   }
   if (rows == 0) return RT_OK;
-  PowerParams P;
-  P.n_bins = n_bins;
-  P.half = (n_bins - 1) / 2;
-  P.alpha = alpha;
-  P.turns = alpha / 6.283185307179586;
-  P.sin_a = sin(alpha);
-  P.cos_a = cos(alpha);
+  const PowerParams P = power_params(n_bins, alpha);
   uint64_t* kk = (uint64_t*)scratch;
   double* aa = (double*)(kk + rows * n_bins);
   hipLaunchKernelGGL(k_power_dense, dim3((unsigned)rows), dim3(64), 0, (hipStream_t)stream, impulse_responses, rows, P,
