@@ -379,17 +379,17 @@ __global__ __launch_bounds__(256, kTrajWaves) void k_traj(CovParams p) {
 // node fetches is split over four lanes.
 constexpr int kTrajSplitG = 4;
 // 4 waves per SIMD: 120 VGPRs, no spills (5: 96 + 23 spilled); K5 rank of 8 1.204 -> 1.154 ms (r3z)
+// Slots [s0, s1) over blocks [0, nblk) of the launch's share (block index b within it).
 template <int G>
-__global__ __launch_bounds__(256, 4) void k_traj_split(CovParams p) {
+__device__ __forceinline__ void traj_split_body(const CovParams& p, int64_t s0, int64_t s1, int64_t b, int64_t nblk) {
   constexpr int LG = G == 16 ? 4 : 2;
-  if (p.zero_ctr && blockIdx.x == 0 && threadIdx.x < 4) p.zero_ctr[threadIdx.x] = 0ull;
   const int j = threadIdx.x & (G - 1);
-  const int64_t stride = ((int64_t)gridDim.x * blockDim.x) >> LG;
+  const int64_t stride = (nblk * blockDim.x) >> LG;
   // every lane of a wave runs the same number of iterations (the shuffles need them all)
-  const int64_t nit = (p.n + stride - 1) / stride;
+  const int64_t nit = (s1 - s0 + stride - 1) / stride;
   for (int64_t it = 0; it < nit; ++it) {
-    const int64_t ir = it * stride + (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> LG);
-    const bool valid = ir < p.n;
+    const int64_t ir = s0 + it * stride + ((b * blockDim.x + threadIdx.x) >> LG);
+    const bool valid = ir < s1;
     const int64_t r = valid ? (p.order ? (int64_t)p.order[ir] : ir) : 0;
     float3 dir = rt::ray_dir(p.ray_offset + r);
     float3 pos = make_float3(p.tx[0], p.tx[1], p.tx[2]);
@@ -435,6 +435,19 @@ __global__ __launch_bounds__(256, 4) void k_traj_split(CovParams p) {
     }
     if (valid && j == 0) p.nseg[ir] = (uint8_t)nseg;
   }
+}
+template <int G>
+__global__ __launch_bounds__(256, 4) void k_traj_split(CovParams p) {
+  if (p.zero_ctr && blockIdx.x == 0 && threadIdx.x < 4) p.zero_ctr[threadIdx.x] = 0ull;
+  traj_split_body<G>(p, 0, p.n, blockIdx.x, gridDim.x);
+}
+// AB: the first n1 slots (the most nearly horizontal rays of the banded order) G1 lanes per ray on
+// blocks [0, nb1), the rest G2 lanes per ray on the other blocks
+template <int G1, int G2>
+__global__ __launch_bounds__(256, 4) void k_traj_split2(CovParams p, int64_t n1, unsigned nb1) {
+  if (p.zero_ctr && blockIdx.x == 0 && threadIdx.x < 4) p.zero_ctr[threadIdx.x] = 0ull;
+  if (blockIdx.x < nb1) traj_split_body<G1>(p, 0, n1, blockIdx.x, nb1);
+  else traj_split_body<G2>(p, n1, p.n, blockIdx.x - nb1, gridDim.x - nb1);
 }
 
 // k_traj for brute-force scenes with few rays (a ray-sharded rank's share, kTrajLdsSplit): G
@@ -3039,6 +3052,13 @@ __global__ __launch_bounds__(256) void k_count_replay(const ReplayItem* items, i
   if ((threadIdx.x & 63) == 0 && acc) atomicAdd(out, acc);
 }
 
+int64_t traj16_frac() {  // AB: 256ths of a rank's slots traced 16 lanes per ray (RFRT_TRAJ16)
+  static const int64_t v = [] {
+    const char* e = getenv("RFRT_TRAJ16");
+    return e ? (int64_t)atoll(e) : (int64_t)0;
+  }();
+  return v;
+}
 // BVH trajectories of at most this many rays run four lanes per ray (RFRT_TRAJ_SPLIT_MAX, 0 = never)
 int64_t traj_split_max_rays() {
   static const int64_t v = [] {
@@ -3202,7 +3222,13 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
     }
     p.order = c->ray_order;
     prof_mark(c, 0, s);
-    if (c->n <= traj_split_max_rays())  // too few rays to fill the GPU: four lanes per ray
+    const int64_t f16 = traj16_frac();
+    if (c->n <= traj_split_max_rays() && f16 > 0) {
+      const int64_t n1 = std::min<int64_t>(c->n, c->n * f16 / 256);
+      const unsigned nb1 = (unsigned)std::max<int64_t>(1, (16 * n1 + 255) / 256);
+      const unsigned nb2 = (unsigned)std::max<int64_t>(1, (kTrajSplitG * (c->n - n1) + 255) / 256);
+      hipLaunchKernelGGL((k_traj_split2<16, kTrajSplitG>), dim3(nb1 + nb2), dim3(256), 0, s, p, n1, nb1);
+    } else if (c->n <= traj_split_max_rays())  // too few rays to fill the GPU: four lanes per ray
       hipLaunchKernelGGL(k_traj_split<kTrajSplitG>,
                          dim3((unsigned)std::min<int64_t>((kTrajSplitG * c->n + 255) / 256, 8192)), dim3(256), 0,
                          s, p);
