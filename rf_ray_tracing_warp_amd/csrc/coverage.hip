@@ -373,10 +373,10 @@ __global__ __launch_bounds__(256, kTrajWaves) void k_traj(CovParams p) {
   }
 }
 
-// k_traj for BVH scenes with few rays (a ray-sharded rank's share): four lanes per ray, each
-// walking its quarter of the tree below the root's grandchildren (rt::split_init); the group's
-// closest hit is the ray's.  Same trajectories bit for bit; the slowest ray's chain of dependent
-// node fetches is split over four lanes.
+// k_traj for BVH scenes with few rays (a ray-sharded rank's share): G lanes per ray (4, or 16 for
+// the most nearly horizontal quarter), each walking its share of the tree below the root's
+// grandchildren (rt::split_init); the group's closest hit is the ray's.  Same trajectories bit for
+// bit; the slowest ray's chain of dependent node fetches is split over the lanes.
 constexpr int kTrajSplitG = 4;
 // 4 waves per SIMD: 120 VGPRs, no spills (5: 96 + 23 spilled); K5 rank of 8 1.204 -> 1.154 ms (r3z)
 // Slots [s0, s1) over blocks [0, nblk) of the launch's share (block index b within it).
@@ -436,15 +436,15 @@ __device__ __forceinline__ void traj_split_body(const CovParams& p, int64_t s0, 
     if (valid && j == 0) p.nseg[ir] = (uint8_t)nseg;
   }
 }
-template <int G>
-__global__ __launch_bounds__(256, 4) void k_traj_split(CovParams p) {
-  if (p.zero_ctr && blockIdx.x == 0 && threadIdx.x < 4) p.zero_ctr[threadIdx.x] = 0ull;
-  traj_split_body<G>(p, 0, p.n, blockIdx.x, gridDim.x);
-}
-// AB: the first n1 slots (the most nearly horizontal rays of the banded order) G1 lanes per ray on
-// blocks [0, nb1), the rest G2 lanes per ray on the other blocks
+// The first n1 slots -- the most nearly horizontal rays of the banded order, whose long grazing
+// walks set the time -- G1 lanes per ray on blocks [0, nb1) (dispatched first), the rest G2 lanes
+// per ray on the other blocks.  A K5 rank of 8 (kernel trace, means over the rank plans): 4 lanes
+// for every ray 218-220 us; 16 lanes for the first 3/16, 1/4, 5/16, 3/8, 1/2 of the slots 206,
+// 189-192, 203-205, 202, 212 us (r6w, r6x).  (16 lanes for every ray: no faster than 4, round 4.)
+constexpr int kTrajSplitWide = 16;   // lanes per ray of the first quarter
+constexpr int kTrajWideShare = 4;    // that quarter: slots [0, n / kTrajWideShare)
 template <int G1, int G2>
-__global__ __launch_bounds__(256, 4) void k_traj_split2(CovParams p, int64_t n1, unsigned nb1) {
+__global__ __launch_bounds__(256, 4) void k_traj_split(CovParams p, int64_t n1, unsigned nb1) {
   if (p.zero_ctr && blockIdx.x == 0 && threadIdx.x < 4) p.zero_ctr[threadIdx.x] = 0ull;
   if (blockIdx.x < nb1) traj_split_body<G1>(p, 0, n1, blockIdx.x, nb1);
   else traj_split_body<G2>(p, n1, p.n, blockIdx.x - nb1, gridDim.x - nb1);
@@ -3052,14 +3052,7 @@ __global__ __launch_bounds__(256) void k_count_replay(const ReplayItem* items, i
   if ((threadIdx.x & 63) == 0 && acc) atomicAdd(out, acc);
 }
 
-int64_t traj16_frac() {  // AB: 256ths of a rank's slots traced 16 lanes per ray (RFRT_TRAJ16)
-  static const int64_t v = [] {
-    const char* e = getenv("RFRT_TRAJ16");
-    return e ? (int64_t)atoll(e) : (int64_t)0;
-  }();
-  return v;
-}
-// BVH trajectories of at most this many rays run four lanes per ray (RFRT_TRAJ_SPLIT_MAX, 0 = never)
+// BVH trajectories of at most this many rays run 16 / 4 lanes per ray (RFRT_TRAJ_SPLIT_MAX, 0 = never)
 int64_t traj_split_max_rays() {
   static const int64_t v = [] {
     const char* e = getenv("RFRT_TRAJ_SPLIT_MAX");
@@ -3222,17 +3215,12 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
     }
     p.order = c->ray_order;
     prof_mark(c, 0, s);
-    const int64_t f16 = traj16_frac();
-    if (c->n <= traj_split_max_rays() && f16 > 0) {
-      const int64_t n1 = std::min<int64_t>(c->n, c->n * f16 / 256);
-      const unsigned nb1 = (unsigned)std::max<int64_t>(1, (16 * n1 + 255) / 256);
+    if (c->n <= traj_split_max_rays()) {  // too few rays to fill the GPU: 16 / 4 lanes per ray
+      const int64_t n1 = c->n / kTrajWideShare;
+      const unsigned nb1 = (unsigned)std::max<int64_t>(1, (kTrajSplitWide * n1 + 255) / 256);
       const unsigned nb2 = (unsigned)std::max<int64_t>(1, (kTrajSplitG * (c->n - n1) + 255) / 256);
-      hipLaunchKernelGGL((k_traj_split2<16, kTrajSplitG>), dim3(nb1 + nb2), dim3(256), 0, s, p, n1, nb1);
-    } else if (c->n <= traj_split_max_rays())  // too few rays to fill the GPU: four lanes per ray
-      hipLaunchKernelGGL(k_traj_split<kTrajSplitG>,
-                         dim3((unsigned)std::min<int64_t>((kTrajSplitG * c->n + 255) / 256, 8192)), dim3(256), 0,
-                         s, p);
-    else
+      hipLaunchKernelGGL((k_traj_split<kTrajSplitWide, kTrajSplitG>), dim3(nb1 + nb2), dim3(256), 0, s, p, n1, nb1);
+    } else
       hipLaunchKernelGGL(k_traj<true>, dim3(grid_rays), dim3(256), lds, s, p);
     prof_mark(c, 1, s);
     p.order = nullptr;
