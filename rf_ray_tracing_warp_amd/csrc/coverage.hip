@@ -3253,10 +3253,16 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
   p.cell_bits = kb.cell;
   int64_t ncand = 0, nrec = 0, nlist = 0;
   const unsigned grid_items = 4096;
-  // k_cols' slot-group stride: coprime to the group count, so that a block's 16 groups spread over the burst
+  // k_cols' slot-group stride: coprime to the group count, so that a block's 16 groups spread over
+  // a rank-sized burst (one round of blocks, where the heavy blocks would set the time); a whole map
+  // keeps its slots in order (stride 1: many rounds of blocks balance it, and the scattered
+  // trajectory reads cost more -- one-GPU maps 62 -> 70 us with the stride, r6z)
   const int64_t col_groups = std::max<int64_t>(1, (c->n + kColGroup - 1) / kColGroup);
-  int64_t col_step = std::max<int64_t>(1, col_groups / 16);
-  while (std::gcd(col_step, col_groups) != 1) ++col_step;
+  int64_t col_step = 1;
+  if (c->n <= traj_split_max_rays()) {
+    col_step = std::max<int64_t>(1, col_groups / 16);
+    while (std::gcd(col_step, col_groups) != 1) ++col_step;
+  }
   // Replay launched before the list length reaches the host (early replay): the kernels read it
   // from the device counter, so the host's counter read-back and its wake-up (~36 us per K3 rank
   // of 8, profiles/r3j_k3.timeline.txt) overlap the replay instead of idling the GPU.  Only for

@@ -31,7 +31,8 @@ KERNELS = {  # short name -> substring of the demangled rocprofv3 name
     "k_cells": "k_cells(",
     "k_cols": "k_cols(",
     "k_power": "k_power(",
-    "k_power_small": "k_power_small(",
+    "k_power_small<1>": "k_power_small<1>(",
+    "k_power_small<8>": "k_power_small<8>(",
     "k_fill_received": "k_fill_received(",
 }
 
