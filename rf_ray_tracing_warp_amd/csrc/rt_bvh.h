@@ -151,6 +151,9 @@ __device__ __forceinline__ WalkStack make_stack() {
 // About half the dependent node fetches of the binary walk per query.  (The top 85 or 192 wide
 // nodes staged in LDS per workgroup measured slower, 1575 / 1603 vs 1522 us on K4 with the same
 // row mapping: every wave of a direction-sorted burst reads the same top nodes, which L1/L2 serve.)
+// (Sorting packed keys instead -- the entry t's bits with the slot in the low 2 bits, two min/max
+// per compare-exchange -- was bit-identical and slower: K4 rt_trace 731-735 vs 714-719 us, the
+// slot decode and extra selects outweighing the cheaper exchanges; profiles/r6za_*, round 6.)
 __device__ __forceinline__ void cas(float& ta, int& ra, float& tb, int& rb) {
   const bool sw = tb < ta;
   const float t0 = sw ? tb : ta, t1 = sw ? ta : tb;
