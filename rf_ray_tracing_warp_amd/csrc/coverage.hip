@@ -1250,7 +1250,7 @@ __global__ __launch_bounds__(256) void k_sel_scatter(const uint8_t* flag, const 
                                                      const int32_t* counts, const uint64_t* keys, const float* trx,
                                                      const uint32_t* gmask, ReplayItem* items,
                                                      unsigned long long* nlist, int B, uint16_t* okey,
-                                                     int32_t* oval) {
+                                                     int32_t* oval, unsigned long long* host_cnt) {
   __shared__ int s4[4];
   __shared__ int w4[4];
   const int64_t n = cand_count(n_dev, cap), tile = sel_tile(n, gridDim.x);
@@ -1258,7 +1258,16 @@ __global__ __launch_bounds__(256) void k_sel_scatter(const uint8_t* flag, const 
   int before = 0;
   for (int j = threadIdx.x; j < (int)blockIdx.x; j += blockDim.x) before += counts[j];
   int64_t base = block_sum(before, s4);
-  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *nlist = (unsigned long long)(base + counts[blockIdx.x]);
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
+    const unsigned long long nl = (unsigned long long)(base + counts[blockIdx.x]);
+    *nlist = nl;
+    // the host's copy of the candidate, item and list counts, in pinned (coherent) memory: one
+    // store each instead of a copy launch after this kernel
+    host_cnt[0] = n_dev[0];
+    host_cnt[1] = n_dev[1];
+    host_cnt[2] = nl;
+    __threadfence_system();
+  }
   const int wave = threadIdx.x >> 6;
   for (int64_t i0 = lo; i0 < hi; i0 += blockDim.x) {  // block-uniform
     const int64_t i = i0 + threadIdx.x;
@@ -2109,7 +2118,9 @@ struct rt_coverage {
   bool profile = false;
   hipEvent_t pev[8] = {};
   unsigned long long* hcnt = nullptr;  // pinned copy of counters[0..2] (the candidate stage's read-back)
+  unsigned long long* hcnt_dev = nullptr;  // the same words as the kernels address them
   int64_t* hbounds = nullptr;          // pinned (ray mode): the trace stage's owner bounds [world + 1], then the look-back error count
+  int64_t* hbounds_dev = nullptr;
   hipEvent_t ev_cnt = nullptr;         // recorded after that copy
   bool ev_rec[8] = {};
   unsigned long long* work = nullptr;
@@ -2758,8 +2769,14 @@ __global__ __launch_bounds__(256) void k_send_runs(SendRuns a) {
 }
 
 // send counts from the owner bounds (rt_coverage_trace_rows_async: they stay on the device)
-__global__ __launch_bounds__(64) void k_bounds_to_counts(const int64_t* bounds, int world, int64_t* counts) {
+// the send counts on the device, and the owner bounds plus the look-back error word into the
+// plan's pinned (coherent) host words -- stores instead of two copy launches
+__global__ __launch_bounds__(64) void k_bounds_to_counts(const int64_t* bounds, int world, int64_t* counts,
+                                                         int64_t* host_bounds, const uint64_t* err) {
   for (int o = threadIdx.x; o < world; o += blockDim.x) counts[o] = bounds[o + 1] - bounds[o];
+  for (int o = threadIdx.x; o <= world; o += blockDim.x) host_bounds[o] = bounds[o];
+  if (threadIdx.x == 0) host_bounds[world + 1] = (int64_t)*err;
+  __threadfence_system();
 }
 
 __global__ __launch_bounds__(256) void k_amps_to_fx(const double* amps, int64_t n, Fx192* sums) {
@@ -3347,12 +3364,12 @@ int cov_records(rt_coverage* c, const float* tx_pos, double tx_power, double lig
                          c->cap, tiles);
       hipLaunchKernelGGL(k_sel_scatter, dim3(G), dim3(256), 0, s, c->first_flag,
                          (const unsigned long long*)c->counters, c->cap, tiles, c->keys, c->trx, c->gmask, c->ritems,
-                         c->counters + 2, p.B, pre_keys ? rord().k_in : nullptr, pre_keys ? rord().v_in : nullptr);
+                         c->counters + 2, p.B, pre_keys ? rord().k_in : nullptr, pre_keys ? rord().v_in : nullptr,
+                         c->hcnt_dev);
     }
     RT_HIP(hipGetLastError());
-    // the counters go to pinned memory ahead of the replay, and the host waits for that copy only;
-    // the list holds at most cap entries (one per candidate)
-    RT_HIP(hipMemcpyAsync(c->hcnt, c->counters, 24, hipMemcpyDeviceToHost, s));
+    // k_sel_scatter wrote the counters to pinned memory ahead of the replay, and the host waits for
+    // that kernel only; the list holds at most cap entries (one per candidate)
     RT_HIP(hipEventRecord(c->ev_cnt, s));
     // early (windowed) replay only for rank plans of a ray-sharded map, whose lists are a rank's
     // share: a one-GPU or cell-sharded plan's whole-map list takes the device-wide sort,
@@ -3564,7 +3581,8 @@ int rt_coverage_create(int device, const rt_mesh* env, int max_bounces, int64_t 
   if (e == hipSuccess) e = hipMemset(c->cepoch, 0, sizeof(int32_t) * nc);  // epochs start at 1
   if (e == hipSuccess) e = hipMalloc(&c->own_aux, 16);
   if (e == hipSuccess) e = hipMemset(c->own_aux, 0, 16);
-  if (e == hipSuccess) e = hipHostMalloc((void**)&c->hcnt, 32, hipHostMallocDefault);
+  if (e == hipSuccess) e = hipHostMalloc((void**)&c->hcnt, 32, hipHostMallocCoherent);
+  if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&c->hcnt_dev, c->hcnt, 0);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_cnt, hipEventDisableTiming);
   if (e != hipSuccess) {
     rt_coverage_destroy(c);
@@ -3661,7 +3679,8 @@ int rt_coverage_create_rays(int device, const rt_mesh* env, int max_bounces, int
   c->n_total = n_rays_total;
   c->ray_mode = true;
   if (hipMalloc(&c->bounds, sizeof(int64_t) * (world + 1)) != hipSuccess ||
-      hipHostMalloc((void**)&c->hbounds, sizeof(int64_t) * (world + 2), hipHostMallocDefault) != hipSuccess) {
+      hipHostMalloc((void**)&c->hbounds, sizeof(int64_t) * (world + 2), hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&c->hbounds_dev, c->hbounds, 0) != hipSuccess) {
     rt_coverage_destroy(c);
     return rt::hip_fail(hipErrorOutOfMemory, "rt_coverage_create_rays");
   }
@@ -3755,12 +3774,12 @@ int trace_rows_impl(rt_coverage* c, const float* tx_pos, double tx_power, double
     hipLaunchKernelGGL(k_send_runs, dim3((unsigned)ntiles), dim3(256), 0, s, a);
     RT_HIP(hipGetLastError());
     prof_mark(c, 7, s);
-    // both into pinned memory (a pageable copy stages through the host: ~20 us of gap per rank),
-    // the bounds and the count of look-back waits that gave up (k_send_runs here, k_owner_runs of
-    // an earlier owner stage): their sums would be wrong, so the run fails instead
-    RT_HIP(hipMemcpyAsync(c->hbounds, c->bounds, sizeof(int64_t) * (world + 1), hipMemcpyDeviceToHost, s));
-    RT_HIP(hipMemcpyAsync(c->hbounds + world + 1, c->own_aux + 1, 8, hipMemcpyDeviceToHost, s));
-    hipLaunchKernelGGL(k_bounds_to_counts, dim3(1), dim3(64), 0, s, c->bounds, world, counts_dev);
+    // into pinned memory by k_bounds_to_counts (a pageable copy stages through the host: ~20 us of
+    // gap per rank; two copy launches ~10 us): the bounds and the count of look-back waits that gave
+    // up (k_send_runs here, k_owner_runs of an earlier owner stage), whose sums would be wrong, so
+    // the run fails instead
+    hipLaunchKernelGGL(k_bounds_to_counts, dim3(1), dim3(64), 0, s, c->bounds, world, counts_dev, c->hbounds_dev,
+                       (const uint64_t*)(c->own_aux + 1));
   } else {
     for (int o = 0; o <= world + 1; ++o) c->hbounds[o] = 0;  // nothing sent (no copy in flight)
     RT_HIP(hipMemsetAsync(counts_dev, 0, sizeof(int64_t) * world, s));
