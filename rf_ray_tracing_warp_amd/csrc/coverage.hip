@@ -764,18 +764,35 @@ __device__ __forceinline__ unsigned column_cells(const CovParams& p, uint64_t it
 // output range; only items with more than kCellBuf candidates run the geometry a second time.
 constexpr int kCellBuf = 8;  // 16 KB of LDS per block instead of 32 (r2zj: candidates stage 0.640 -> 0.636 ms on K3, 0.49 -> 0.48 on K5)
 
+// Items per thread between two appends: every append is one atomic on the device-wide candidate
+// counter, and same-address atomics serialize (~10 ns each): one item per thread made k_cells a
+// chain of ~35k appends on a whole map (K3 map 426 us, K5 314 us; ranks 59 / 45 us).  Four items
+// per thread on whole maps (K3 185, K5 188 us), two on a rank's ~1M items (K3 35, K5 30 us: four
+// left too few blocks for a rank's items; r6ze).  Eight were slower (K3 map 305 us: the thread's
+// LDS slots overflow, and the overflowing items run their geometry twice).
+constexpr int kCellsQMax = 4;
+constexpr int64_t kCellsQ4Items = 4 << 20;  // column items from which four per thread
 __global__ __launch_bounds__(256) void k_cells(CovParams p) {
   __shared__ uint64_t sbuf[kCellBuf][256];
   const int64_t nitems = (int64_t)min(*p.item_count, (unsigned long long)p.item_cap);
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int qn = nitems >= kCellsQ4Items ? 4 : 2;  // grid-uniform
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * qn;
   const int tid = threadIdx.x;
-  for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < nitems; base += stride) {
-    const int64_t i = base + tid;
-    const bool active = i < nitems;
-    const uint64_t item = active ? p.items[i] : 0;
-    const unsigned c = active ? column_cells(p, item, [&](unsigned j, uint64_t key) {
-      if (j < kCellBuf) sbuf[j][tid] = key;
-    }) : 0;
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x * qn; base < nitems; base += stride) {
+    uint64_t item[kCellsQMax];
+    unsigned cq[kCellsQMax];
+    unsigned c = 0;
+#pragma unroll
+    for (int q = 0; q < kCellsQMax; ++q) {
+      const int64_t i = base + q * 256 + tid;
+      const bool active = q < qn && i < nitems;
+      item[q] = active ? p.items[i] : 0;
+      const unsigned c0 = c;
+      cq[q] = active ? column_cells(p, item[q], [&](unsigned j, uint64_t key) {
+        if (c0 + j < (unsigned)kCellBuf) sbuf[c0 + j][tid] = key;
+      }) : 0;
+      c += cq[q];
+    }
     unsigned pre;
     const unsigned long long at = block_append(p.count, c, pre);
     if (c && (int64_t)(at + pre + c) <= p.cap) {
@@ -783,7 +800,12 @@ __global__ __launch_bounds__(256) void k_cells(CovParams p) {
       if (c <= (unsigned)kCellBuf) {
         for (unsigned j = 0; j < c; ++j) dst[j] = sbuf[j][tid];
       } else {
-        column_cells(p, item, [&](unsigned j, uint64_t key) { dst[j] = key; });
+        unsigned off = 0;
+#pragma unroll
+        for (int q = 0; q < kCellsQMax; ++q) {
+          if (cq[q]) column_cells(p, item[q], [&](unsigned j, uint64_t key) { dst[off + j] = key; });
+          off += cq[q];
+        }
       }
     }
   }
