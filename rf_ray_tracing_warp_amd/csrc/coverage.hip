@@ -2554,7 +2554,7 @@ __global__ __launch_bounds__(256) void k_owner_runs(OwnerRuns a) {
 
 // ---- Trace-stage reduce in one launch: the sorted replay records of a ray-sharded
 // rank -> its unique (owner, cell, bin) keys with their exact sums, the send rows and the owner
-// bounds.  Tiles of kSendTile records in ticket order; each thread holds 4 consecutive records.  A
+// bounds.  Tiles of kSendTile records in ticket order; each thread holds kSendItems consecutive records.  A
 // run of equal keys may be any length (a K3 rank's transmitter cell: ~125k records in one bin), so
 // the sums are a segmented scan: per tile its head count and its segmented tail (the sum after its
 // last head, or of the whole tile if it has none), combined across tiles by decoupled look-back --
@@ -2566,8 +2566,10 @@ __global__ __launch_bounds__(256) void k_owner_runs(OwnerRuns a) {
 // record: key, exact sum, f64, its row (packed 32 B or key + sum) and, at owner changes, the bounds.
 // Replaces k_tile_heads, k_tile_sums, k_cross_tiles and k_bounds_strip (four launches, ~50 us per
 // rank of 8, profiles/r4h_k5.timeline.txt).  Integer sums: the same bits in any grouping.
-constexpr int kSendItems = 4, kSendTile = 256 * kSendItems;
-static_assert(kSendTile == kOwnTile, "k_send_runs shares k_owner_runs' tile states");
+// 8 records per thread (k_owner_runs keeps 4): K3 rank of 8 48 -> 38 us, K5 46 -> 42 us; 8 for the
+// owner stage too was slower there (K3 21 -> 35 us), 2 here 70 us (r6zh)
+constexpr int kSendItems = 8, kSendTile = 256 * kSendItems;
+static_assert(kSendTile >= kOwnTile, "k_send_runs uses k_owner_runs' tile states (sized per kOwnTile)");
 constexpr uint64_t kSendHead = 1ull << 37, kSendCount = (1ull << 37) - 1;
 struct SegFx {  // segmented sum of a stretch of records: h = it holds a head, t = the sum after its last head
   bool h;
