@@ -20,6 +20,9 @@ def main():
     from rf_ray_tracing_warp_amd._lib import DeviceMesh
     from rf_ray_tracing_warp_amd.coverage import Coverage, CoverageGrid
     from rf_ray_tracing_warp_amd.mesh import load_stl, synthetic_terrain
+    if os.environ.get("REPLAY_WINDOW_MAX"):  # A/B: rank lists above this length take the device-wide sort
+        from rf_ray_tracing_warp_amd._lib import lib
+        lib().rt_debug_replay_window_max(int(os.environ["REPLAY_WINDOW_MAX"]))
     cases = os.environ.get("CASES", "k3,k5").split(",")
     shards = [int(s) for s in os.environ.get("SHARDS", "1,8").split(",")]
     reps = int(os.environ.get("REPS", "3"))
