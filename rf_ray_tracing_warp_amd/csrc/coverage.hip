@@ -1694,8 +1694,11 @@ __global__ __launch_bounds__(256) void k_cell_ranges(const uint64_t* ukeys, cons
 }
 
 constexpr int kPowLds = 192;  // terms per wave staged in LDS (3 per lane); larger cells read global memory
-constexpr int kPowSmall = 16;  // cells with at most this many terms: k_power_small
-constexpr int kPowGroup = 8;   // lanes per such cell when a plan owns few cells (4 and 16 measured no better, r6q)
+constexpr int kPowSmall = 16;  // cells with at most this many terms: k_power_small (one thread each, large maps)
+// Small maps: kPowGroup lanes per cell for cells of at most kPowGroupMax terms.  K3 map / rank of 8,
+// k_power_small + k_power (us): 8 lanes up to 16 terms 60 + 103 / 19 + 22; 16 lanes up to 32 terms
+// 62 + 54 / 19 + 14; 16 up to 64 89 + 17 / 27 + 15; 8 up to 32 75 + 54 / 25 + 14 (r6zo)
+constexpr int kPowGroup = 16, kPowGroupMax = 32;
 constexpr int64_t kPowGroupMaxCells = 131072;  // maps of at most this many cells (the map's, not a shard's)
 // (Copying each thread's terms into its LDS column first measured K3 rank 37 -> 33 us but K5 rank
 // 42 -> 65 us -- 53 KB of LDS, 3 waves per CU; r3f.  Removed in round 5.)
@@ -1719,8 +1722,8 @@ __device__ __forceinline__ double interval_sq(double Pv, double Qv, int64_t L, d
   return Pv * Pv * (0.5 * ((double)L - D)) + Qv * Qv * (0.5 * ((double)L + D)) + 2.0 * Pv * Qv * (0.5 * E);
 }
 
-// Cells of ours with 0..kPowSmall terms, G lanes per cell (kPowGroup for maps of at most
-// kPowGroupMaxCells cells; G = 1 is the serial sweep of power_sparse).  G > 1: the cell's terms are staged in the wave's LDS with compensated
+// Cells of ours with 0..KMAX terms, G lanes per cell (kPowGroup lanes up to kPowGroupMax terms for
+// maps of at most kPowGroupMaxCells cells; G = 1 is the serial sweep of power_sparse up to kPowSmall).  G > 1: the cell's terms are staged in the wave's LDS with compensated
 // (double-double) prefix sums of a cos / a sin, and each lane closes the intervals that start at its
 // events, as k_power does for larger cells -- equal to the serial sweep up to the order of summation.
 // (One thread per cell made the kernel as long as one thread's chain of up to 2 x 16 intervals, each
@@ -1728,17 +1731,17 @@ __device__ __forceinline__ double interval_sq(double Pv, double Qv, int64_t L, d
 // Larger cells are listed (big[], count in *nbig; one atomic per wave) for k_power, which then
 // visits only them (it used to stride over every cell of the map to skip the small ones: 1M cell
 // ranges read per K5 map for a few thousand large cells).
-template <int G>
+template <int G, int KMAX = kPowSmall>
 __global__ __launch_bounds__(64) void k_power_small(TermArrays T, const int32_t* cstart, const int32_t* cend,
                                                      const int32_t* cepoch, int32_t epoch, rt_grid g, int shard,
                                                      int nshard, PowerParams P, double* power, int32_t* big,
                                                      unsigned* nbig) {
   static_assert(G == 1 || G == 4 || G == 8 || G == 16, "1, 4, 8 or 16 lanes per cell");
-  constexpr int NG = 64 / G, TP = (kPowSmall + G - 1) / G;  // cells per wave, terms per lane
-  __shared__ int32_t s_st[NG][kPowSmall], s_e1[NG][kPowSmall], s_m[NG][kPowSmall];
-  __shared__ double s_pch[NG][kPowSmall + 1], s_pcl[NG][kPowSmall + 1], s_psh[NG][kPowSmall + 1],
-      s_psl[NG][kPowSmall + 1];
-  __shared__ double s_ev[NG][4 * kPowSmall];
+  constexpr int NG = 64 / G, TP = (KMAX + G - 1) / G;  // cells per wave, terms per lane
+  constexpr int KL = G > 1 ? KMAX : 1;                // LDS slots per cell (the serial form has none)
+  __shared__ int32_t s_st[NG][KL], s_e1[NG][KL], s_m[NG][KL];
+  __shared__ double s_pch[NG][KL + 1], s_pcl[NG][KL + 1], s_psh[NG][KL + 1], s_psl[NG][KL + 1];
+  __shared__ double s_ev[NG][4 * KL];
   const int64_t nxo = g.nx > shard ? (g.nx - shard + nshard - 1) / nshard : 0;
   const int64_t nown = nxo * g.ny * g.nz;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -1769,7 +1772,7 @@ __global__ __launch_bounds__(64) void k_power_small(TermArrays T, const int32_t*
       const bool has = cepoch[c] == epoch;
       lo = has ? cstart[c] : 0;
       hi = has ? cend[c] : 0;
-      small = hi - lo <= kPowSmall;
+      small = hi - lo <= KMAX;
       is_big = !small;
     }
     const uint64_t m = __ballot(is_big && j == 0);
@@ -2105,7 +2108,7 @@ struct rt_coverage {
   int32_t *cstart = nullptr, *cend = nullptr;  // per cell: its run in the unique keys
   int32_t* cepoch = nullptr;                   // per cell: the run (range_epoch) that wrote cstart/cend
   int32_t range_epoch = 0;
-  int32_t* bigcells = nullptr;  // per cell slot: the cells k_power sweeps (more than kPowSmall terms)
+  int32_t* bigcells = nullptr;  // per cell slot: the cells k_power sweeps (more terms than k_power_small takes)
   int32_t* runs = nullptr;  // exact run sums: [cap] head flags, [cap] their scan, [cap] run starts, [64] counters
   // k_owner_runs' look-back: [cap / kOwnTile + 1] state words, [ticket counter, error count]; host:
   // tickets issued so far, the call's tag
@@ -3528,7 +3531,7 @@ int cov_power(rt_coverage* c, int64_t nrec, int64_t n_bins, double alpha, double
   // so a sharded map's few thousand cells must still spread over every CU
   const unsigned grid_small = (unsigned)std::min<int64_t>((ncell / c->nshard + 64) / 64, 16384);
   const TermArrays terms{c->ukeys, c->tcos, c->tsin, c->ev};
-  // cells with more than kPowSmall terms, listed by k_power_small for k_power (count reset by k_cell_ranges)
+  // cells with more terms than k_power_small takes, listed by it for k_power (count reset by k_cell_ranges)
   int32_t* big = c->bigcells;
   unsigned* nbig = reinterpret_cast<unsigned*>(c->runs + 3 * c->cap + 1);
   if (!ranges_done) {
@@ -3548,7 +3551,7 @@ int cov_power(rt_coverage* c, int64_t nrec, int64_t n_bins, double alpha, double
   // r6r).  The choice depends on the map, never on the shard, so that every cell's power is summed
   // in the same order whoever owns it (a sharded map equals the whole map bit for bit).
   if (ncell <= kPowGroupMaxCells)
-    hipLaunchKernelGGL(k_power_small<kPowGroup>, dim3(std::min<int64_t>((int64_t)grid_small * kPowGroup, 65536)),
+    hipLaunchKernelGGL((k_power_small<kPowGroup, kPowGroupMax>), dim3(std::min<int64_t>((int64_t)grid_small * kPowGroup, 65536)),
                        dim3(64), 0, s, terms, c->cstart, c->cend, c->cepoch, epoch, c->grid, c->shard, c->nshard, P,
                        power, big, nbig);
   else
