@@ -33,6 +33,7 @@ KERNELS = {  # short name -> substring of the demangled rocprofv3 name
     "k_power": "k_power(",
     "k_power_small<1>": "k_power_small<1>(",
     "k_power_small<8>": "k_power_small<8>(",
+    "k_power_small<16,32>": "k_power_small<16, 32>(",
     "k_fill_received": "k_fill_received(",
 }
 
